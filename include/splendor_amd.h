@@ -1,0 +1,138 @@
+/*
+ * splendor_amd.h — C-ABI of the MI355X (gfx950) Splendor rollout engine.
+ *
+ * The reference has no FFI: its hot path is the Python functions below, called per table.
+ * Each entry point here replaces one of them for a whole batch of tables living in HBM:
+ *
+ *   spl_ctx_create     engine/state.py:113-178 (_load_cards_from_json/_load_nobles_from_json,
+ *                      re-parsed on every reset in the reference) -> constant tables uploaded
+ *                      once; also builds the token-return RNG table (engine/rules.py:170-176)
+ *   spl_reset          envs/splendor_env.py:41-48 SplendorEnv.reset -> engine/state.py:181-211
+ *                      initial_state (CPython MT19937 shuffles on device)
+ *   spl_step           envs/splendor_env.py:51-90 SplendorEnv.step = rules.py:40-93 legal_moves,
+ *                      :196-287 apply_action, encode.py:124-187 encode_observation, reward /
+ *                      termination, plus gymnasium-0.29 SyncVectorEnv same-step autoreset
+ *   spl_encode         engine/encode.py:124-187 encode_observation (current state)
+ *   spl_legal          engine/rules.py:40-93 legal_moves (current state)
+ *   spl_sample_uniform scripts/random_rollout.py:23 / wrappers/dual_step_native.py:215-223
+ *                      random_opponent (uniform over legal; Philox stream, not numpy's)
+ *   spl_table_download / spl_table_upload
+ *                      the reference's direct `env.state` access (tests/utils.py:25-53 mutate
+ *                      it in place) -> host view spl_table_t (splendor_table.h)
+ *
+ * Conventions
+ *  - Every buffer is caller-owned device memory (e.g. a PyTorch-ROCm tensor) passed as a raw
+ *    pointer; the library owns only the constant tables inside spl_ctx_t.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream).  Calls are asynchronous
+ *    on that stream except spl_ctx_create/destroy and the table download/upload helpers.
+ *  - Return value: 0 on success, negative SPL_E_* on a host-side argument error (nothing was
+ *    launched); spl_last_error() describes it.  Per-table conditions are reported in `flags`.
+ *  - Not re-entrant per arena: one host thread drives one arena.
+ */
+#ifndef SPLENDOR_AMD_H
+#define SPLENDOR_AMD_H
+
+#include <stdint.h>
+
+#include "splendor_table.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPL_ABI_VERSION 1
+
+/* ---- per-table flag bits (uint8) --------------------------------------------------- */
+#define SPL_F_ILLEGAL 0x01        /* info["illegal_action"]      envs/splendor_env.py:64-66 */
+#define SPL_F_DRAW 0x02           /* info["draw"] (no legal move) envs/splendor_env.py:56-61 */
+#define SPL_F_TURN_LIMIT 0x04     /* info["turn_limit"]          envs/splendor_env.py:82-83 */
+#define SPL_F_AFTER_TERMINAL 0x08 /* reference raises RuntimeError envs/splendor_env.py:53-54 */
+#define SPL_F_OOB 0x10            /* reference raises ValueError  envs/splendor_env.py:62-63 */
+#define SPL_F_RESET 0x20          /* autoreset: obs/mask describe the freshly dealt table   */
+#define SPL_F_RNG_LIMIT 0x40      /* a deal needed more MT outputs than the device streams; */
+                                  /* never observed, reported instead of guessed */
+
+/* ---- error codes -------------------------------------------------------------------- */
+#define SPL_OK 0
+#define SPL_E_ARG -1      /* bad argument (null pointer, size, player count) */
+#define SPL_E_HIP -2      /* HIP runtime error */
+#define SPL_E_RANGE -3    /* host view out of the device's representable range */
+
+typedef struct spl_ctx_s spl_ctx_t;
+
+/* Device arena descriptor (host memory, owned by the caller).  `base` points at caller-owned
+ * device memory of at least spl_arena_bytes(n, players) bytes, 256-byte aligned. */
+typedef struct spl_arena_s {
+    void *base;
+    int64_t bytes;
+    int32_t n;            /* tables */
+    int32_t players;      /* 2..4 */
+    int64_t steps;        /* maintained by the library: spl_step calls since the last reset */
+} spl_arena_t;
+
+/* Batched step arguments (all device pointers; [n] = one entry per table). */
+typedef struct spl_step_args_s {
+    const int32_t *actions;  /* [n] action per table (0..44 legal range)                    */
+    int32_t *obs;            /* [n][297] observation after the step (reset obs on SPL_F_RESET) */
+    int8_t *mask;            /* [n][45]  action mask after the step                          */
+    float *reward;           /* [n]      reward of the mover                                 */
+    uint8_t *terminated;     /* [n]                                                          */
+    uint8_t *flags;          /* [n]      SPL_F_* bits                                        */
+    int8_t *winner;          /* [n] or NULL: winner of the state the step produced (−1 None) */
+    int32_t *final_obs;      /* [n][297] or NULL: terminal obs, written on SPL_F_RESET rows  */
+    int32_t autoreset;       /* 1: terminated tables are re-dealt in the same step          */
+    int32_t *next_actions;   /* [n] or NULL: fused uniform-random policy over the new mask   */
+    uint64_t policy_seed;    /* Philox key for next_actions                                  */
+    uint64_t ply;            /* Philox counter for next_actions                              */
+    int64_t table0;          /* global id of table 0 (sharding: streams keyed by global id) */
+    float *ep_return;        /* [n] or NULL: += final reward of player 0 on termination      */
+    uint32_t *ep_count;      /* [n] or NULL: += 1 on termination                             */
+} spl_step_args_t;
+
+int spl_abi_version(void);
+const char *spl_last_error(void);
+
+/* cards: 90 x 8 int32 [tier, bonus colour, points, cost w,b,g,r,k];
+ * nobles: 10 x 6 int32 [req w,b,g,r,k, points]   (splendor_gym/engine/data/tables.json) */
+int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_ctx_t **out);
+int spl_ctx_destroy(spl_ctx_t *ctx);
+/* Pool refill period in steps (default 8); 0 disables automatic refills (inline deals). */
+int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period);
+
+int64_t spl_arena_bytes(int32_t n, int32_t players);
+
+/* Reset tables.  pcg (device, nullable): 4 x uint64 per table = numpy PCG64 state
+ * (state_hi, state_lo, inc_hi, inc_lo) of the table's gymnasium np_random after seeding; when
+ * given, the table's engine-seed stream restarts from it (reset(seed=...)); when NULL the
+ * stream continues (reset() without a seed).  reset_mask (device, nullable): tables with a
+ * non-zero byte are reset, NULL = all.  obs/mask (nullable) receive every table's current
+ * observation / action mask after the reset. */
+int spl_reset(spl_ctx_t *ctx, spl_arena_t *arena, const uint64_t *pcg, const uint8_t *reset_mask,
+              int32_t *obs, int8_t *mask, void *stream);
+
+int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *args, void *stream);
+
+/* Pool maintenance: deal the next episode of every table whose pool slot was consumed. */
+int spl_refill(spl_ctx_t *ctx, spl_arena_t *arena, void *stream);
+
+int spl_encode(spl_ctx_t *ctx, spl_arena_t *arena, int32_t *obs, void *stream);
+int spl_legal(spl_ctx_t *ctx, spl_arena_t *arena, int8_t *mask, void *stream);
+
+/* Uniform-random legal action per table from a [n][45] int8 mask (0 if none is legal). */
+int spl_sample_uniform(spl_ctx_t *ctx, int32_t n, const int8_t *mask, int32_t *actions,
+                       uint64_t seed, uint64_t ply, int64_t table0, void *stream);
+
+/* Host-view copies of `count` tables starting at `first` (synchronous on `stream`). */
+int spl_table_download(spl_ctx_t *ctx, spl_arena_t *arena, int32_t first, int32_t count,
+                       spl_table_t *host, void *stream);
+int spl_table_upload(spl_ctx_t *ctx, spl_arena_t *arena, int32_t first, int32_t count,
+                     const spl_table_t *host, void *stream);
+
+/* Copy of the token-return RNG table (spl_ctx_create builds it on device), for tests.
+ * Returns the number of uint32 words (4 per entry) when out == NULL. */
+int64_t spl_ctx_token_lut(spl_ctx_t *ctx, uint32_t *out, int64_t words);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPLENDOR_AMD_H */
