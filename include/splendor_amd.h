@@ -100,6 +100,8 @@ int spl_ctx_destroy(spl_ctx_t *ctx);
 int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period);
 
 int64_t spl_arena_bytes(int32_t n, int32_t players);
+/* Zero the arena (must precede the first spl_reset of a fresh allocation). */
+int spl_arena_init(spl_ctx_t *ctx, spl_arena_t *arena, void *stream);
 
 /* Reset tables.  pcg (device, nullable): 4 x uint64 per table = numpy PCG64 state
  * (state_hi, state_lo, inc_hi, inc_lo) of the table's gymnasium np_random after seeding; when

@@ -1,0 +1,1517 @@
+// spl_engine.hip — MI355X (gfx950) Splendor rollout engine: kernels + C-ABI.
+//
+// One wavefront lane = one table; a workgroup is ONE wave (64 tables) so small batches still
+// spread over all 256 CUs.  State lives in HBM as 32-bit word planes (spl_layout.h) and is
+// held in VGPRs for the whole step; branchy rules are predicated per lane (no MFMA: this is
+// small-integer work).  Observations are staged in LDS as bytes (every value <= 255 except
+// move_count, patched separately) and leave the CU as coalesced 16-byte int32x4 stores; masks
+// leave as packed bytes built from per-lane 45-bit words in LDS.
+//
+// Reference semantics restated here (paths relative to the reference root):
+//   engine/rules.py:40-93 legal_moves, :101-122 _pay_for_card, :125-129 _refill_slot,
+//   :132-147 _grant_noble_if_applicable, :150-193 auto_return_tokens/_enforce_token_limit,
+//   :196-287 apply_action, :290-312 compute_winner/is_terminal; engine/state.py:61-71
+//   can_afford, :181-211 initial_state; engine/encode.py:124-187 encode_observation;
+//   envs/splendor_env.py:41-115 reset/step/get_final_rewards.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/splendor_amd.h"
+#include "spl_layout.h"
+#include "spl_rng.h"
+
+namespace spl {
+
+// ------------------------------------------------------------------------------------------
+// kernel parameter blocks
+// ------------------------------------------------------------------------------------------
+struct KArena {
+    uint32_t *planes;
+    uint8_t *slots;
+    uint8_t *pcg;
+    uint32_t *needy;  // [0] = count, [1..n] = table ids
+    int n;
+};
+
+struct KTables {
+    const uint4 *cards;   // [90] {1,tier,points,oh_w | oh_b..oh_k | cost w,b,g,r | cost k,colour,0,0}
+    const uint2 *nobles;  // [10] {1,req w,b,g | req r,k,points,0}
+    const uint4 *lut;     // [kLutEntries] token-return MT outputs (top 3 bits, 10 per word)
+};
+
+struct KStep {
+    const int32_t *actions;
+    int32_t *obs;
+    int8_t *mask;
+    float *reward;
+    uint8_t *terminated;
+    uint8_t *flags;
+    int8_t *winner;
+    int32_t *final_obs;
+    int32_t *next_actions;
+    float *ep_return;
+    uint32_t *ep_count;
+    uint64_t policy_seed;
+    uint64_t ply;
+    int64_t table0;
+    int autoreset;
+};
+
+constexpr int kObsDim = 297;
+constexpr int kScratchStride = 112;  // per-lane deal scratch in LDS (16-aligned)
+
+struct __align__(16) BlockLDS {
+    uint4 cards[90];
+    uint2 nobles[10];
+    uint64_t mask[64];
+    uint8_t rows[64 * kObsDim];  // observation staging; also the deal scratch (64 x 112 B)
+};
+
+// ------------------------------------------------------------------------------------------
+// small helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bget(uint32_t w, int k) { return (w >> (8 * k)) & 0xFFu; }
+__device__ __forceinline__ uint32_t bset(uint32_t w, int k, uint32_t v) {
+    return (w & ~(0xFFu << (8 * k))) | ((v & 0xFFu) << (8 * k));
+}
+__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+
+// Launder a value through an empty asm so that a select chain over struct members stays a
+// select of VALUES: otherwise LLVM folds "c ? s.a : s.b" into a load at a selected offset,
+// which pins the whole struct in scratch memory.
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+    asm("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ int opaque(int x) {
+    asm("" : "+v"(x));
+    return x;
+}
+
+template <int P>
+struct Tab {
+    uint32_t sw[SW_COUNT];
+    uint32_t pw[P][4];
+};
+
+struct Pl {
+    int tok[6], bon[5], pres, nres, rev, res[3];
+};
+
+__device__ __forceinline__ Pl unpack_pl(const uint32_t w[4]) {
+    Pl p;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) p.tok[c] = (int)bget(w[0], c);
+    p.tok[4] = (int)bget(w[1], 0);
+    p.tok[5] = (int)bget(w[1], 1);
+    p.bon[0] = (int)bget(w[1], 2);
+    p.bon[1] = (int)bget(w[1], 3);
+    p.bon[2] = (int)bget(w[2], 0);
+    p.bon[3] = (int)bget(w[2], 1);
+    p.bon[4] = (int)bget(w[2], 2);
+    p.pres = (int)bget(w[2], 3);
+    p.nres = (int)(w[3] & 3u);
+    p.rev = (int)((w[3] >> 2) & 7u);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) p.res[i] = (int)bget(w[3], i + 1);
+    return p;
+}
+
+__device__ __forceinline__ void pack_pl(const Pl &p, uint32_t w[4]) {
+    w[0] = (uint32_t)p.tok[0] | ((uint32_t)p.tok[1] << 8) | ((uint32_t)p.tok[2] << 16) | ((uint32_t)p.tok[3] << 24);
+    w[1] = (uint32_t)p.tok[4] | ((uint32_t)p.tok[5] << 8) | ((uint32_t)p.bon[0] << 16) | ((uint32_t)p.bon[1] << 24);
+    w[2] = (uint32_t)p.bon[2] | ((uint32_t)p.bon[3] << 8) | ((uint32_t)p.bon[4] << 16) | ((uint32_t)p.pres << 24);
+    w[3] = ((uint32_t)p.nres & 3u) | (((uint32_t)p.rev & 7u) << 2) | (((uint32_t)p.res[0] & 0xFFu) << 8) |
+           (((uint32_t)p.res[1] & 0xFFu) << 16) | (((uint32_t)p.res[2] & 0xFFu) << 24);
+}
+
+template <int P>
+__device__ __forceinline__ void get_player(const Tab<P> &T, int p, uint32_t w[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t v = opaque(T.pw[0][k]);
+#pragma unroll
+        for (int q = 1; q < P; ++q) v = (p == q) ? opaque(T.pw[q][k]) : v;
+        w[k] = v;
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void put_player(Tab<P> &T, int p, const uint32_t w[4]) {
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) T.pw[q][k] = (p == q) ? w[k] : T.pw[q][k];
+}
+
+__device__ __forceinline__ void get_bank(const uint32_t *sw, int bank[6]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) bank[c] = (int)bget(sw[SW_BANK0], c);
+    bank[4] = (int)bget(sw[SW_BANK1], 0);
+    bank[5] = (int)bget(sw[SW_BANK1], 1);
+}
+
+__device__ __forceinline__ void put_bank(uint32_t *sw, const int bank[6]) {
+    sw[SW_BANK0] = (uint32_t)bank[0] | ((uint32_t)bank[1] << 8) | ((uint32_t)bank[2] << 16) | ((uint32_t)bank[3] << 24);
+    sw[SW_BANK1] = (sw[SW_BANK1] & 0xFFFF0000u) | (uint32_t)bank[4] | ((uint32_t)bank[5] << 8);
+}
+
+__device__ __forceinline__ int board_get(const uint32_t *sw, int k) {  // runtime k
+    const uint32_t b0 = opaque(sw[SW_BOARD]), b1 = opaque(sw[SW_BOARD + 1]), b2 = opaque(sw[SW_BOARD + 2]);
+    const uint32_t w = k < 4 ? b0 : (k < 8 ? b1 : b2);
+    return (int)bget(w, k & 3);
+}
+__device__ __forceinline__ void board_set(uint32_t *sw, int k, uint32_t v) {  // runtime k
+#pragma unroll
+    for (int t = 0; t < 3; ++t) sw[SW_BOARD + t] = (k >> 2) == t ? bset(sw[SW_BOARD + t], k & 3, v) : sw[SW_BOARD + t];
+}
+
+__device__ __forceinline__ uint4 card_rec(const BlockLDS &L, int id) { return L.cards[id < 90 ? id : 0]; }
+
+__device__ __forceinline__ int card_cost(uint4 rec, int c) { return c < 4 ? (int)bget(rec.z, c) : (int)bget(rec.w, 0); }
+
+// engine/state.py:61-71 can_afford
+__device__ __forceinline__ bool afford(const Pl &p, uint4 rec) {
+    int need = 0;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        const int d = max(card_cost(rec, c) - p.bon[c], 0);
+        need += max(d - p.tok[c], 0);
+    }
+    return p.tok[5] >= need;
+}
+
+// take-3 colour sets in itertools.combinations(range(5), 3) order (engine/encode.py:35)
+constexpr uint64_t kTake3Masks = (0x07ull) | (0x0Bull << 5) | (0x13ull << 10) | (0x0Dull << 15) |
+                                 (0x15ull << 20) | (0x19ull << 25) | (0x0Eull << 30) | (0x16ull << 35) |
+                                 (0x1Aull << 40) | (0x1Cull << 45);
+__device__ __forceinline__ uint32_t take3_mask(int i) { return (uint32_t)(kTake3Masks >> (5 * i)) & 31u; }
+
+// engine/rules.py:40-93 legal_moves -> 45-bit mask
+__device__ __forceinline__ uint64_t legal_mask(const uint32_t *sw, const Pl &p, const int bank[6], const BlockLDS &L) {
+    uint32_t avail = 0;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) avail |= (bank[c] >= 1 ? 1u : 0u) << c;
+    const int nav = __popc(avail);
+    uint64_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {  // :45-58 reduced take-3 rule
+        const uint32_t cm = take3_mask(i);
+        const bool ok = nav >= 3 ? ((cm & avail) == cm) : (nav >= 1 && (avail & cm) == avail);
+        m |= (uint64_t)ok << i;
+    }
+#pragma unroll
+    for (int c = 0; c < 5; ++c) m |= (uint64_t)(bank[c] >= 4) << (10 + c);  // :61-63
+    const bool can_res = p.nres < 3;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {  // :66-80
+        const int id = (int)bget(sw[SW_BOARD + k / 4], k % 4);
+        const bool present = id != 0xFF;
+        m |= (uint64_t)(present && afford(p, card_rec(L, id))) << (15 + k);
+        m |= (uint64_t)(present && can_res) << (27 + k);
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) m |= (uint64_t)(can_res && bget(sw[SW_DECK], t) > 0) << (39 + t);  // :83-86
+#pragma unroll
+    for (int i = 0; i < 3; ++i)  // :89-91
+        m |= (uint64_t)(i < p.nres && afford(p, card_rec(L, p.res[i]))) << (42 + i);
+    return m;
+}
+
+// engine/rules.py:101-122 _pay_for_card
+__device__ __forceinline__ void pay_for_card(Pl &p, int bank[6], uint4 rec) {
+    const int gold_avail = p.tok[5];
+    int gold_spent = 0;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        const int disc = max(card_cost(rec, c) - p.bon[c], 0);
+        const int spend = min(p.tok[c], disc);
+        p.tok[c] -= spend;
+        bank[c] += spend;
+        const int rem = disc - spend;
+        gold_spent += rem > 0 ? min(rem, gold_avail - gold_spent) : 0;
+    }
+    p.tok[5] -= gold_spent;
+    bank[5] += gold_spent;
+    const int colour = (int)bget(rec.w, 1);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) p.bon[c] += colour == c ? 1 : 0;
+    p.pres += (int)bget(rec.x, 2);
+}
+
+__device__ __forceinline__ uint8_t *slot_rec(const KArena &A, int t, int slot) {
+    return A.slots + ((size_t)t * 2 + slot) * kSlotBytes;
+}
+
+// engine/rules.py:125-129 _refill_slot / deck.pop(): top of tier t from the live record
+__device__ __forceinline__ uint32_t deck_pop(uint32_t *sw, const uint8_t *rec, int t) {
+    const int len = (int)bget(sw[SW_DECK], t);
+    if (len <= 0) return 0xFFu;
+    sw[SW_DECK] = bset(sw[SW_DECK], t, (uint32_t)(len - 1));
+    return rec[tier_base(t) + len - 1];
+}
+
+// pick the r-th colour (ascending) among non-gold colours the player holds
+__device__ __forceinline__ void return_one(Pl &p, int bank[6], int r) {
+    int seen = 0;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        const bool has = p.tok[c] > 0;
+        const bool hit = has && seen == r;
+        p.tok[c] -= hit ? 1 : 0;
+        bank[c] += hit ? 1 : 0;
+        seen += has ? 1 : 0;
+    }
+}
+
+__device__ __forceinline__ int non_gold_kinds(const Pl &p) {
+    int n = 0;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) n += p.tok[c] > 0 ? 1 : 0;
+    return n;
+}
+
+// engine/rules.py:150-185 auto_return_tokens on the full CPython MT stream (rare: seeds
+// outside the precomputed table, or a table entry that ran out of draws).
+__device__ __forceinline__ void token_return_mt(Pl &p, int bank[6], int remaining, uint64_t seed, uint32_t &flags) {
+    MTStream ms;
+    ms.init(seed);
+    bool done = false;
+    for (int j = 0;; ++j) {
+        const int nch = non_gold_kinds(p);
+        done = done || remaining <= 0 || nch == 0;
+        if (!__any(!done)) break;
+        if (j >= MTStream::kMaxOut) {
+            if (!done) flags |= SPL_F_RNG_LIMIT;
+            break;
+        }
+        const uint32_t y = ms.next(j);
+        if (!done) {
+            const int kb = bit_length((uint32_t)nch);
+            const int r = (int)(y >> (32 - kb));
+            if (r < nch) {  // rng.choice(choices) accepted
+                return_one(p, bank, r);
+                remaining -= 1;
+            }
+        }
+    }
+    if (remaining > 0 && p.tok[5] > 0) {
+        const int give = min(remaining, p.tok[5]);
+        p.tok[5] -= give;
+        bank[5] += give;
+    }
+}
+
+// engine/rules.py:188-193 _enforce_token_limit -> :150-185 auto_return_tokens
+__device__ __forceinline__ void enforce_token_limit(Pl &p, int bank[6], int turn_count, int to_play,
+                                                    const uint4 *lut, uint32_t &flags) {
+    int total = 0, bank_total = 0;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) total += p.tok[c];
+    if (total <= 10) return;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) bank_total += bank[c];
+    const bool in_lut = turn_count < kLutTc && to_play < kLutTp && total <= 13 && bank_total < kLutSb;
+    bool need_mt = !in_lut;
+    if (in_lut) {
+        const uint4 e = lut[((turn_count * kLutTp + to_play) * kLutSt + (total - 11)) * kLutSb + bank_total];
+        Pl p2 = p;
+        int bank2[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) bank2[c] = bank[c];
+        int remaining = total - 10, pos = 0, word = 0, sub = 0;
+        bool ok = true;
+        while (remaining > 0) {
+            const int nch = non_gold_kinds(p2);
+            if (nch == 0) break;
+            const int kb = nch >= 4 ? 3 : (nch >= 2 ? 2 : 1);
+            int r = nch;
+            while (r >= nch) {
+                if (pos >= kLutOutputs) { ok = false; break; }
+                const uint32_t w = word == 0 ? e.x : (word == 1 ? e.y : (word == 2 ? e.z : e.w));
+                r = (int)(((w >> (3 * sub)) & 7u) >> (3 - kb));
+                ++pos;
+                if (++sub == 10) { sub = 0; ++word; }
+            }
+            if (!ok) break;
+            return_one(p2, bank2, r);
+            remaining -= 1;
+        }
+        if (ok) {
+            if (remaining > 0 && p2.tok[5] > 0) {
+                const int give = min(remaining, p2.tok[5]);
+                p2.tok[5] -= give;
+                bank2[5] += give;
+            }
+            p = p2;
+#pragma unroll
+            for (int c = 0; c < 6; ++c) bank[c] = bank2[c];
+        } else {
+            need_mt = true;
+        }
+    }
+    if (need_mt) {
+        const uint64_t seed = ((uint64_t)turn_count * 1315423911ull) ^ ((uint64_t)to_play * 2654435761ull) ^
+                              ((uint64_t)total * 97531ull) ^ ((uint64_t)bank_total * 31337ull);
+        token_return_mt(p, bank, total - 10, seed, flags);
+    }
+}
+
+// engine/rules.py:132-147 _grant_noble_if_applicable (first visible noble in slot order)
+__device__ __forceinline__ void grant_noble(uint32_t *sw, Pl &p, int to_play, const BlockLDS &L) {
+    const int nn = (int)bget(sw[SW_DECK], 3);
+    uint32_t owners = (sw[SW_NOB1] >> 8) & 0x7FFFu;
+    bool granted = false;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        const int idx = s < 4 ? (int)bget(sw[SW_NOB0], s) : (int)bget(sw[SW_NOB1], 0);
+        const bool visible = s < nn && ((owners >> (3 * s)) & 7u) == 0 && idx < 10;
+        const uint2 rec = L.nobles[idx < 10 ? idx : 0];
+        const bool meets = p.bon[0] >= (int)bget(rec.x, 1) && p.bon[1] >= (int)bget(rec.x, 2) &&
+                           p.bon[2] >= (int)bget(rec.x, 3) && p.bon[3] >= (int)bget(rec.y, 0) &&
+                           p.bon[4] >= (int)bget(rec.y, 1);
+        const bool take = !granted && visible && meets;
+        owners |= take ? ((uint32_t)(to_play + 1) << (3 * s)) : 0u;
+        p.pres += take ? (int)bget(rec.y, 2) : 0;
+        granted = granted || take;
+    }
+    sw[SW_NOB1] = (sw[SW_NOB1] & 0xFFu) | (owners << 8);
+}
+
+// engine/rules.py:290-303 compute_winner: key (prestige, -cards, -reserved); tie of the top
+// two keys -> None
+template <int P>
+__device__ __forceinline__ int compute_winner(const Tab<P> &T) {
+    // track the top two keys as values (a runtime-indexed key[] array would go to scratch)
+    int best = -1;
+    uint32_t kbest = 0, ksecond = 0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        const Pl p = unpack_pl(T.pw[q]);
+        const int nb = p.bon[0] + p.bon[1] + p.bon[2] + p.bon[3] + p.bon[4];
+        const uint32_t key = ((uint32_t)p.pres << 16) | ((uint32_t)(1023 - nb) << 4) | (uint32_t)(15 - p.nres);
+        if (q == 0) {
+            best = 0;
+            kbest = key;
+        } else if (key >= kbest) {
+            ksecond = kbest;
+            kbest = key;
+            best = q;
+        } else if (q == 1 || key >= ksecond) {
+            ksecond = key;
+        }
+    }
+    return kbest == ksecond ? -1 : best;
+}
+
+__device__ __forceinline__ int get_to_play(const uint32_t *sw) { return (int)bget(sw[SW_BANK1], 2); }
+__device__ __forceinline__ int get_turn(const uint32_t *sw) { return (int)bget(sw[SW_BANK1], 3); }
+__device__ __forceinline__ int get_moves(const uint32_t *sw) { return (int)(sw[SW_MISC] & 0xFFFFu); }
+__device__ __forceinline__ int get_winner(const uint32_t *sw) { return (int)(sw[SW_MISC] >> 24) - 1; }
+__device__ __forceinline__ bool is_terminal(const uint32_t *sw) {
+    return (sw[SW_MISC] & ST_GAME_OVER) && get_to_play(sw) == 0;
+}
+
+// engine/rules.py:196-287 apply_action on the current player (action known legal)
+template <int P>
+__device__ __forceinline__ void apply_action(Tab<P> &T, int a, const uint8_t *live_rec, const BlockLDS &L,
+                                             const uint4 *lut, uint32_t &flags) {
+    uint32_t *sw = T.sw;
+    const int tp = get_to_play(sw);
+    uint32_t w[4];
+    get_player(T, tp, w);
+    Pl p = unpack_pl(w);
+    int bank[6];
+    get_bank(sw, bank);
+    if (a < 10) {  // :201-210 take-3 (only colours still in the bank)
+        const uint32_t cm = take3_mask(a);
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+            const bool take = ((cm >> c) & 1u) && bank[c] >= 1;
+            bank[c] -= take ? 1 : 0;
+            p.tok[c] += take ? 1 : 0;
+        }
+    } else if (a < 15) {  // :211-215 take-2
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+            bank[c] -= (a - 10) == c ? 2 : 0;
+            p.tok[c] += (a - 10) == c ? 2 : 0;
+        }
+    } else if (a < 27) {  // :216-225 buy visible, refill
+        const int k = a - 15;
+        pay_for_card(p, bank, card_rec(L, board_get(sw, k)));
+        board_set(sw, k, deck_pop(sw, live_rec, k >> 2));
+    } else if (a < 39) {  // :226-240 reserve visible, gold if any, refill
+        const int k = a - 27;
+        const int card = board_get(sw, k);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) p.res[i] = p.nres == i ? card : p.res[i];
+        p.rev |= 1 << p.nres;
+        p.nres += 1;
+        const bool gold = bank[5] > 0;
+        bank[5] -= gold ? 1 : 0;
+        p.tok[5] += gold ? 1 : 0;
+        board_set(sw, k, deck_pop(sw, live_rec, k >> 2));
+    } else if (a < 42) {  // :241-249 reserve blind (hidden), gold if any
+        const int card = (int)deck_pop(sw, live_rec, a - 39);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) p.res[i] = p.nres == i ? card : p.res[i];
+        p.rev &= ~(1 << p.nres);
+        p.nres += 1;
+        const bool gold = bank[5] > 0;
+        bank[5] -= gold ? 1 : 0;
+        p.tok[5] += gold ? 1 : 0;
+    } else {  // :250-255 buy reserved: list.pop(i) shifts later slots
+        const int i = a - 42;
+        const int r0 = opaque(p.res[0]), r1 = opaque(p.res[1]), r2 = opaque(p.res[2]);
+        const int card = i == 0 ? r0 : (i == 1 ? r1 : r2);
+        p.res[0] = i == 0 ? r1 : r0;
+        p.res[1] = i <= 1 ? r2 : r1;
+        p.res[2] = 0xFF;
+        p.rev = (p.rev & ((1 << i) - 1)) | ((p.rev >> (i + 1)) << i);
+        p.nres -= 1;
+        pay_for_card(p, bank, card_rec(L, card));
+    }
+    grant_noble(sw, p, tp, L);                                              // :260
+    enforce_token_limit(p, bank, get_turn(sw), tp, lut, flags);             // :261
+    uint32_t misc = sw[SW_MISC];
+    if (p.pres >= 15) misc |= ST_GAME_OVER;                                 // :264-265
+    pack_pl(p, w);
+    put_player(T, tp, w);
+    put_bank(sw, bank);
+    const int moves = (int)(misc & 0xFFFFu) + 1;                            // :268-272
+    const int ntp = (tp + 1) % P;
+    const int turn = moves / 2 + 1;
+    misc = (misc & 0xFFFF0000u) | (uint32_t)moves;
+    sw[SW_BANK1] = (sw[SW_BANK1] & 0x0000FFFFu) | ((uint32_t)ntp << 16) | ((uint32_t)min(turn, 255) << 24);
+    if (turn >= 100) {                                                      // :275-279
+        misc |= ST_GAME_OVER | ST_TURN_LIMIT;
+        misc &= 0x00FFFFFFu;  // winner None
+    } else if ((misc & ST_GAME_OVER) && ntp == 0) {                         // :282-285
+        sw[SW_MISC] = misc;
+        const int wnr = compute_winner(T);
+        misc = (misc & 0x00FFFFFFu) | ((uint32_t)(wnr + 1) << 24);
+    }
+    sw[SW_MISC] = misc;
+}
+
+// ------------------------------------------------------------------------------------------
+// observation (engine/encode.py:124-187) into this lane's LDS row, as bytes
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void put4(uint8_t *row, int o, uint32_t w) {
+    row[o] = (uint8_t)w;
+    row[o + 1] = (uint8_t)(w >> 8);
+    row[o + 2] = (uint8_t)(w >> 16);
+    row[o + 3] = (uint8_t)(w >> 24);
+}
+
+__device__ __forceinline__ void put_card13(uint8_t *row, int o, uint4 rec, bool present) {
+    put4(row, o, present ? rec.x : 0u);
+    put4(row, o + 4, present ? rec.y : 0u);
+    put4(row, o + 8, present ? rec.z : 0u);
+    row[o + 12] = present ? (uint8_t)rec.w : (uint8_t)0;
+}
+
+template <int P>
+__device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *row, const BlockLDS &L) {
+    const uint32_t *sw = T.sw;
+    const int tp = get_to_play(sw);
+    put4(row, 0, sw[SW_BANK0]);                 // bank :128
+    row[4] = (uint8_t)sw[SW_BANK1];
+    row[5] = (uint8_t)(sw[SW_BANK1] >> 8);
+    uint32_t me[4], op[4];
+    get_player(T, tp, me);                      // current :131-135
+    get_player(T, (tp + 1) % P, op);            // opponent = next player :138-142
+    put4(row, 6, me[0]);
+    put4(row, 10, me[1]);
+    put4(row, 14, me[2]);
+    row[18] = (uint8_t)(me[3] & 3u);
+    put4(row, 19, op[0]);
+    put4(row, 23, op[1]);
+    put4(row, 27, op[2]);
+    row[31] = (uint8_t)(op[3] & 3u);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {              // board :144-147
+        const int id = (int)bget(sw[SW_BOARD + k / 4], k % 4);
+        put_card13(row, 32 + 13 * k, card_rec(L, id), id != 0xFF);
+    }
+    const int mn = (int)(me[3] & 3u), on = (int)(op[3] & 3u), orev = (int)((op[3] >> 2) & 7u);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {               // own reserved, always revealed :151-155
+        const bool pr = i < mn;
+        put_card13(row, 188 + 14 * i, card_rec(L, (int)bget(me[3], i + 1)), pr);
+        row[188 + 14 * i + 13] = pr ? 1 : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {               // opponent reserved, hidden -> zeros :158-168
+        const bool pr = i < on && ((orev >> i) & 1);
+        put_card13(row, 230 + 14 * i, card_rec(L, (int)bget(op[3], i + 1)), pr);
+        row[230 + 14 * i + 13] = pr ? 1 : 0;
+    }
+    const int nn = (int)bget(sw[SW_DECK], 3);
+    const uint32_t owners = (sw[SW_NOB1] >> 8) & 0x7FFFu;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {               // nobles[:3] :171-178
+        const int idx = (int)bget(sw[SW_NOB0], i);
+        const bool pr = i < nn && ((owners >> (3 * i)) & 7u) == 0 && idx < 10;
+        const uint2 rec = L.nobles[idx < 10 ? idx : 0];
+        put4(row, 272 + 6 * i, pr ? rec.x : 0u);
+        row[272 + 6 * i + 4] = pr ? (uint8_t)rec.y : (uint8_t)0;
+        row[272 + 6 * i + 5] = pr ? (uint8_t)(rec.y >> 8) : (uint8_t)0;
+    }
+    row[290] = (uint8_t)sw[SW_DECK];            // deck sizes :180-181
+    row[291] = (uint8_t)(sw[SW_DECK] >> 8);
+    row[292] = (uint8_t)(sw[SW_DECK] >> 16);
+    row[293] = (uint8_t)get_turn(sw);           // misc :183-186
+    row[294] = (uint8_t)tp;
+    row[295] = (uint8_t)get_moves(sw);          // > 255 patched after the block store
+    row[296] = is_terminal(sw) ? 1 : 0;
+}
+
+// Block store of this wave's staged rows: obs[t0 .. t0+rows) as int32, 16 B per lane-store.
+__device__ __forceinline__ void store_obs_block(const BlockLDS &L, int rows, int32_t *dst) {
+    const int nbytes = rows * kObsDim;
+    const int full = nbytes >> 2;
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(L.rows);
+    for (int d = lane_id(); d < full; d += 64) {
+        const uint32_t w = src[d];
+        *reinterpret_cast<int4 *>(dst + 4 * d) =
+            make_int4((int)(w & 0xFFu), (int)((w >> 8) & 0xFFu), (int)((w >> 16) & 0xFFu), (int)(w >> 24));
+    }
+    for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) dst[b] = (int32_t)L.rows[b];
+}
+
+// Block store of this wave's masks: mask[t0 .. t0+rows) as int8 [rows][45].
+__device__ __forceinline__ void store_mask_block(const BlockLDS &L, int rows, int8_t *dst) {
+    const int nbytes = rows * 45;
+    for (int d = lane_id(); 4 * d < nbytes; d += 64) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int b = 4 * d + q;
+            const int r = b / 45, c = b - 45 * r;
+            const uint32_t bit = b < nbytes ? (uint32_t)((L.mask[r < 64 ? r : 63] >> c) & 1ull) : 0u;
+            v |= bit << (8 * q);
+        }
+        if (4 * d + 3 < nbytes) {
+            *reinterpret_cast<uint32_t *>(dst + 4 * d) = v;
+        } else {
+            for (int q = 0; 4 * d + q < nbytes; ++q) dst[4 * d + q] = (int8_t)(v >> (8 * q));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// deal: engine/state.py:181-211 initial_state's shuffles, from one engine seed
+// ------------------------------------------------------------------------------------------
+// Fisher–Yates (Lib/random.py:389-394) over tier 1, 2, 3 decks then the nobles, driven by ONE
+// uniform loop over MT outputs: every lane advances its own stream by one output per
+// iteration and its own shuffle state machine accepts or rejects it (_randbelow), so the cost
+// is the wave's maximum output count, not the sum of per-draw maxima.
+__device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec, uint8_t *scr) {
+    for (int i = 0; i < 100; ++i) scr[i] = (uint8_t)(i < 90 ? i : i - 90);
+    MTStream ms;
+    ms.init(seed);
+    int d = 0, base = 0, i = 39;
+    uint32_t flags = 0;
+    for (int j = 0;; ++j) {
+        const bool done = d >= 4;
+        if (!__any(!done)) break;
+        if (j >= MTStream::kMaxOut) {
+            if (!done) flags |= SPL_F_RNG_LIMIT;
+            break;
+        }
+        const uint32_t y = ms.next(j);
+        if (!done) {
+            const int n = i + 1;
+            const int r = (int)(y >> (32 - bit_length((uint32_t)n)));
+            if (r < n) {
+                const uint8_t xi = scr[base + i], xr = scr[base + r];
+                scr[base + i] = xr;
+                scr[base + r] = xi;
+                if (--i == 0) {
+                    ++d;
+                    base = d == 1 ? 40 : (d == 2 ? 70 : 90);
+                    i = d == 1 ? 29 : (d == 2 ? 19 : 9);
+                }
+            }
+        }
+    }
+    // deck bytes (list order; the 4 dealt cards per tier sit past deck_len)
+    const uint4 *s4 = reinterpret_cast<const uint4 *>(scr);
+    uint4 *r4 = reinterpret_cast<uint4 *>(rec);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) r4[q] = s4[q];
+    uint32_t board[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {  // board[tier][i] = deck.pop()
+        const int b = tier_base(t), n = tier_size(t);
+        board[t] = (uint32_t)scr[b + n - 1] | ((uint32_t)scr[b + n - 2] << 8) | ((uint32_t)scr[b + n - 3] << 16) |
+                   ((uint32_t)scr[b + n - 4] << 24);
+    }
+    const int nn = P + 1 < 10 ? P + 1 : 10;  // state.py:194 (<= 5 for P <= 4)
+    uint32_t nob0 = 0, nob1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) nob0 |= (s < nn ? (uint32_t)scr[90 + s] : 0xFFu) << (8 * s);
+    nob1 = nn > 4 ? (uint32_t)scr[94] : 0xFFu;
+    uint4 tail0 = make_uint4(board[0], board[1], board[2], 36u | (26u << 8) | (16u << 16) | ((uint32_t)nn << 24));
+    uint4 tail1 = make_uint4(nob0, nob1, 1u, seed);
+    r4[6] = tail0;
+    r4[7] = tail1;
+    return flags;
+}
+
+template <int P>
+__device__ __forceinline__ void fresh_state(Tab<P> &T, uint32_t status, uint4 tail0, uint4 tail1) {
+    T.sw[SW_BANK0] = 0x04040404u;                       // DEFAULT_BANK, state.py:26-33
+    T.sw[SW_BANK1] = 4u | (5u << 8) | (0u << 16) | (1u << 24);  // to_play 0, turn_count 1
+    T.sw[SW_MISC] = status;                              // move_count 0, winner None
+    T.sw[SW_BOARD] = tail0.x;
+    T.sw[SW_BOARD + 1] = tail0.y;
+    T.sw[SW_BOARD + 2] = tail0.z;
+    T.sw[SW_DECK] = tail0.w;
+    T.sw[SW_NOB0] = tail1.x;
+    T.sw[SW_NOB1] = tail1.y;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        T.pw[q][0] = T.pw[q][1] = T.pw[q][2] = 0u;
+        T.pw[q][3] = 0xFFFFFF00u;
+    }
+}
+
+__device__ __forceinline__ Pcg64 load_pcg(const KArena &A, int t) {
+    const uint64_t *p = reinterpret_cast<const uint64_t *>(A.pcg + (size_t)t * kPcgBytes);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(p + 4);
+    Pcg64 g;
+    g.s_hi = p[0];
+    g.s_lo = p[1];
+    g.inc_hi = p[2];
+    g.inc_lo = p[3];
+    g.has32 = q[0];
+    g.u32 = q[1];
+    return g;
+}
+__device__ __forceinline__ void store_pcg(const KArena &A, int t, const Pcg64 &g) {
+    uint64_t *p = reinterpret_cast<uint64_t *>(A.pcg + (size_t)t * kPcgBytes);
+    uint32_t *q = reinterpret_cast<uint32_t *>(p + 4);
+    p[0] = g.s_hi;
+    p[1] = g.s_lo;
+    p[2] = g.inc_hi;
+    p[3] = g.inc_lo;
+    q[0] = g.has32;
+    q[1] = g.u32;
+}
+
+// queue `t` for a pool refill (wave-aggregated: one atomic per wave)
+__device__ __forceinline__ void push_needy(uint32_t *needy, bool want, uint32_t t) {
+    const uint64_t b = __ballot(want);
+    if (b == 0) return;
+    const int leader = __ffsll((unsigned long long)b) - 1;
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(&needy[0], (uint32_t)__popcll(b));
+    base = __shfl(base, leader);
+    const int rank = __popcll(b & ((1ull << lane_id()) - 1ull));
+    if (want) needy[1 + base + rank] = t;
+}
+
+// reset() without a seed / same-step autoreset: the next episode is the pool deal
+// (envs/splendor_env.py:43-44 continued np_random stream).  Returns SPL_F_* bits.
+template <int P>
+__device__ __forceinline__ uint32_t reset_from_pool(Tab<P> &T, const KArena &A, int t, uint8_t *scr, bool &push) {
+    const uint32_t misc = T.sw[SW_MISC];
+    const int nxt = ((misc & ST_ACTIVE) ? 1 : 0) ^ 1;
+    uint8_t *rec = slot_rec(A, t, nxt);
+    uint32_t *rw = reinterpret_cast<uint32_t *>(rec);
+    uint32_t flags = 0;
+    if (rw[kRecReady / 4] == 0u) {  // pool not refilled yet: deal inline (correct, just slower)
+        Pcg64 g = load_pcg(A, t);
+        const uint32_t seed = g.engine_seed();
+        store_pcg(A, t, g);
+        flags |= deal_into(seed, P, rec, scr);
+    }
+    const uint4 tail0 = *reinterpret_cast<const uint4 *>(rec + kRecBoard);
+    const uint4 tail1 = *reinterpret_cast<const uint4 *>(rec + kRecNob0);
+    rw[kRecReady / 4] = 0u;  // now live
+    const bool pending = (misc & ST_PENDING) != 0;
+    push = !pending;
+    const uint32_t status = (nxt ? ST_ACTIVE : 0u) | ST_PENDING;
+    fresh_state(T, status, tail0, tail1);
+    return flags;
+}
+
+template <int P>
+__device__ __forceinline__ void load_tab(Tab<P> &T, const KArena &A, int t) {
+#pragma unroll
+    for (int w = 0; w < SW_COUNT; ++w) T.sw[w] = A.planes[(size_t)w * A.n + t];
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) T.pw[q][k] = A.planes[(size_t)pw_index(q, k) * A.n + t];
+}
+
+template <int P>
+__device__ __forceinline__ void store_tab(const Tab<P> &T, const KArena &A, int t) {
+#pragma unroll
+    for (int w = 0; w < SW_COUNT; ++w) A.planes[(size_t)w * A.n + t] = T.sw[w];
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) A.planes[(size_t)pw_index(q, k) * A.n + t] = T.pw[q][k];
+}
+
+__device__ __forceinline__ void load_tables_lds(BlockLDS &L, const KTables &Tb) {
+    for (int i = lane_id(); i < 90; i += 64) L.cards[i] = Tb.cards[i];
+    if (lane_id() < 10) L.nobles[lane_id()] = Tb.nobles[lane_id()];
+}
+
+template <int P>
+__device__ __forceinline__ uint64_t legal_of(const Tab<P> &T, const BlockLDS &L) {
+    uint32_t w[4];
+    get_player(T, get_to_play(T.sw), w);
+    const Pl p = unpack_pl(w);
+    int bank[6];
+    get_bank(T.sw, bank);
+    return legal_mask(T.sw, p, bank, L);
+}
+
+// uniform-random legal action: Philox(seed; table, ply) scaled to the legal count
+__device__ __forceinline__ int sample_uniform(uint64_t m, uint64_t seed, uint64_t table, uint64_t ply) {
+    const int n = __popcll(m);
+    if (n == 0) return 0;
+    const uint4 r = philox4x32(make_uint4((uint32_t)table, (uint32_t)(table >> 32), (uint32_t)ply, (uint32_t)(ply >> 32)),
+                               make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    int k = (int)(((uint64_t)r.x * (uint64_t)n) >> 32);
+    // position of the k-th set bit
+    uint64_t mm = m;
+    int pos = 0;
+#pragma unroll
+    for (int width = 32; width >= 1; width >>= 1) {
+        const uint64_t low = mm & ((1ull << width) - 1ull);
+        const int c = __popcll(low);
+        const bool up = k >= c;
+        k -= up ? c : 0;
+        pos += up ? width : 0;
+        mm = up ? (mm >> width) : low;
+    }
+    return pos;
+}
+
+// ------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------
+
+// Token-return table: for every (turn_count, to_play, sum(tokens), sum(bank)) in the domain,
+// the top 3 bits of the first 40 outputs of random.Random(seed) (engine/rules.py:170-176).
+__global__ __launch_bounds__(64) void k_build_lut(uint4 *lut) {
+    const int e = blockIdx.x * 64 + lane_id();
+    if (e >= kLutEntries) return;
+    const int sb = e % kLutSb, st = 11 + (e / kLutSb) % kLutSt, tp = (e / (kLutSb * kLutSt)) % kLutTp,
+              tc = e / (kLutSb * kLutSt * kLutTp);
+    const uint64_t seed = ((uint64_t)tc * 1315423911ull) ^ ((uint64_t)tp * 2654435761ull) ^ ((uint64_t)st * 97531ull) ^
+                          ((uint64_t)sb * 31337ull);
+    MTStream ms;
+    ms.init(seed);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int j = 0; j < kLutOutputs; ++j) {
+        const uint32_t top = ms.next(j) >> 29;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] |= (j / 10 == q) ? top << (3 * (j % 10)) : 0u;
+    }
+    lut[e] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// SplendorEnv.step for every table (envs/splendor_env.py:51-90) + same-step autoreset.
+template <int P>
+__global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
+    __shared__ BlockLDS L;
+    const int lane = lane_id();
+    const int t0 = blockIdx.x * 64;
+    const int t = t0 + lane;
+    const bool valid = t < A.n;
+    const int rows = min(64, A.n - t0);
+    load_tables_lds(L, Tb);
+
+    Tab<P> T;
+    int action = 0;
+    if (valid) {
+        load_tab(T, A, t);
+        action = S.actions[t];
+    } else {
+        fresh_state(T, 0u, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u), make_uint4(0xFFFFFFFFu, 0xFFu, 0u, 0u));
+    }
+    __syncthreads();
+
+    uint32_t flags = 0;
+    float reward = 0.0f;
+    bool term = false;
+    uint64_t outmask = 0;
+    const uint8_t *live = slot_rec(A, valid ? t : 0, (T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0);
+    if (valid) {
+        if (is_terminal(T.sw)) {                                  // :53-54 RuntimeError
+            flags = SPL_F_AFTER_TERMINAL;
+        } else {
+            const uint64_t m = legal_of(T, L);                    // :55
+            if (m == 0) {                                         // :56-61 no legal move: draw
+                T.sw[SW_MISC] = (T.sw[SW_MISC] | ST_GAME_OVER) & 0x00FFFFFFu;
+                T.sw[SW_BANK1] &= 0xFF00FFFFu;                    // to_play = 0
+                term = true;
+                flags = SPL_F_DRAW;
+            } else if (action < 0 || action >= SPL_NUM_ACTIONS) { // :62-63 ValueError
+                flags = SPL_F_OOB;
+                outmask = m;
+            } else if (!((m >> action) & 1ull)) {                 // :64-66 illegal
+                flags = SPL_F_ILLEGAL;
+                reward = -0.01f;
+                outmask = m;
+            } else {
+                apply_action(T, action, live, L, Tb.lut, flags);  // :68
+                term = is_terminal(T.sw);                         // :70
+                if (term) {                                       // :71-80
+                    const int w = get_winner(T.sw);
+                    const bool tl = (T.sw[SW_MISC] & ST_TURN_LIMIT) != 0;
+                    reward = (w < 0 && tl) ? -0.1f : (w < 0 ? 0.0f : (w == P - 1 ? 1.0f : -1.0f));
+                    flags |= tl ? SPL_F_TURN_LIMIT : 0u;          // :82-83
+                } else {
+                    outmask = legal_of(T, L);                     // :81
+                }
+            }
+        }
+    }
+    const int8_t wnr = (int8_t)get_winner(T.sw);
+
+    // terminal observations for gymnasium's info["final_observation"]
+    const bool want_final = S.autoreset && S.final_obs != nullptr;
+    const uint64_t fin = __ballot(valid && term && want_final);
+    if (fin) {
+        if (valid && term) encode_row(T, &L.rows[lane * kObsDim], L);
+        __syncthreads();
+        uint64_t b = fin;
+        while (b) {
+            const int r = __ffsll((unsigned long long)b) - 1;
+            b &= b - 1;
+            int32_t *dst = S.final_obs + (size_t)(t0 + r) * kObsDim;
+            for (int e = lane; e < kObsDim; e += 64) dst[e] = (int32_t)L.rows[r * kObsDim + e];
+        }
+        __syncthreads();
+    }
+    // episode statistics (player 0's final reward, envs/splendor_env.py:92-115)
+    if (valid && term) {
+        const int w = get_winner(T.sw);
+        const bool tl = (T.sw[SW_MISC] & ST_TURN_LIMIT) != 0;
+        const float r0 = w < 0 ? (tl ? -0.1f : 0.0f) : (w == 0 ? 1.0f : -1.0f);
+        if (S.ep_return) S.ep_return[t] += r0;
+        if (S.ep_count) S.ep_count[t] += 1u;
+        if (want_final && get_moves(T.sw) > 255) S.final_obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
+    }
+    // same-step autoreset from the pool
+    bool push = false;
+    if (valid && term && S.autoreset) {
+        flags |= SPL_F_RESET | reset_from_pool(T, A, t, &L.rows[lane * kScratchStride], push);
+        outmask = legal_of(T, L);
+    }
+    push_needy(A.needy, push, (uint32_t)t);
+    __syncthreads();  // deal scratch (rows) free again
+
+    // observation + mask of the current state, block stores
+    encode_row(T, &L.rows[lane * kObsDim], L);
+    L.mask[lane] = outmask;
+    __syncthreads();
+    int32_t *obs_dst = S.obs + (size_t)t0 * kObsDim;
+    store_obs_block(L, rows, obs_dst);
+    store_mask_block(L, rows, S.mask + (size_t)t0 * 45);
+    if (__any(valid && get_moves(T.sw) > 255)) {
+        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): block store of this dword has left
+        if (valid && get_moves(T.sw) > 255) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
+    }
+    if (valid) {
+        S.reward[t] = reward;
+        S.terminated[t] = term ? 1 : 0;
+        S.flags[t] = (uint8_t)flags;
+        if (S.winner) S.winner[t] = wnr;
+        if (S.next_actions)
+            S.next_actions[t] = sample_uniform(outmask, S.policy_seed, (uint64_t)(S.table0 + t), S.ply);
+        store_tab(T, A, t);
+    }
+}
+
+// Explicit reset (SplendorEnv.reset / VectorEnv.reset), then observation + mask of all tables.
+template <int P>
+__global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64_t *pcg_in, const uint8_t *mask_in,
+                                              int32_t *obs, int8_t *mask_out) {
+    __shared__ BlockLDS L;
+    const int lane = lane_id();
+    const int t0 = blockIdx.x * 64;
+    const int t = t0 + lane;
+    const bool valid = t < A.n;
+    const int rows = min(64, A.n - t0);
+    load_tables_lds(L, Tb);
+    Tab<P> T;
+    if (valid) load_tab(T, A, t);
+    else fresh_state(T, 0u, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u), make_uint4(0xFFFFFFFFu, 0xFFu, 0u, 0u));
+    __syncthreads();
+    const bool doit = valid && (mask_in == nullptr || mask_in[t] != 0);
+    uint8_t *scr = &L.rows[lane * kScratchStride];
+    bool push = false;
+    if (doit) {
+        if (pcg_in) {  // reset(seed=...): restart this table's np_random stream, deal 2 episodes
+            Pcg64 g;
+            g.s_hi = pcg_in[4 * (size_t)t];
+            g.s_lo = pcg_in[4 * (size_t)t + 1];
+            g.inc_hi = pcg_in[4 * (size_t)t + 2];
+            g.inc_lo = pcg_in[4 * (size_t)t + 3];
+            g.has32 = 0;
+            g.u32 = 0;
+            uint8_t *r0 = slot_rec(A, t, 0), *r1 = slot_rec(A, t, 1);
+            const uint32_t seed0 = g.engine_seed();
+            deal_into(seed0, P, r0, scr);
+            const uint32_t seed1 = g.engine_seed();
+            deal_into(seed1, P, r1, scr);
+            store_pcg(A, t, g);
+            const uint4 tail0 = *reinterpret_cast<const uint4 *>(r0 + kRecBoard);
+            const uint4 tail1 = *reinterpret_cast<const uint4 *>(r0 + kRecNob0);
+            reinterpret_cast<uint32_t *>(r0)[kRecReady / 4] = 0u;
+            // keep ST_PENDING: a queued refill entry (if any) must stay unique
+            fresh_state(T, T.sw[SW_MISC] & ST_PENDING, tail0, tail1);
+        } else {       // reset() without a seed: continue the stream (pool deal)
+            reset_from_pool(T, A, t, scr, push);
+        }
+    }
+    push_needy(A.needy, push, (uint32_t)t);
+    __syncthreads();
+    if (obs || mask_out) {
+        encode_row(T, &L.rows[lane * kObsDim], L);
+        L.mask[lane] = (valid && !is_terminal(T.sw)) ? legal_of(T, L) : 0ull;  // env info mask
+        __syncthreads();
+        if (obs) store_obs_block(L, rows, obs + (size_t)t0 * kObsDim);
+        if (mask_out) store_mask_block(L, rows, mask_out + (size_t)t0 * 45);
+    }
+    if (valid) store_tab(T, A, t);
+}
+
+// Pool refill: deal the next episode of every queued table (compacted list; the grid covers
+// the worst case and idle waves exit at once).
+template <int P>
+__global__ __launch_bounds__(64) void k_refill(KArena A) {
+    __shared__ uint8_t scr_all[64 * kScratchStride] __attribute__((aligned(16)));
+    const int lane = lane_id();
+    const uint32_t count = A.needy[0];
+    const uint32_t e = blockIdx.x * 64u + (uint32_t)lane;
+    if (blockIdx.x * 64u >= count) return;  // whole wave idle
+    if (e < count) {
+        const int t = (int)A.needy[1 + e];
+        const size_t mi = (size_t)SW_MISC * A.n + t;
+        const uint32_t misc = A.planes[mi];
+        const int nxt = ((misc & ST_ACTIVE) ? 1 : 0) ^ 1;
+        uint8_t *rec = slot_rec(A, t, nxt);
+        if (reinterpret_cast<const uint32_t *>(rec)[kRecReady / 4] == 0u) {
+            Pcg64 g = load_pcg(A, t);
+            const uint32_t seed = g.engine_seed();
+            store_pcg(A, t, g);
+            deal_into(seed, P, rec, &scr_all[lane * kScratchStride]);
+        }
+        A.planes[mi] = misc & ~ST_PENDING;
+    }
+}
+
+// Observation and/or mask of the current state (spl_encode / spl_legal).
+template <int P>
+__global__ __launch_bounds__(64) void k_observe(KArena A, KTables Tb, int32_t *obs, int8_t *mask_out) {
+    __shared__ BlockLDS L;
+    const int lane = lane_id();
+    const int t0 = blockIdx.x * 64;
+    const int t = t0 + lane;
+    const bool valid = t < A.n;
+    const int rows = min(64, A.n - t0);
+    load_tables_lds(L, Tb);
+    Tab<P> T;
+    if (valid) load_tab(T, A, t);
+    else fresh_state(T, 0u, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u), make_uint4(0xFFFFFFFFu, 0xFFu, 0u, 0u));
+    __syncthreads();
+    if (obs) encode_row(T, &L.rows[lane * kObsDim], L);
+    L.mask[lane] = valid ? legal_of(T, L) : 0ull;  // engine legal_moves (no terminal check)
+    __syncthreads();
+    if (obs) {
+        store_obs_block(L, rows, obs + (size_t)t0 * kObsDim);
+        if (__any(valid && get_moves(T.sw) > 255)) {
+            __builtin_amdgcn_s_waitcnt(0);
+            if (valid && get_moves(T.sw) > 255) obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
+        }
+    }
+    if (mask_out) store_mask_block(L, rows, mask_out + (size_t)t0 * 45);
+}
+
+__global__ __launch_bounds__(64) void k_sample(int n, const int8_t *mask, int32_t *actions, uint64_t seed, uint64_t ply,
+                                               int64_t table0) {
+    const int t = blockIdx.x * 64 + lane_id();
+    if (t >= n) return;
+    uint64_t m = 0;
+    for (int i = 0; i < 45; ++i) m |= (uint64_t)(mask[(size_t)t * 45 + i] != 0) << i;
+    actions[t] = sample_uniform(m, seed, (uint64_t)(table0 + t), ply);
+}
+
+// host view <-> arena (splendor_table.h)
+template <int P>
+__global__ __launch_bounds__(64) void k_download(KArena A, int first, int count, spl_table_t *out) {
+    const int i = blockIdx.x * 64 + lane_id();
+    if (i >= count) return;
+    const int t = first + i;
+    Tab<P> T;
+    load_tab(T, A, t);
+    spl_table_t &v = out[i];
+    const uint32_t *sw = T.sw;
+    v.num_players = P;
+    int bank[6];
+    get_bank(sw, bank);
+    for (int c = 0; c < 6; ++c) v.bank[c] = bank[c];
+    const uint32_t owners = (sw[SW_NOB1] >> 8) & 0x7FFFu;
+    const int nn = (int)bget(sw[SW_DECK], 3);
+    for (int q = 0; q < SPL_MAX_PLAYERS; ++q) {
+        spl_player_t &pv = v.players[q];
+        for (int k = 0; k < 3; ++k) pv.reserved[k] = -1, pv.revealed[k] = 0;
+        for (int k = 0; k < 5; ++k) pv.nobles[k] = -1;
+        for (int c = 0; c < 6; ++c) pv.tokens[c] = 0;
+        for (int c = 0; c < 5; ++c) pv.bonuses[c] = 0;
+        pv.prestige = pv.n_reserved = pv.n_nobles = 0;
+        if (q >= P) continue;
+        const Pl p = unpack_pl(T.pw[q]);
+        for (int c = 0; c < 6; ++c) pv.tokens[c] = p.tok[c];
+        for (int c = 0; c < 5; ++c) pv.bonuses[c] = p.bon[c];
+        pv.prestige = p.pres;
+        pv.n_reserved = p.nres;
+        for (int k = 0; k < p.nres; ++k) {
+            pv.reserved[k] = p.res[k];
+            pv.revealed[k] = (p.rev >> k) & 1;
+        }
+        int nk = 0;
+        for (int s = 0; s < nn && s < 5; ++s) {
+            if ((int)((owners >> (3 * s)) & 7u) == q + 1)
+                pv.nobles[nk++] = s < 4 ? (int)bget(sw[SW_NOB0], s) : (int)bget(sw[SW_NOB1], 0);
+        }
+        pv.n_nobles = nk;
+    }
+    for (int k = 0; k < 12; ++k) {
+        const int id = (int)bget(sw[SW_BOARD + k / 4], k % 4);
+        v.board[k] = id == 0xFF ? -1 : id;
+    }
+    const uint8_t *rec = slot_rec(A, t, (sw[SW_MISC] & ST_ACTIVE) ? 1 : 0);
+    for (int tt = 0; tt < 3; ++tt) {
+        const int len = (int)bget(sw[SW_DECK], tt);
+        v.deck_len[tt] = len;
+        for (int k = 0; k < 40; ++k) v.decks[tt][k] = k < len ? (int)rec[tier_base(tt) + k] : -1;
+    }
+    v.n_nobles = nn;
+    for (int s = 0; s < 5; ++s) {
+        const int idx = s < 4 ? (int)bget(sw[SW_NOB0], s) : (int)bget(sw[SW_NOB1], 0);
+        const bool taken = ((owners >> (3 * s)) & 7u) != 0 || idx >= 10;
+        v.nobles[s] = (s < nn && !taken) ? idx : -1;
+    }
+    v.to_play = get_to_play(sw);
+    v.turn_count = get_turn(sw);
+    v.move_count = get_moves(sw);
+    v.game_over = (sw[SW_MISC] & ST_GAME_OVER) ? 1 : 0;
+    v.winner = get_winner(sw);
+    v.turn_limit_reached = (sw[SW_MISC] & ST_TURN_LIMIT) ? 1 : 0;
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void k_upload(KArena A, int first, int count, const spl_table_t *in) {
+    const int i = blockIdx.x * 64 + lane_id();
+    if (i >= count) return;
+    const int t = first + i;
+    const spl_table_t &v = in[i];
+    Tab<P> T;
+    uint32_t *sw = T.sw;
+    const uint32_t old_misc = A.planes[(size_t)SW_MISC * A.n + t];
+    int bank[6];
+    for (int c = 0; c < 6; ++c) bank[c] = v.bank[c];
+    sw[SW_BANK1] = ((uint32_t)v.to_play << 16) | ((uint32_t)v.turn_count << 24);
+    put_bank(sw, bank);
+    sw[SW_MISC] = ((uint32_t)v.move_count & 0xFFFFu) | (v.game_over ? ST_GAME_OVER : 0u) |
+                  (v.turn_limit_reached ? ST_TURN_LIMIT : 0u) | (old_misc & (ST_ACTIVE | ST_PENDING)) |
+                  ((uint32_t)(v.winner + 1) << 24);
+    for (int tt = 0; tt < 3; ++tt) {
+        uint32_t w = 0;
+        for (int s = 0; s < 4; ++s) w |= (uint32_t)(v.board[tt * 4 + s] < 0 ? 0xFF : v.board[tt * 4 + s]) << (8 * s);
+        sw[SW_BOARD + tt] = w;
+    }
+    sw[SW_DECK] = (uint32_t)v.deck_len[0] | ((uint32_t)v.deck_len[1] << 8) | ((uint32_t)v.deck_len[2] << 16) |
+                  ((uint32_t)v.n_nobles << 24);
+    // visible slots keep their noble; taken slots get the players' nobles in order
+    int slot_idx[5];
+    uint32_t owners = 0;
+    int next_taken = 0;
+    for (int s = 0; s < 5; ++s) slot_idx[s] = (s < v.n_nobles && v.nobles[s] >= 0) ? v.nobles[s] : 0xFF;
+    for (int s = 0; s < 5 && s < v.n_nobles; ++s)
+        if (v.nobles[s] < 0) owners |= 7u << (3 * s);
+    for (int q = 0; q < P; ++q) {
+        for (int k = 0; k < v.players[q].n_nobles; ++k) {
+            while (next_taken < v.n_nobles && !(v.nobles[next_taken] < 0)) ++next_taken;
+            if (next_taken < v.n_nobles) {
+                slot_idx[next_taken] = v.players[q].nobles[k];
+                owners = (owners & ~(7u << (3 * next_taken))) | ((uint32_t)(q + 1) << (3 * next_taken));
+                ++next_taken;
+            }
+        }
+    }
+    sw[SW_NOB0] = (uint32_t)slot_idx[0] | ((uint32_t)slot_idx[1] << 8) | ((uint32_t)slot_idx[2] << 16) |
+                  ((uint32_t)slot_idx[3] << 24);
+    sw[SW_NOB1] = (uint32_t)slot_idx[4] | (owners << 8);
+    for (int q = 0; q < P; ++q) {
+        Pl p;
+        const spl_player_t &pv = v.players[q];
+        for (int c = 0; c < 6; ++c) p.tok[c] = pv.tokens[c];
+        for (int c = 0; c < 5; ++c) p.bon[c] = pv.bonuses[c];
+        p.pres = pv.prestige;
+        p.nres = pv.n_reserved;
+        p.rev = 0;
+        for (int k = 0; k < 3; ++k) {
+            p.res[k] = k < pv.n_reserved ? pv.reserved[k] : 0xFF;
+            p.rev |= (k < pv.n_reserved && pv.revealed[k]) ? (1 << k) : 0;
+        }
+        pack_pl(p, T.pw[q]);
+    }
+    store_tab(T, A, t);
+    uint8_t *rec = slot_rec(A, t, (old_misc & ST_ACTIVE) ? 1 : 0);
+    for (int tt = 0; tt < 3; ++tt)
+        for (int k = 0; k < tier_size(tt); ++k) rec[tier_base(tt) + k] = (uint8_t)(k < v.deck_len[tt] ? v.decks[tt][k] : 0xFF);
+    reinterpret_cast<uint32_t *>(rec)[kRecReady / 4] = 0u;
+}
+
+}  // namespace spl
+
+// ==========================================================================================
+// host side: C-ABI
+// ==========================================================================================
+using namespace spl;
+
+struct spl_ctx_s {
+    int device;
+    uint4 *cards;
+    uint2 *nobles;
+    uint4 *lut;
+    int refill_period;
+    void *stage;
+    size_t stage_bytes;
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess) return fail(SPL_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+static KTables ktables(const spl_ctx_t *c) { return KTables{c->cards, c->nobles, c->lut}; }
+
+static int check_arena(const spl_ctx_t *ctx, const spl_arena_t *a) {
+    if (!ctx) return fail(SPL_E_ARG, "null context");
+    if (!a || !a->base) return fail(SPL_E_ARG, "null arena");
+    if (a->players < 2 || a->players > 4) return fail(SPL_E_ARG, "players must be 2..4");
+    if (a->n <= 0) return fail(SPL_E_ARG, "arena must hold at least one table");
+    if (((uintptr_t)a->base & 255u) != 0) return fail(SPL_E_ARG, "arena base must be 256-byte aligned");
+    if (a->bytes < spl_arena_bytes(a->n, a->players)) return fail(SPL_E_ARG, "arena too small");
+    return SPL_OK;
+}
+
+static KArena karena(const spl_arena_t *a) {
+    const ArenaLayout L = arena_layout(a->n, a->players);
+    uint8_t *b = static_cast<uint8_t *>(a->base);
+    return KArena{reinterpret_cast<uint32_t *>(b + L.planes), b + L.slots, b + L.pcg,
+                  reinterpret_cast<uint32_t *>(b + L.needy), a->n};
+}
+
+static int launch_check() {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(SPL_E_HIP, std::string("kernel launch: ") + hipGetErrorString(e));
+    return SPL_OK;
+}
+
+static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 63) / 64); }
+
+extern "C" {
+
+int spl_abi_version(void) { return SPL_ABI_VERSION; }
+
+const char *spl_last_error(void) { return g_err.c_str(); }
+
+int64_t spl_arena_bytes(int32_t n, int32_t players) {
+    if (n <= 0 || players < 2 || players > 4) return -1;
+    return arena_layout(n, players).total;
+}
+
+int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_ctx_t **out) {
+    if (!cards || !nobles || !out) return fail(SPL_E_ARG, "null argument");
+    *out = nullptr;
+    // constant records: observation-ready card bytes (engine/encode.py:77-96) + costs
+    std::vector<uint4> crec(90);
+    for (int i = 0; i < 90; ++i) {
+        const int32_t *c = cards + 8 * i;
+        if (c[0] < 1 || c[0] > 3 || c[1] < 0 || c[1] > 4 || c[2] < 0 || c[2] > 255)
+            return fail(SPL_E_ARG, "bad card table row " + std::to_string(i));
+        uint8_t b[16] = {0};
+        b[0] = 1;
+        b[1] = (uint8_t)c[0];
+        b[2] = (uint8_t)c[2];
+        b[3 + c[1]] = 1;
+        for (int k = 0; k < 5; ++k) {
+            if (c[3 + k] < 0 || c[3 + k] > 255) return fail(SPL_E_ARG, "bad card cost");
+            b[8 + k] = (uint8_t)c[3 + k];
+        }
+        b[13] = (uint8_t)c[1];
+        memcpy(&crec[i], b, 16);
+    }
+    std::vector<uint2> nrec(10);
+    for (int i = 0; i < 10; ++i) {
+        const int32_t *n = nobles + 6 * i;
+        uint8_t b[8] = {0};
+        b[0] = 1;
+        for (int k = 0; k < 5; ++k) {
+            if (n[k] < 0 || n[k] > 255) return fail(SPL_E_ARG, "bad noble table");
+            b[1 + k] = (uint8_t)n[k];
+        }
+        b[6] = (uint8_t)n[5];
+        memcpy(&nrec[i], b, 8);
+    }
+    HIP_TRY(hipSetDevice(device));
+    spl_ctx_t *c = new spl_ctx_t();
+    c->device = device;
+    c->refill_period = 8;
+    if (hipMalloc(&c->cards, sizeof(uint4) * 90) != hipSuccess || hipMalloc(&c->nobles, sizeof(uint2) * 10) != hipSuccess ||
+        hipMalloc(&c->lut, sizeof(uint4) * kLutEntries) != hipSuccess) {
+        spl_ctx_destroy(c);
+        return fail(SPL_E_HIP, "hipMalloc of constant tables failed");
+    }
+    HIP_TRY(hipMemcpy(c->cards, crec.data(), sizeof(uint4) * 90, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->nobles, nrec.data(), sizeof(uint2) * 10, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_build_lut, dim3(blocks_for(kLutEntries)), dim3(64), 0, 0, c->lut);
+    if (int r = launch_check()) {
+        spl_ctx_destroy(c);
+        return r;
+    }
+    HIP_TRY(hipDeviceSynchronize());
+    *out = c;
+    return SPL_OK;
+}
+
+int spl_ctx_destroy(spl_ctx_t *ctx) {
+    if (!ctx) return SPL_OK;
+    if (ctx->cards) (void)hipFree(ctx->cards);
+    if (ctx->nobles) (void)hipFree(ctx->nobles);
+    if (ctx->lut) (void)hipFree(ctx->lut);
+    if (ctx->stage) (void)hipFree(ctx->stage);
+    delete ctx;
+    return SPL_OK;
+}
+
+int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period) {
+    if (!ctx || period < 0) return fail(SPL_E_ARG, "bad refill period");
+    ctx->refill_period = period;
+    return SPL_OK;
+}
+
+int64_t spl_ctx_token_lut(spl_ctx_t *ctx, uint32_t *out, int64_t words) {
+    const int64_t need = (int64_t)kLutEntries * 4;
+    if (!ctx) return fail(SPL_E_ARG, "null context");
+    if (!out) return need;
+    if (words < need) return fail(SPL_E_ARG, "output too small");
+    HIP_TRY(hipMemcpy(out, ctx->lut, need * 4, hipMemcpyDeviceToHost));
+    return need;
+}
+
+#define DISPATCH_P(P_, call)                        \
+    switch (P_) {                                   \
+        case 2: { constexpr int PP = 2; call; } break; \
+        case 3: { constexpr int PP = 3; call; } break; \
+        case 4: { constexpr int PP = 4; call; } break; \
+        default: return fail(SPL_E_ARG, "players must be 2..4"); \
+    }
+
+int spl_reset(spl_ctx_t *ctx, spl_arena_t *arena, const uint64_t *pcg, const uint8_t *reset_mask, int32_t *obs,
+              int8_t *mask, void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    if (obs && ((uintptr_t)obs & 15u)) return fail(SPL_E_ARG, "obs must be 16-byte aligned");
+    if (mask && ((uintptr_t)mask & 3u)) return fail(SPL_E_ARG, "mask must be 4-byte aligned");
+    const KArena A = karena(arena);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_reset<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
+                                                  ktables(ctx), pcg, reset_mask, obs, mask));
+    if (int r = launch_check()) return r;
+    arena->steps = 0;
+    return SPL_OK;
+}
+
+int spl_arena_init(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    HIP_TRY(hipMemsetAsync(arena->base, 0, (size_t)spl_arena_bytes(arena->n, arena->players),
+                           static_cast<hipStream_t>(stream)));
+    arena->steps = 0;
+    return SPL_OK;
+}
+
+int spl_refill(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    const KArena A = karena(arena);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_refill<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A));
+    if (int r = launch_check()) return r;
+    HIP_TRY(hipMemsetAsync(A.needy, 0, sizeof(uint32_t), s));
+    return SPL_OK;
+}
+
+int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    if (!a || !a->actions || !a->obs || !a->mask || !a->reward || !a->terminated || !a->flags)
+        return fail(SPL_E_ARG, "spl_step: actions/obs/mask/reward/terminated/flags are required");
+    if (((uintptr_t)a->obs & 15u) || (a->final_obs && ((uintptr_t)a->final_obs & 3u)))
+        return fail(SPL_E_ARG, "obs must be 16-byte aligned");
+    if ((uintptr_t)a->mask & 3u) return fail(SPL_E_ARG, "mask must be 4-byte aligned");
+    KStep S;
+    S.actions = a->actions;
+    S.obs = a->obs;
+    S.mask = a->mask;
+    S.reward = a->reward;
+    S.terminated = a->terminated;
+    S.flags = a->flags;
+    S.winner = a->winner;
+    S.final_obs = a->final_obs;
+    S.next_actions = a->next_actions;
+    S.ep_return = a->ep_return;
+    S.ep_count = a->ep_count;
+    S.policy_seed = a->policy_seed;
+    S.ply = a->ply;
+    S.table0 = a->table0;
+    S.autoreset = a->autoreset;
+    const KArena A = karena(arena);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DISPATCH_P(arena->players,
+               hipLaunchKernelGGL(k_step<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A, ktables(ctx), S));
+    if (int r = launch_check()) return r;
+    arena->steps += 1;
+    if (a->autoreset && ctx->refill_period > 0 && arena->steps % ctx->refill_period == 0)
+        return spl_refill(ctx, arena, stream);
+    return SPL_OK;
+}
+
+int spl_encode(spl_ctx_t *ctx, spl_arena_t *arena, int32_t *obs, void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    if (!obs || ((uintptr_t)obs & 15u)) return fail(SPL_E_ARG, "obs must be non-null and 16-byte aligned");
+    const KArena A = karena(arena);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_observe<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
+                                                  ktables(ctx), obs, (int8_t *)nullptr));
+    return launch_check();
+}
+
+int spl_legal(spl_ctx_t *ctx, spl_arena_t *arena, int8_t *mask, void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    if (!mask || ((uintptr_t)mask & 3u)) return fail(SPL_E_ARG, "mask must be non-null and 4-byte aligned");
+    const KArena A = karena(arena);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_observe<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
+                                                  ktables(ctx), (int32_t *)nullptr, mask));
+    return launch_check();
+}
+
+int spl_sample_uniform(spl_ctx_t *ctx, int32_t n, const int8_t *mask, int32_t *actions, uint64_t seed, uint64_t ply,
+                       int64_t table0, void *stream) {
+    if (!ctx || n <= 0 || !mask || !actions) return fail(SPL_E_ARG, "bad sample arguments");
+    hipLaunchKernelGGL(k_sample, dim3(blocks_for(n)), dim3(64), 0, static_cast<hipStream_t>(stream), n, mask, actions,
+                       seed, ply, table0);
+    return launch_check();
+}
+
+static int ensure_stage(spl_ctx_t *ctx, size_t bytes) {
+    if (ctx->stage_bytes >= bytes) return SPL_OK;
+    if (ctx->stage) (void)hipFree(ctx->stage);
+    ctx->stage = nullptr;
+    ctx->stage_bytes = 0;
+    HIP_TRY(hipMalloc(&ctx->stage, bytes));
+    ctx->stage_bytes = bytes;
+    return SPL_OK;
+}
+
+int spl_table_download(spl_ctx_t *ctx, spl_arena_t *arena, int32_t first, int32_t count, spl_table_t *host,
+                       void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    if (!host || first < 0 || count <= 0 || first + count > arena->n) return fail(SPL_E_ARG, "bad download range");
+    if (int r = ensure_stage(ctx, sizeof(spl_table_t) * (size_t)count)) return r;
+    const KArena A = karena(arena);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    spl_table_t *st = static_cast<spl_table_t *>(ctx->stage);
+    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_download<PP>, dim3(blocks_for(count)), dim3(64), 0, s, A, first, count, st));
+    if (int r = launch_check()) return r;
+    HIP_TRY(hipMemcpyAsync(host, st, sizeof(spl_table_t) * (size_t)count, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return SPL_OK;
+}
+
+static int validate_view(const spl_table_t &v, int P) {
+    if (v.num_players != P) return fail(SPL_E_RANGE, "num_players does not match the arena");
+    for (int c = 0; c < 6; ++c)
+        if (v.bank[c] < 0 || v.bank[c] > 255) return fail(SPL_E_RANGE, "bank out of range");
+    int owned = 0;
+    for (int q = 0; q < P; ++q) {
+        const spl_player_t &p = v.players[q];
+        for (int c = 0; c < 6; ++c)
+            if (p.tokens[c] < 0 || p.tokens[c] > 255) return fail(SPL_E_RANGE, "tokens out of range");
+        for (int c = 0; c < 5; ++c)
+            if (p.bonuses[c] < 0 || p.bonuses[c] > 255) return fail(SPL_E_RANGE, "bonuses out of range");
+        if (p.prestige < 0 || p.prestige > 255) return fail(SPL_E_RANGE, "prestige out of range");
+        if (p.n_reserved < 0 || p.n_reserved > 3) return fail(SPL_E_RANGE, "n_reserved out of range");
+        for (int k = 0; k < p.n_reserved; ++k)
+            if (p.reserved[k] < 0 || p.reserved[k] >= 90) return fail(SPL_E_RANGE, "reserved card id out of range");
+        if (p.n_nobles < 0 || p.n_nobles > 5) return fail(SPL_E_RANGE, "player nobles out of range");
+        for (int k = 0; k < p.n_nobles; ++k)
+            if (p.nobles[k] < 0 || p.nobles[k] >= 10) return fail(SPL_E_RANGE, "player noble id out of range");
+        owned += p.n_nobles;
+    }
+    for (int k = 0; k < 12; ++k)
+        if (v.board[k] < -1 || v.board[k] >= 90) return fail(SPL_E_RANGE, "board card id out of range");
+    for (int t = 0; t < 3; ++t) {
+        if (v.deck_len[t] < 0 || v.deck_len[t] > tier_size(t)) return fail(SPL_E_RANGE, "deck too long for its record");
+        for (int k = 0; k < v.deck_len[t]; ++k)
+            if (v.decks[t][k] < 0 || v.decks[t][k] >= 90) return fail(SPL_E_RANGE, "deck card id out of range");
+    }
+    if (v.n_nobles < 0 || v.n_nobles > 5) return fail(SPL_E_RANGE, "visible noble slots out of range");
+    int taken = 0;
+    for (int s = 0; s < v.n_nobles; ++s) {
+        if (v.nobles[s] >= 10 || v.nobles[s] < -1) return fail(SPL_E_RANGE, "noble id out of range");
+        taken += v.nobles[s] < 0;
+    }
+    if (owned > taken) return fail(SPL_E_RANGE, "players hold more nobles than taken slots");
+    if (v.to_play < 0 || v.to_play >= P) return fail(SPL_E_RANGE, "to_play out of range");
+    if (v.turn_count < 0 || v.turn_count > 255) return fail(SPL_E_RANGE, "turn_count out of range");
+    if (v.move_count < 0 || v.move_count > 508) return fail(SPL_E_RANGE, "move_count out of range (<= 508)");
+    if (v.winner < -1 || v.winner >= P) return fail(SPL_E_RANGE, "winner out of range");
+    return SPL_OK;
+}
+
+int spl_table_upload(spl_ctx_t *ctx, spl_arena_t *arena, int32_t first, int32_t count, const spl_table_t *host,
+                     void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    if (!host || first < 0 || count <= 0 || first + count > arena->n) return fail(SPL_E_ARG, "bad upload range");
+    for (int i = 0; i < count; ++i)
+        if (int r = validate_view(host[i], arena->players)) return r;
+    if (int r = ensure_stage(ctx, sizeof(spl_table_t) * (size_t)count)) return r;
+    const KArena A = karena(arena);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    spl_table_t *st = static_cast<spl_table_t *>(ctx->stage);
+    HIP_TRY(hipMemcpyAsync(st, host, sizeof(spl_table_t) * (size_t)count, hipMemcpyHostToDevice, s));
+    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_upload<PP>, dim3(blocks_for(count)), dim3(64), 0, s, A, first, count, st));
+    if (int r = launch_check()) return r;
+    HIP_TRY(hipStreamSynchronize(s));
+    return SPL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,84 @@
+// spl_layout.h — HBM layout of a Splendor arena and the packed per-table state words.
+//
+// One wavefront lane owns one table.  The mutable table state lives in 32-bit WORD PLANES:
+// plane w holds word w of every table, so lane t touching word w reads plane[w * n + t] and a
+// wave moves 256 contiguous bytes per plane (coalesced).  Words (bytes little-endian):
+//
+//   SW_BANK0   bank white, blue, green, red
+//   SW_BANK1   bank black, gold, to_play, turn_count
+//   SW_MISC    move_count (16) | status (8) | winner+1 (8)
+//   SW_BOARD+t board tier t+1, slots 0..3 (card id, 0xFF = empty)
+//   SW_DECK    deck_len tier 1..3, number of visible noble slots
+//   SW_NOB0    noble index in visible slots 0..3 (0xFF = none)
+//   SW_NOB1    slot 4 index | slot owners << 8 (3 bits per slot: 0 visible, p+1 taken by
+//              player p, 7 taken by an unknown player)
+//   PW(p,0..3) player p: tokens w b g r | tokens k, gold, bonus w, b | bonus g, r, k, prestige |
+//              n_reserved (bits 0-1) + revealed (bits 2-4), reserved card ids 0..2 (0xFF none)
+//
+// The 13 observation bytes of a player (tokens 6, bonuses 5, prestige, n_reserved —
+// reference engine/encode.py:131-142) are exactly PW0, PW1, PW2 and (PW3 & 3).
+//
+// Deck storage: two 128-byte SLOT RECORDS per table (AoS, [n][2][128]).  The active record
+// holds the live deck (bytes 0..89: tier 1 at 0, tier 2 at 40, tier 3 at 70, list order, top
+// = deck_len-1); the other is the POOL: the next episode's deal, prepared ahead from the
+// table's engine-seed stream.  Record bytes 96..123 hold the deal's board / deck / noble words
+// (SW_BOARD.., SW_DECK, SW_NOB0, SW_NOB1), a ready word and the engine seed.
+#pragma once
+#include <stdint.h>
+
+namespace spl {
+
+enum : int {
+    SW_BANK0 = 0,
+    SW_BANK1 = 1,
+    SW_MISC = 2,
+    SW_BOARD = 3,
+    SW_DECK = 6,
+    SW_NOB0 = 7,
+    SW_NOB1 = 8,
+    SW_COUNT = 9,
+};
+__host__ __device__ constexpr int num_words(int P) { return SW_COUNT + 4 * P; }
+__host__ __device__ constexpr int pw_index(int p, int k) { return SW_COUNT + 4 * p + k; }
+
+// SW_MISC status bits
+constexpr uint32_t ST_GAME_OVER = 1u << 16;
+constexpr uint32_t ST_TURN_LIMIT = 1u << 17;
+constexpr uint32_t ST_ACTIVE = 1u << 18;   // which slot record holds the live deck
+constexpr uint32_t ST_PENDING = 1u << 19;  // table is queued for a pool refill
+
+constexpr int kSlotBytes = 128;
+constexpr int kRecBoard = 96;   // 3 words: board at deal
+constexpr int kRecDeck = 108;   // SW_DECK at deal
+constexpr int kRecNob0 = 112;   // SW_NOB0 at deal
+constexpr int kRecNob1 = 116;   // SW_NOB1 at deal
+constexpr int kRecReady = 120;  // 1 = dealt and unused
+constexpr int kRecSeed = 124;   // engine seed of the deal (diagnostic)
+constexpr int kPcgBytes = 64;   // per-table numpy PCG64 record: s_hi s_lo inc_hi inc_lo has32 u32
+
+__host__ __device__ constexpr int tier_base(int t) { return t == 0 ? 0 : (t == 1 ? 40 : 70); }
+__host__ __device__ constexpr int tier_size(int t) { return t == 0 ? 40 : (t == 1 ? 30 : 20); }
+
+// token-return RNG table domain (engine/rules.py:170-175 seed fields):
+//   turn_count < 128, to_play < 4, sum(tokens) in 11..13, sum(bank) < 16
+constexpr int kLutTc = 128, kLutTp = 4, kLutSt = 3, kLutSb = 16;
+constexpr int kLutEntries = kLutTc * kLutTp * kLutSt * kLutSb;
+constexpr int kLutOutputs = 40;  // top 3 bits of the first 40 MT outputs, 10 per word
+
+struct ArenaLayout {
+    int64_t planes, slots, pcg, needy, total;
+};
+
+__host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+__host__ __device__ inline ArenaLayout arena_layout(int64_t n, int P) {
+    ArenaLayout L;
+    L.planes = 0;
+    L.slots = align256(L.planes + (int64_t)num_words(P) * n * 4);
+    L.pcg = align256(L.slots + n * 2 * kSlotBytes);
+    L.needy = align256(L.pcg + n * kPcgBytes);
+    L.total = align256(L.needy + (n + 1) * 4);
+    return L;
+}
+
+}  // namespace spl

@@ -1,0 +1,170 @@
+"""Engine: a batch of Splendor tables resident on one MI355X, driven through the C-ABI.
+
+All buffers are PyTorch-ROCm tensors (caller-owned device memory, include/splendor_amd.h
+"Conventions"); launches go on the current torch stream, so they compose with torch work and
+never synchronise the host except for the explicit download/upload helpers.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native
+from ._native import NUM_ACTIONS, OBS_DIM, TABLE_DTYPE, ArenaDesc, StepArgs, check, ptr
+from .engine.state import load_tables
+from .seeding import pcg64_states
+
+
+class Engine:
+    """`num_tables` independent tables of `num_players` players on `device`.
+
+    table0: global id of table 0 — the policy stream of a shard is keyed by global table ids,
+    so results do not depend on how tables are split across GPUs.
+    """
+
+    def __init__(self, num_tables, num_players=2, device=None, refill_period=8, table0=0):
+        torch = _native.require_gpu()
+        self.torch = torch
+        self.lib = _native.load_library()
+        if not 2 <= num_players <= 4:
+            raise ValueError("num_players must be 2..4")
+        if num_tables <= 0:
+            raise ValueError("num_tables must be positive")
+        self.n, self.P, self.table0 = int(num_tables), int(num_players), int(table0)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        cards, nobles = load_tables()
+        ctx = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_ctx_create(self.device.index, cards.ctypes.data, nobles.ctypes.data,
+                                                    ctypes.byref(ctx)))
+        self.ctx = ctx
+        check(self.lib, self.lib.spl_ctx_set_refill_period(self.ctx, int(refill_period)))
+        nbytes = int(self.lib.spl_arena_bytes(self.n, self.P))
+        dev = self.device
+        self._arena_raw = torch.zeros(nbytes + 256, dtype=torch.uint8, device=dev)
+        off = (-self._arena_raw.data_ptr()) % 256
+        self.arena = self._arena_raw[off:off + nbytes]
+        self.desc = ArenaDesc(self.arena.data_ptr(), nbytes, self.n, self.P, 0)
+        n = self.n
+        self.obs = torch.zeros((n, OBS_DIM), dtype=torch.int32, device=dev)
+        self.mask = torch.zeros((n, NUM_ACTIONS), dtype=torch.int8, device=dev)
+        self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.terminated = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.winner = torch.zeros(n, dtype=torch.int8, device=dev)
+        self.final_obs = torch.zeros((n, OBS_DIM), dtype=torch.int32, device=dev)
+        self.actions = torch.zeros(n, dtype=torch.int32, device=dev)
+        with torch.cuda.device(dev):
+            check(self.lib, self.lib.spl_arena_init(self.ctx, ctypes.byref(self.desc), self.stream()))
+
+    # ------------------------------------------------------------------------------------
+    def stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def close(self):
+        if getattr(self, "ctx", None) is not None and self.ctx.value:
+            self.torch.cuda.synchronize(self.device)
+            self.lib.spl_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------------------------
+    def reset(self, seeds=None, mask=None, obs=True):
+        """Reset tables (all, or where `mask` is true).  seeds: None continues every table's
+        engine-seed stream (reset() without a seed); else one seed per table (reset(seed=s)).
+        Writes self.obs / self.mask for every table."""
+        torch = self.torch
+        pcg = None
+        if seeds is not None:
+            seeds = list(seeds)
+            if len(seeds) != self.n:
+                raise ValueError(f"expected {self.n} seeds")
+            pcg = torch.from_numpy(pcg64_states(seeds).reshape(-1)).to(self.device)
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+            if m.numel() != self.n:
+                raise ValueError("mask must have one entry per table")
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_reset(self.ctx, ctypes.byref(self.desc), ptr(pcg), ptr(m),
+                                               ptr(self.obs) if obs else None, ptr(self.mask) if obs else None,
+                                               self.stream()))
+        self._keep = (pcg, m)  # alive until the async reset has consumed them
+        return self.obs, self.mask
+
+    def step(self, actions=None, autoreset=True, final_obs=True, next_actions=None, policy_seed=0, ply=0,
+             ep_return=None, ep_count=None):
+        """One env step on every table (SplendorEnv.step semantics per table)."""
+        torch = self.torch
+        if actions is None:
+            actions = self.actions
+        if not (isinstance(actions, torch.Tensor) and actions.device == self.device and actions.dtype == torch.int32
+                and actions.is_contiguous()):
+            actions = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
+        if actions.numel() != self.n:
+            raise ValueError(f"expected {self.n} actions")
+        a = StepArgs(actions=actions.data_ptr(), obs=self.obs.data_ptr(), mask=self.mask.data_ptr(),
+                     reward=self.reward.data_ptr(), terminated=self.terminated.data_ptr(),
+                     flags=self.flags.data_ptr(), winner=self.winner.data_ptr(),
+                     final_obs=self.final_obs.data_ptr() if (final_obs and autoreset) else None,
+                     autoreset=1 if autoreset else 0,
+                     next_actions=None if next_actions is None else next_actions.data_ptr(),
+                     policy_seed=int(policy_seed) & (2**64 - 1), ply=int(ply) & (2**64 - 1), table0=self.table0,
+                     ep_return=None if ep_return is None else ep_return.data_ptr(),
+                     ep_count=None if ep_count is None else ep_count.data_ptr())
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_step(self.ctx, ctypes.byref(self.desc), ctypes.byref(a), self.stream()))
+        self._keep_actions = actions
+        return self.obs, self.mask, self.reward, self.terminated, self.flags
+
+    def refill(self):
+        with self.torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_refill(self.ctx, ctypes.byref(self.desc), self.stream()))
+
+    def encode(self, out=None):
+        out = self.obs if out is None else out
+        with self.torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_encode(self.ctx, ctypes.byref(self.desc), ptr(out), self.stream()))
+        return out
+
+    def legal(self, out=None):
+        out = self.mask if out is None else out
+        with self.torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_legal(self.ctx, ctypes.byref(self.desc), ptr(out), self.stream()))
+        return out
+
+    def sample_uniform(self, mask=None, out=None, seed=0, ply=0):
+        mask = self.mask if mask is None else mask
+        out = self.actions if out is None else out
+        with self.torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_sample_uniform(self.ctx, self.n, ptr(mask), ptr(out), int(seed), int(ply),
+                                                        self.table0, self.stream()))
+        return out
+
+    # ------------------------------------------------------------------------------------
+    def download(self, first=0, count=None):
+        """numpy TABLE_DTYPE[count] host views (synchronous)."""
+        count = self.n - first if count is None else count
+        out = np.zeros(count, TABLE_DTYPE)
+        with self.torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_table_download(self.ctx, ctypes.byref(self.desc), first, count,
+                                                        out.ctypes.data, self.stream()))
+        return out
+
+    def upload(self, records, first=0):
+        recs = np.ascontiguousarray(np.atleast_1d(records).astype(TABLE_DTYPE))
+        with self.torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_table_upload(self.ctx, ctypes.byref(self.desc), first, len(recs),
+                                                      recs.ctypes.data, self.stream()))
+
+    def token_lut(self):
+        words = int(self.lib.spl_ctx_token_lut(self.ctx, None, 0))
+        out = np.zeros(words, np.uint32)
+        check(self.lib, self.lib.spl_ctx_token_lut(self.ctx, out.ctypes.data, words))
+        return out.reshape(-1, 4)

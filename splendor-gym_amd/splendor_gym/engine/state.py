@@ -1,0 +1,154 @@
+"""Constants, game data and the HOST VIEW of one table.
+
+The live state of every table is on the GPU (word planes in HBM, see csrc/spl_layout.h).  This
+module gives the reference-shaped host view used for inspection, rendering and crafted-state
+tests — the device copy is exchanged through spl_table_download / spl_table_upload.
+
+Mirrors the reference's splendor_gym/engine/state.py:10-104 (colour order, DEFAULT_BANK, Card,
+Noble, PlayerState, SplendorState field names) so code that reads ``env.state`` keeps working.
+"""
+import json
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+TOKEN_COLORS = ["white", "blue", "green", "red", "black", "gold"]
+STANDARD_COLORS = TOKEN_COLORS[:-1]
+COLOR_INDEX = {c: i for i, c in enumerate(TOKEN_COLORS)}
+STANDARD_COLOR_INDEX = {c: i for i, c in enumerate(STANDARD_COLORS)}
+HUMAN_TO_INTERNAL = {"diamond": "white", "sapphire": "blue", "emerald": "green", "ruby": "red", "onyx": "black"}
+INTERNAL_TO_HUMAN = {v: k for k, v in HUMAN_TO_INTERNAL.items()}
+DEFAULT_BANK = {"white": 4, "blue": 4, "green": 4, "red": 4, "black": 4, "gold": 5}
+
+DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+
+
+def load_tables():
+    """(cards int32[90, 8], nobles int32[10, 6]) from data/tables.json (tools/gen_tables.py)."""
+    with open(os.path.join(DATA_DIR, "tables.json")) as f:
+        t = json.load(f)
+    cards = np.ascontiguousarray(np.array(t["cards"], np.int32))
+    nobles = np.ascontiguousarray(np.array(t["nobles"], np.int32))
+    assert cards.shape == (90, 8) and nobles.shape == (10, 6)
+    return cards, nobles
+
+
+@dataclass(frozen=True)
+class Card:
+    id: int
+    tier: int
+    color: str
+    points: int
+    cost: Dict[str, int]
+
+
+@dataclass(frozen=True)
+class Noble:
+    id: int
+    requirements: Dict[str, int]
+    points: int = 3
+
+
+_CARDS = None
+_NOBLES = None
+
+
+def cards_by_id():
+    global _CARDS, _NOBLES
+    if _CARDS is None:
+        c, n = load_tables()
+        _CARDS = [Card(i, int(r[0]), STANDARD_COLORS[int(r[1])], int(r[2]),
+                       {STANDARD_COLORS[k]: int(r[3 + k]) for k in range(5) if r[3 + k]}) for i, r in enumerate(c)]
+        _NOBLES = [Noble(1000 + i, {STANDARD_COLORS[k]: int(r[k]) for k in range(5) if r[k]}, int(r[5]))
+                   for i, r in enumerate(n)]
+    return _CARDS
+
+
+def nobles_by_index():
+    cards_by_id()
+    return _NOBLES
+
+
+@dataclass
+class PlayerState:
+    tokens: List[int] = field(default_factory=lambda: [0] * 6)
+    bonuses: List[int] = field(default_factory=lambda: [0] * 5)
+    prestige: int = 0
+    reserved: List[Card] = field(default_factory=list)
+    revealed_reserved: List[bool] = field(default_factory=list)
+    nobles: List[Noble] = field(default_factory=list)
+
+
+@dataclass
+class SplendorState:
+    """Host snapshot of one device table (reference engine/state.py:74-87 field names)."""
+    num_players: int
+    bank: List[int]
+    players: List[PlayerState]
+    board: Dict[int, List[Optional[Card]]]
+    decks: Dict[int, List[Card]]
+    nobles: List[Optional[Noble]]
+    to_play: int = 0
+    turn_count: int = 1
+    move_count: int = 0
+    game_over: bool = False
+    winner_index: Optional[int] = None
+    turn_limit_reached: bool = False
+
+    @classmethod
+    def from_record(cls, r):
+        """numpy record of _native.TABLE_DTYPE -> SplendorState."""
+        cards, nobles = cards_by_id(), nobles_by_index()
+        P = int(r["num_players"])
+        players = []
+        for p in range(P):
+            q = r["players"][p]
+            n = int(q["n_reserved"])
+            players.append(PlayerState(tokens=[int(x) for x in q["tokens"]], bonuses=[int(x) for x in q["bonuses"]],
+                                       prestige=int(q["prestige"]),
+                                       reserved=[cards[int(i)] for i in q["reserved"][:n]],
+                                       revealed_reserved=[bool(x) for x in q["revealed"][:n]],
+                                       nobles=[nobles[int(i)] for i in q["nobles"][:int(q["n_nobles"])]]))
+        board = {t: [(cards[int(i)] if i >= 0 else None) for i in r["board"][(t - 1) * 4:t * 4]] for t in (1, 2, 3)}
+        decks = {t: [cards[int(i)] for i in r["decks"][t - 1][:int(r["deck_len"][t - 1])]] for t in (1, 2, 3)}
+        nob = [(nobles[int(i)] if i >= 0 else None) for i in r["nobles"][:int(r["n_nobles"])]]
+        w = int(r["winner"])
+        return cls(P, [int(x) for x in r["bank"]], players, board, decks, nob, int(r["to_play"]), int(r["turn_count"]),
+                   int(r["move_count"]), bool(r["game_over"]), None if w < 0 else w, bool(r["turn_limit_reached"]))
+
+    def to_record(self):
+        from .._native import TABLE_DTYPE
+        r = np.zeros((), TABLE_DTYPE)
+        r["num_players"] = self.num_players
+        r["bank"] = self.bank
+        for p in range(4):
+            q = r["players"][p]
+            q["reserved"] = -1
+            q["nobles"] = -1
+            if p >= self.num_players:
+                continue
+            ps = self.players[p]
+            q["tokens"], q["bonuses"], q["prestige"] = ps.tokens, ps.bonuses, ps.prestige
+            n = len(ps.reserved)
+            q["n_reserved"] = n
+            q["reserved"][:n] = [c.id for c in ps.reserved]
+            rev = list(ps.revealed_reserved) + [False] * n
+            q["revealed"][:n] = [int(bool(x)) for x in rev[:n]]
+            q["n_nobles"] = len(ps.nobles)
+            q["nobles"][:len(ps.nobles)] = [nb.id - 1000 for nb in ps.nobles]
+        r["board"] = [(c.id if c is not None else -1) for t in (1, 2, 3) for c in self.board[t]]
+        r["decks"] = -1
+        for t in (1, 2, 3):
+            d = self.decks[t]
+            r["deck_len"][t - 1] = len(d)
+            r["decks"][t - 1][:len(d)] = [c.id for c in d]
+        r["n_nobles"] = len(self.nobles)
+        r["nobles"] = -1
+        r["nobles"][:len(self.nobles)] = [(nb.id - 1000 if nb is not None else -1) for nb in self.nobles]
+        r["to_play"], r["turn_count"], r["move_count"] = self.to_play, self.turn_count, self.move_count
+        r["game_over"] = int(bool(self.game_over))
+        r["winner"] = -1 if self.winner_index is None else self.winner_index
+        r["turn_limit_reached"] = int(bool(self.turn_limit_reached))
+        return r

@@ -1,0 +1,130 @@
+"""SplendorEnv: the reference's single-table Gymnasium env, stepped by the HIP engine.
+
+Drop-in for reference splendor_gym/envs/splendor_env.py:23-130 — same constructor, spaces, info
+keys, reward values and exceptions.  The table lives on the GPU (an Engine of one table,
+autoreset off); each call launches the step kernel and copies the ~1.3 KB result back.
+For throughput use SplendorVectorEnv (thousands of tables per launch).
+"""
+from typing import Any, Dict, Optional, Tuple
+
+import numpy as np
+
+from .. import _native
+from .._gym_compat import Env, spaces
+from ..engine.encode import OBSERVATION_DIM, TOTAL_ACTIONS
+from ..engine.state import SplendorState
+
+
+class SplendorEnv(Env):
+    metadata = {"render_modes": ["human"], "name": "Splendor-v0"}
+
+    def __init__(self, num_players: int = 2, render_mode: Optional[str] = None, seed: Optional[int] = None,
+                 device=None):
+        super().__init__()
+        if num_players != 2:  # reference envs/splendor_env.py:28-29
+            raise NotImplementedError("Current env supports 2 players only.")
+        self.num_players = num_players
+        self.render_mode = render_mode
+        self.action_space = spaces.Discrete(TOTAL_ACTIONS)
+        self.observation_space = spaces.Box(low=0, high=50, shape=(OBSERVATION_DIM,), dtype=np.int32)
+        self.current_player = 0
+        self._device = device
+        self._eng = None
+        self._seeded = False
+        self._terminal = False
+        _native.load_library()  # fail loudly at construction if the HIP engine is missing
+        _native.require_gpu()
+
+    # --------------------------------------------------------------------------------------
+    def _engine(self):
+        if self._eng is None:
+            from ..device import Engine
+            self._eng = Engine(1, self.num_players, device=self._device, refill_period=0)
+        return self._eng
+
+    def _fetch(self):
+        e = self._eng
+        obs = e.obs[0].cpu().numpy()
+        mask = e.mask[0].cpu().numpy()
+        return obs, mask
+
+    def reset(self, *, seed: Optional[int] = None, options: Optional[Dict[str, Any]] = None):
+        super().reset(seed=seed)
+        eng = self._engine()
+        if seed is not None or not self._seeded:  # gymnasium: reseed, or first reset from entropy
+            eng.reset(seeds=[seed])
+            self._seeded = True
+        else:                                     # continue this env's np_random stream
+            eng.reset(seeds=None)
+        obs, mask = self._fetch()
+        self._terminal = False
+        self.current_player = int(obs[294])
+        return obs, {"action_mask": mask, "to_play": int(obs[294])}
+
+    def step(self, action) -> Tuple[np.ndarray, float, bool, bool, Dict[str, Any]]:
+        if self._eng is None:
+            raise AssertionError("Call reset() first")
+        e = self._eng
+        try:
+            a = int(action)
+        except (TypeError, ValueError):
+            raise ValueError("Action out of bounds for action_space")
+        a = max(min(a, 2**31 - 1), -(2**31))
+        e.actions.fill_(a)
+        e.step(e.actions, autoreset=False)
+        flags = int(e.flags[0].item())
+        if flags & _native.F_AFTER_TERMINAL:  # envs/splendor_env.py:53-54
+            raise RuntimeError("Cannot call step() after episode termination. Call reset().")
+        if flags & _native.F_OOB:             # :62-63
+            raise ValueError("Action out of bounds for action_space")
+        obs, mask = self._fetch()
+        to_play = int(obs[294])
+        self.current_player = to_play
+        if flags & _native.F_DRAW:            # :56-61
+            self._terminal = True
+            return obs, 0.0, True, False, {"action_mask": np.zeros(TOTAL_ACTIONS, dtype=np.int8),
+                                           "to_play": to_play, "draw": True}
+        if flags & _native.F_ILLEGAL:         # :64-66
+            return obs, -0.01, False, False, {"illegal_action": True, "action_mask": mask, "to_play": to_play}
+        reward = float(e.reward[0].item())
+        terminated = bool(e.terminated[0].item())
+        info = {"action_mask": mask, "to_play": to_play}
+        if terminated:
+            self._terminal = True
+            if flags & _native.F_TURN_LIMIT:
+                info["turn_limit"] = True
+            info["final_rewards"] = self._final_rewards(int(e.winner[0].item()), bool(flags & _native.F_TURN_LIMIT))
+        return obs, reward, terminated, False, info
+
+    def _final_rewards(self, w, turn_limit):
+        # envs/splendor_env.py:92-115
+        if w < 0:
+            return {p: (-0.1 if turn_limit else 0.0) for p in range(self.num_players)}
+        return {p: (1.0 if p == w else -1.0) for p in range(self.num_players)}
+
+    def get_final_rewards(self) -> Dict[int, float]:
+        s = self.state
+        if not (s.game_over and s.to_play == 0):
+            raise RuntimeError("Cannot get final rewards for non-terminal state")
+        return self._final_rewards(-1 if s.winner_index is None else s.winner_index, s.turn_limit_reached)
+
+    # ---- host view of the device table ---------------------------------------------------
+    @property
+    def state(self) -> Optional[SplendorState]:
+        """A host SNAPSHOT of the device table (mutations do not write back: use set_state)."""
+        if self._eng is None:
+            return None
+        return SplendorState.from_record(self._eng.download(0, 1)[0])
+
+    def set_state(self, state: SplendorState) -> None:
+        self._engine().upload(state.to_record())
+
+    def render(self):
+        if self.render_mode not in ("human", None):
+            return
+        from ..render import format_game_state
+        print(format_game_state(self.state))
+
+
+def make(num_players: int = 2, render_mode: Optional[str] = None, seed: Optional[int] = None) -> SplendorEnv:
+    return SplendorEnv(num_players=num_players, render_mode=render_mode, seed=seed)

@@ -1,0 +1,81 @@
+"""Multi-GPU sharding: one process per GPU, tables split by contiguous global id ranges.
+
+Tables are independent games, so the step path never communicates.  The only
+collective is at report time: an all-gather of per-table episode-return sums and episode counts
+(torch.distributed; backend "nccl" is RCCL over xGMI on ROCm, "gloo" for CPU tests).  Every RNG
+stream is keyed by the GLOBAL table id, so per-table results are identical for 1/2/4/8 GPUs.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n_global, rank, world):
+    """[lo, hi) global table ids owned by `rank` (contiguous, sizes differ by at most one)."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    base, extra = divmod(int(n_global), int(world))
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def init_distributed(backend=None):
+    """Initialise the default process group from torchrun's env (RANK, WORLD_SIZE, LOCAL_RANK,
+    MASTER_ADDR/PORT).  Returns (rank, world, local_rank); (0, 1, 0) without a launcher."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+    return rank, world, local
+
+
+def gather_returns(ep_return, ep_count, n_global=None):
+    """All-gather per-table (return sum, episode count) shards into full [n_global] tensors on
+    every rank.  Shards may differ in size by one (shard_range); they are padded to equal
+    length for all_gather_into_tensor and trimmed after."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return ep_return.clone(), ep_count.clone()
+    world = dist.get_world_size()
+    n_local = torch.tensor([ep_return.numel()], dtype=torch.int64, device=ep_return.device)
+    sizes = [torch.zeros_like(n_local) for _ in range(world)]
+    dist.all_gather(sizes, n_local)
+    sizes = [int(s.item()) for s in sizes]
+    width = max(sizes)
+    packed = torch.zeros((2, width), dtype=torch.float64, device=ep_return.device)
+    packed[0, :ep_return.numel()] = ep_return.to(torch.float64)
+    packed[1, :ep_count.numel()] = ep_count.to(torch.float64)
+    out = torch.empty((world * 2, width), dtype=torch.float64, device=ep_return.device)
+    dist.all_gather_into_tensor(out, packed)  # rank-major concatenation along dim 0
+    out = out.view(world, 2, width)
+    ret = torch.cat([out[r, 0, :sizes[r]] for r in range(world)])
+    cnt = torch.cat([out[r, 1, :sizes[r]] for r in range(world)])
+    if n_global is not None and ret.numel() != n_global:
+        raise RuntimeError(f"gathered {ret.numel()} tables, expected {n_global}")
+    return ret.to(torch.float32), cnt.to(torch.int64)
+
+
+def max_over_ranks(value, device=None):
+    """Max of a host float over all ranks (the bench's slowest-rank time)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(device=None):
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if device is not None and device.type == "cuda":
+            dist.barrier(device_ids=[device.index])
+        else:
+            dist.barrier()

@@ -1,0 +1,182 @@
+"""HIP engine parity: bit-exact against the CPU oracle (itself pinned to the reference by
+tests/test_oracle_golden.py) and directly against the reference's own outputs for crafted
+states (tests/golden/edge_cases.json).  Every call goes through the C-ABI library."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle, OracleVec, table_to_view, view_to_table
+from schema import canon
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return Oracle()
+
+
+def engine(n, P, **kw):
+    from splendor_gym.device import Engine
+    return Engine(n, P, **kw)
+
+
+def bits_of(mask_i8):
+    m = np.asarray(mask_i8).astype(np.uint64)
+    return (m << np.arange(45, dtype=np.uint64)).sum(axis=-1).astype(np.uint64)
+
+
+def test_token_lut_matches_cpython():
+    e = engine(64, 2)
+    lut = e.token_lut()
+    assert lut.shape == (128 * 4 * 3 * 16, 4)
+    rs = np.random.default_rng(0)
+    idx = np.concatenate([np.arange(0, 2048), rs.integers(0, len(lut), 2048)])
+    for i in idx:
+        i = int(i)
+        sb, st, tp, tc = i % 16, 11 + (i // 16) % 3, (i // 48) % 4, i // 192
+        seed = (tc * 1315423911) ^ (tp * 2654435761) ^ (st * 97531) ^ (sb * 31337)
+        r = random.Random(seed)
+        tops = [r.getrandbits(32) >> 29 for _ in range(40)]
+        words = [sum(tops[10 * q + k] << (3 * k) for k in range(10)) for q in range(4)]
+        assert [int(x) for x in lut[i]] == words, i
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_reset_deals(orc, P):
+    n = 1000  # not a multiple of 64: exercises the partial last wave
+    seeds = list(range(7000, 7000 + n))
+    e = engine(n, P)
+    obs, mask = e.reset(seeds=seeds)
+    vec = OracleVec(orc, n, P, seeds)
+    np.testing.assert_array_equal(obs.cpu().numpy(), vec.obs)
+    np.testing.assert_array_equal(bits_of(mask.cpu().numpy()), vec.mask)
+    recs = e.download()
+    for t in range(n):
+        assert canon(table_to_view(recs[t])) == canon(vec.table(t)), t
+
+
+def run_parity(orc, P, n, plies, refill_period, seed, device_policy, check_state_every=50):
+    import torch
+    e = engine(n, P, refill_period=refill_period)
+    seeds = [seed + i for i in range(n)]
+    e.reset(seeds=seeds)
+    vec = OracleVec(orc, n, P, seeds)
+    rs = np.random.default_rng(seed)
+    next_actions = torch.zeros(n, dtype=torch.int32, device=e.device)
+    e.sample_uniform(out=next_actions, seed=seed, ply=0)
+    n_reset = 0
+    for k in range(plies):
+        if device_policy:
+            acts = next_actions.cpu().numpy().copy()
+        else:
+            acts = np.zeros(n, np.int32)
+            for t in range(n):
+                legal = np.flatnonzero((int(vec.mask[t]) >> np.arange(45)) & 1)
+                acts[t] = rs.choice(legal) if len(legal) else rs.integers(0, 45)
+        # inject illegal and (rarely) out-of-range actions: flagged, state unchanged
+        inj = rs.random(n)
+        acts = np.where(inj < 0.03, rs.integers(0, 45, n), acts)
+        acts = np.where(inj > 0.998, rs.choice([-1, 45, 99], n), acts).astype(np.int32)
+        e.step(torch.from_numpy(acts).to(e.device), next_actions=next_actions, policy_seed=seed, ply=k + 1)
+        ref = vec.step(acts, want_final=True)
+        np.testing.assert_array_equal(e.flags.cpu().numpy(), ref["flags"], err_msg=f"flags ply {k}")
+        np.testing.assert_array_equal(e.reward.cpu().numpy(), ref["reward"], err_msg=f"reward ply {k}")
+        np.testing.assert_array_equal(e.terminated.cpu().numpy(), ref["terminated"], err_msg=f"term ply {k}")
+        np.testing.assert_array_equal(e.winner.cpu().numpy(), ref["winner"], err_msg=f"winner ply {k}")
+        np.testing.assert_array_equal(e.obs.cpu().numpy(), ref["obs"], err_msg=f"obs ply {k}")
+        np.testing.assert_array_equal(bits_of(e.mask.cpu().numpy()), ref["mask"], err_msg=f"mask ply {k}")
+        rows = np.flatnonzero(ref["terminated"])
+        n_reset += len(rows)
+        if len(rows):
+            np.testing.assert_array_equal(e.final_obs.cpu().numpy()[rows], ref["final_obs"][rows],
+                                          err_msg=f"final obs ply {k}")
+        if check_state_every and (k % check_state_every == check_state_every - 1):
+            recs = e.download()
+            for t in range(0, n, max(1, n // 128)):
+                assert canon(table_to_view(recs[t])) == canon(vec.table(t)), (k, t)
+    return n_reset
+
+
+@pytest.mark.parametrize("refill_period", [8, 1, 0])
+def test_trajectories_p2_device_policy(orc, refill_period):
+    """C2 shape: 2 players, 4096 tables, uniform-random policy drawn on the device; every
+    output of every ply compared bit-for-bit with the oracle replaying the same actions.
+    The pool refill schedule (every ply / every 8 / inline deals only) must not matter."""
+    resets = run_parity(orc, 2, 4096, 240 if refill_period == 8 else 120, refill_period, 1234, True)
+    assert resets > 1000
+
+
+@pytest.mark.parametrize("P", [3, 4])
+def test_trajectories_multiplayer(orc, P):
+    resets = run_parity(orc, P, 1024, 200, 8, 99 * P, False)
+    assert resets > 50
+
+
+def test_edge_cases_against_reference():
+    """Crafted and fuzzed states from the REAL reference (make_golden.py): upload, one step
+    without autoreset, compare outputs and the resulting state."""
+    import torch
+    with open(os.path.join(GOLD, "edge_cases.json")) as f:
+        cases = json.load(f)
+    for P in (2, 3, 4):
+        cs = [c for c in cases if c["P"] == P]
+        e = engine(len(cs), P)
+        e.reset(seeds=list(range(len(cs))))
+        recs = np.stack([view_to_table(c["before"]) for c in cs])
+        e.upload(recs)
+        acts = torch.tensor([c["action"] for c in cs], dtype=torch.int32, device=e.device)
+        e.step(acts, autoreset=False)
+        flags = e.flags.cpu().numpy()
+        obs, mask = e.obs.cpu().numpy(), bits_of(e.mask.cpu().numpy())
+        rew, term = e.reward.cpu().numpy(), e.terminated.cpu().numpy()
+        after = e.download()
+        for i, c in enumerate(cs):
+            exp_err = {None: 0, "RuntimeError": 0x08, "ValueError": 0x10}[c["exception"]]
+            assert flags[i] & 0x18 == exp_err, c["name"]
+            assert canon(table_to_view(after[i])) == canon(c["after"]), c["name"]
+            if exp_err:
+                continue
+            np.testing.assert_array_equal(obs[i], np.array(c["obs"], np.int32), err_msg=c["name"])
+            assert int(mask[i]) == c["mask"], c["name"]
+            assert rew[i] == np.float32(c["reward"]), c["name"]
+            assert term[i] == c["terminated"], c["name"]
+            assert flags[i] & 7 == c["flags"], c["name"]
+
+
+def test_upload_download_roundtrip(orc):
+    e = engine(300, 2)
+    e.reset(seeds=list(range(300)))
+    recs = e.download()
+    e.upload(recs)
+    again = e.download()
+    assert recs.tobytes() == again.tobytes()
+
+
+def test_sharded_equals_whole():
+    """Tables split over two engines (global ids 0..2047 and 2048..4095) evolve exactly as one
+    engine of 4096: streams are keyed by global table id (multi-GPU sharding invariance)."""
+    import torch
+    n, half, plies = 4096, 2048, 150
+    whole = engine(n, 2)
+    parts = [engine(half, 2, table0=0), engine(half, 2, table0=half)]
+    seeds = list(range(n))
+    whole.reset(seeds=seeds)
+    parts[0].reset(seeds=seeds[:half])
+    parts[1].reset(seeds=seeds[half:])
+    na_w = torch.zeros(n, dtype=torch.int32, device=whole.device)
+    na_p = [torch.zeros(half, dtype=torch.int32, device=whole.device) for _ in parts]
+    whole.sample_uniform(out=na_w, seed=5, ply=0)
+    for p, na in zip(parts, na_p):
+        p.sample_uniform(out=na, seed=5, ply=0)
+    for k in range(plies):
+        whole.step(na_w.clone(), next_actions=na_w, policy_seed=5, ply=k + 1)
+        for p, na in zip(parts, na_p):
+            p.step(na.clone(), next_actions=na, policy_seed=5, ply=k + 1)
+        got = torch.cat([parts[0].obs, parts[1].obs])
+        assert torch.equal(got, whole.obs), k
+        assert torch.equal(torch.cat([parts[0].flags, parts[1].flags]), whole.flags), k

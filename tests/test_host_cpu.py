@@ -1,0 +1,162 @@
+"""CPU-only tests: C-ABI exports, host-side seeding/layout logic, the device RNG formulation
+compiled for the host, and the gloo multi-process sharding path."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INCLUDE = os.path.join(REPO, "include")
+
+
+def header_functions():
+    names = set()
+    for h in os.listdir(INCLUDE):
+        src = open(os.path.join(INCLUDE, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(spl_[a-z_0-9]+)\s*\(", src, flags=re.M))
+    return names
+
+
+def test_library_exports_every_header_symbol():
+    from splendor_gym import _native
+    lib = _native.load_library()  # dlopen only: no GPU needed
+    declared = header_functions()
+    assert len(declared) >= 15, declared
+    assert declared == set(_native.SIGNATURES), declared ^ set(_native.SIGNATURES)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.spl_abi_version() == 1
+
+
+def test_abi_host_side_errors():
+    """Argument errors are reported before any device work (runs without a GPU)."""
+    from splendor_gym import _native
+    lib = _native.load_library()
+    out = ctypes.c_void_p()
+    assert lib.spl_ctx_create(0, None, None, ctypes.byref(out)) == -1
+    assert b"null" in lib.spl_last_error()
+    assert lib.spl_arena_bytes(0, 2) == -1 and lib.spl_arena_bytes(10, 5) == -1
+    arena = _native.ArenaDesc(None, 0, 10, 2, 0)
+    assert lib.spl_step(None, ctypes.byref(arena), None, None) == -1
+
+
+def test_arena_layout_sizes():
+    from splendor_gym import _native
+    lib = _native.load_library()
+    for n in (1, 63, 64, 65536):
+        for P in (2, 3, 4):
+            words = 9 + 4 * P
+            b = int(lib.spl_arena_bytes(n, P))
+            # planes + 2 deck slots x 128 B + 64 B PCG record + refill list, 256-aligned regions
+            assert b >= words * 4 * n + 256 * n + 64 * n + 4 * (n + 1)
+            assert b % 256 == 0 and b <= words * 4 * n + 320 * n + 4 * n + 4 * 256 + 4
+
+
+def test_table_dtype_matches_oracle_struct():
+    from oracle.oracle import Oracle, TABLE_DTYPE as ORC
+    from splendor_gym._native import TABLE_DTYPE
+    assert TABLE_DTYPE == ORC
+    assert TABLE_DTYPE.itemsize == Oracle().L.orc_table_size()
+
+
+def test_seeding_matches_numpy_generator():
+    from splendor_gym.seeding import pcg64_state, vector_seeds
+    for seed in (0, 1, 12345, 2**40):
+        s = pcg64_state(seed)
+        st = np.random.PCG64(np.random.SeedSequence(seed)).state["state"]
+        assert (s[0] << 64 | s[1]) == st["state"] and (s[2] << 64 | s[3]) == st["inc"]
+    assert vector_seeds(5, 3) == [5, 6, 7]
+    assert vector_seeds(None, 3) is None
+    with pytest.raises(ValueError):
+        vector_seeds([1, 2], 3)
+
+
+def test_engine_seed_stream_matches_gymnasium_semantics():
+    """The device continues numpy's PCG64 stream for engine seeds; the oracle restatement of
+    that continuation equals numpy's own Generator.integers(0, 2**31-1)."""
+    from oracle.oracle import Oracle
+    o = Oracle()
+    for seed in (0, 3, 99, 2024):
+        g = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+        assert o.engine_seeds(seed, 6) == [int(g.integers(0, 2**31 - 1)) for _ in range(6)]
+
+
+def test_constants_match_reference_layout():
+    from splendor_gym.engine import encode as E
+    assert (E.TAKE3_OFFSET, E.TAKE2_OFFSET, E.BUY_VISIBLE_OFFSET, E.RESERVE_VISIBLE_OFFSET,
+            E.RESERVE_BLIND_OFFSET, E.BUY_RESERVED_OFFSET, E.TOTAL_ACTIONS) == (0, 10, 15, 27, 39, 42, 45)
+    assert E.OBSERVATION_DIM == 297
+    assert E.TAKE3_COMBOS[0] == (0, 1, 2) and E.TAKE3_COMBOS[-1] == (2, 3, 4)
+    assert E.encode_buy_visible_index(2, 3) == 22 and E.encode_reserve_blind_index(3) == 41
+
+
+def test_host_state_record_roundtrip():
+    from oracle.oracle import Oracle, view_to_table
+    from splendor_gym.engine.state import SplendorState
+    from splendor_gym.render import format_game_state
+    o = Oracle()
+    v = o.initial_state(2, 42)
+    rec = view_to_table(v)
+    s = SplendorState.from_record(rec)
+    assert s.to_record().tobytes() == rec.tobytes()
+    assert s.board[1][0].id == v["board"][0] and s.bank == [4, 4, 4, 4, 4, 5]
+    assert "Bank" in format_game_state(s)
+
+
+def test_device_mt_stream_formulation_on_host(tmp_path):
+    """The register-only MT19937 stream of csrc/spl_rng.h, compiled for the host, equals the
+    oracle's full-state MT19937 for 454 outputs (1- and 2-word keys)."""
+    exe = tmp_path / "mtstream"
+    orc = tmp_path / "orc.o"
+    subprocess.run(["gcc", "-O2", "-c", "-o", str(orc), os.path.join(REPO, "oracle", "splendor_oracle.c")], check=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), os.path.join(REPO, "tests", "native", "mtstream_host.cpp"),
+                    str(orc)], check=True)
+    r = subprocess.run([str(exe), "400"], capture_output=True, text=True)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+
+
+def test_shard_ranges():
+    from splendor_gym.parallel import shard_range
+    for n, w in ((65536, 8), (1000, 3), (5, 4)):
+        rs = [shard_range(n, r, w) for r in range(w)]
+        assert rs[0][0] == 0 and rs[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+        assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from splendor_gym.parallel import gather_returns, init_distributed, max_over_ranks, shard_range
+    init_distributed(backend="gloo")
+    n_global = 1001
+    lo, hi = shard_range(n_global, rank, world)
+    ids = torch.arange(lo, hi, dtype=torch.float32)
+    ret, cnt = gather_returns(ids * 0.5, (ids % 7).to(torch.int64), n_global=n_global)
+    t = max_over_ranks(float(rank) + 0.25)
+    q.put((rank, ret.tolist(), cnt.tolist(), t))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_gather_returns():
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + os.getpid() % 300
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ret, cnt, t in res:
+        assert ret == [i * 0.5 for i in range(1001)]
+        assert cnt == [i % 7 for i in range(1001)]
+        assert t == 1.25
