@@ -1,0 +1,209 @@
+"""Headline benchmark: env-steps/sec, 2-player Splendor, 65536 tables per MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--tables T] [--players P]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One "step" = one SplendorEnv.step on every table of the batch (BASELINE.json config 3: legal
+mask + uniform-random policy, same-step autoreset, obs int32[297] + mask int8[45] + reward +
+terminated written per table).  Actions are drawn on the device by the step kernel itself
+(fused Philox policy over the new mask), so the timed loop is spl_step launches plus the pool
+refill every 8 steps.  Inputs are resident in HBM before the timed region.
+
+Weak scaling: each rank owns `--tables` tables (global ids rank*T ...), no collective in the
+step path; after the timed region one all-gather (RCCL) collects episode returns.  value =
+tables x world x steps / max-over-ranks wall time.
+
+Printed on rank 0: ONE JSON line with the roofline of the step kernel (HIP events around every
+step launch in the timed region; algorithmic bytes per SURVEY.md §8d: 1370 B per 2-player
+table-step) and, at N=1, the CPU baseline (the C oracle port, one process per core).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "splendor-gym_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
+ALGO_BYTES = {2: 1370, 3: 1408, 4: 1446}  # 2*S_P + 297*4 + 45 + 4 + 4 + 1 (3p interpolated)
+REFILL_EVERY = 8
+
+
+def cpu_baseline(players, procs, steps_per_proc):
+    """The C oracle (a port of the reference engine) as `procs` single-env random rollouts,
+    one process per core, started BEFORE this process touches the GPU (fork-safe)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+
+    def work(i):
+        import numpy as np
+        from oracle.oracle import Oracle, pcg_state_of
+        o = Oracle()
+        pcg = np.array(pcg_state_of(1000 + i), np.uint64)
+        eps = ctypes.c_int64()
+        t = time.perf_counter()
+        n = o.L.orc_random_rollout(players, pcg.ctypes.data, 7 + i, steps_per_proc, ctypes.byref(eps))
+        q.put((n, time.perf_counter() - t, eps.value))
+
+    ps = [ctx.Process(target=work, args=(i,)) for i in range(procs)]
+    t0 = time.perf_counter()
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=600) for _ in ps]
+    wall = time.perf_counter() - t0
+    for p in ps:
+        p.join()
+    total = sum(r[0] for r in res)
+    per_core = sum(r[0] / r[1] for r in res) / len(res)
+    return {"value": round(total / wall, 1), "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "per_core": round(per_core, 1),
+            "sample": (f"C oracle (port of engine/rules.py + envs/splendor_env.py step), {players}p, "
+                       f"{procs} processes x {steps_per_proc} env steps, 1 env each, uniform-random legal "
+                       f"policy with autoreset ({sum(r[2] for r in res)} episodes); reference Python "
+                       "engine measured at 5.4k steps/s/core in SURVEY.md §6")}
+
+
+def load_pmc_traffic(players, tables):
+    """HBM bytes per step launch from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(REPO, "profiles", "pmc_step_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("players") == players and d.get("tables") == tables:
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
+    except (OSError, ValueError):
+        pass
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--tables", type=int, default=65536, help="tables per GPU")
+    ap.add_argument("--players", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-steps", type=int, default=1_000_000, help="env steps per CPU process")
+    args = ap.parse_args()
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rank_env = int(os.environ.get("RANK", "0"))
+    cpu = None
+    if world_env == 1 and rank_env == 0 and not args.no_cpu_baseline:
+        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+        cpu = cpu_baseline(args.players, procs, args.cpu_steps)
+
+    import torch
+    from splendor_gym import _native
+    from splendor_gym.device import Engine
+    from splendor_gym.parallel import barrier, gather_returns, init_distributed, max_over_ranks
+
+    rank, world, local = init_distributed()
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    T, P = args.tables, args.players
+    table0 = rank * T
+    eng = Engine(T, P, device=dev, refill_period=0, table0=table0)
+    eng.reset(seeds=range(table0, table0 + T))
+    lib = eng.lib
+    buf = [torch.zeros(T, dtype=torch.int32, device=dev) for _ in range(2)]
+    eng.sample_uniform(out=buf[0], seed=args.seed, ply=0)
+    ep_ret = torch.zeros(T, dtype=torch.float32, device=dev)
+    ep_cnt = torch.zeros(T, dtype=torch.int32, device=dev)
+
+    def mkargs(a_in, a_out):
+        return _native.StepArgs(actions=a_in.data_ptr(), obs=eng.obs.data_ptr(), mask=eng.mask.data_ptr(),
+                                reward=eng.reward.data_ptr(), terminated=eng.terminated.data_ptr(),
+                                flags=eng.flags.data_ptr(), winner=eng.winner.data_ptr(),
+                                final_obs=eng.final_obs.data_ptr(), autoreset=1, next_actions=a_out.data_ptr(),
+                                policy_seed=args.seed, ply=0, table0=table0, ep_return=ep_ret.data_ptr(),
+                                ep_count=ep_cnt.data_ptr())
+
+    step_args = [mkargs(buf[0], buf[1]), mkargs(buf[1], buf[0])]
+    ctx, desc = eng.ctx, ctypes.byref(eng.desc)
+    stream = eng.stream()
+
+    def run(k0, k1, ev=None):
+        for k in range(k0, k1):
+            sa = step_args[k & 1]
+            sa.ply = k + 1
+            if ev is not None:
+                ev[0][k - k0].record()
+            _native.check(lib, lib.spl_step(ctx, desc, ctypes.byref(sa), stream))
+            if ev is not None:
+                ev[1][k - k0].record()
+            if (k + 1) % REFILL_EVERY == 0:
+                _native.check(lib, lib.spl_refill(ctx, desc, stream))
+
+    run(0, args.warmup)
+    K = args.steps
+    ev = ([torch.cuda.Event(enable_timing=True) for _ in range(K)],
+          [torch.cuda.Event(enable_timing=True) for _ in range(K)])
+    barrier(dev)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(args.warmup, args.warmup + K, ev)
+    torch.cuda.synchronize(dev)
+    barrier(dev)
+    elapsed = time.perf_counter() - t0
+    elapsed_max = max_over_ranks(elapsed, device=dev)
+    kern_ms = [ev[0][k].elapsed_time(ev[1][k]) for k in range(K)]
+    kern_avg_s = sum(kern_ms) / K / 1e3
+    # correctness canaries on the measured run: no error flags, episodes completed
+    bad = int(((eng.flags & (_native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT)) != 0).sum().item())
+    rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
+    episodes = int(cnts.sum().item())
+
+    if rank == 0:
+        total_steps = T * world * K
+        value = total_steps / elapsed_max
+        algo_bytes = ALGO_BYTES[P] * T
+        achieved = algo_bytes / kern_avg_s / 1e9
+        traffic, traffic_src = load_pmc_traffic(P, T)
+        out = {
+            "metric": f"env-steps/sec (whole node), {P}p {T} tables/GPU",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic: seeded deals (table id = env seed), device uniform-random legal policy",
+            "config": {"workload": f"{P}-player SplendorEnv.step x {T} tables per GPU, legal mask + uniform-random "
+                                   "policy, same-step autoreset, obs int32[297] + mask int8[45] per table-step",
+                       "tables_per_gpu": T, "players": P, "parallelism": f"table-sharded x{world}",
+                       "refill_every": REFILL_EVERY},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": f"spl::k_step<{P}>", "kernel_avg_us": round(kern_avg_s * 1e6, 2),
+                         "algo_bytes_per_launch": algo_bytes},
+            "cpu_baseline": cpu,
+            "episodes": episodes,
+            "mean_final_reward_p0": round(float(rets.sum().item()) / max(1, episodes), 4),
+            "error_flags": bad,
+        }
+        print(json.dumps(out))
+    eng.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
