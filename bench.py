@@ -31,7 +31,7 @@ for _p in (REPO, os.path.join(REPO, "splendor-gym_amd")):
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 ALGO_BYTES = {2: 1370, 3: 1408, 4: 1446}  # 2*S_P + 297*4 + 45 + 4 + 4 + 1 (3p interpolated)
-REFILL_EVERY = 8
+REFILL_EVERY = 16  # pool refill period; random 2p games last >= 24 plies, so no inline deals
 
 
 def cpu_baseline(players, procs, steps_per_proc):
@@ -85,14 +85,16 @@ def load_pmc_traffic(players, tables):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=1024)
+    ap.add_argument("--warmup", type=int, default=96)
     ap.add_argument("--tables", type=int, default=65536, help="tables per GPU")
     ap.add_argument("--players", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--cpu-steps", type=int, default=1_000_000, help="env steps per CPU process")
+    ap.add_argument("--graph-steps", type=int, default=64,
+                    help="steps per captured HIP graph (multiple of 32); 0 = eager launches")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -121,45 +123,82 @@ def main():
     eng.sample_uniform(out=buf[0], seed=args.seed, ply=0)
     ep_ret = torch.zeros(T, dtype=torch.float32, device=dev)
     ep_cnt = torch.zeros(T, dtype=torch.int32, device=dev)
+    ply_base = torch.zeros(1, dtype=torch.int64, device=dev)  # policy counter base, advanced per replay
 
     def mkargs(a_in, a_out):
         return _native.StepArgs(actions=a_in.data_ptr(), obs=eng.obs.data_ptr(), mask=eng.mask.data_ptr(),
                                 reward=eng.reward.data_ptr(), terminated=eng.terminated.data_ptr(),
                                 flags=eng.flags.data_ptr(), winner=eng.winner.data_ptr(),
                                 final_obs=eng.final_obs.data_ptr(), autoreset=1, next_actions=a_out.data_ptr(),
-                                policy_seed=args.seed, ply=0, table0=table0, ep_return=ep_ret.data_ptr(),
+                                ply_base=ply_base.data_ptr(), policy_seed=args.seed, ply=0, table0=table0,
+                                ep_return=ep_ret.data_ptr(),
                                 ep_count=ep_cnt.data_ptr())
 
     step_args = [mkargs(buf[0], buf[1]), mkargs(buf[1], buf[0])]
     ctx, desc = eng.ctx, ctypes.byref(eng.desc)
     stream = eng.stream()
 
-    def run(k0, k1, ev=None):
+    def run(k0, k1, strm, ev=None):
+        """Steps k0..k1-1 (ply k+1 relative to ply_base), refill every REFILL_EVERY steps."""
         for k in range(k0, k1):
             sa = step_args[k & 1]
             sa.ply = k + 1
             if ev is not None:
                 ev[0][k - k0].record()
-            _native.check(lib, lib.spl_step(ctx, desc, ctypes.byref(sa), stream))
+            _native.check(lib, lib.spl_step(ctx, desc, ctypes.byref(sa), strm))
             if ev is not None:
                 ev[1][k - k0].record()
             if (k + 1) % REFILL_EVERY == 0:
-                _native.check(lib, lib.spl_refill(ctx, desc, stream))
+                _native.check(lib, lib.spl_refill(ctx, desc, strm))
 
-    run(0, args.warmup)
+    W = (args.warmup // (2 * REFILL_EVERY)) * (2 * REFILL_EVERY)  # action-buffer / refill-list parity
+    run(0, W, stream)
     K = args.steps
-    ev = ([torch.cuda.Event(enable_timing=True) for _ in range(K)],
-          [torch.cuda.Event(enable_timing=True) for _ in range(K)])
+    G = args.graph_steps
+    graph, mode = None, "eager"
+    if G > 0:
+        if G % (2 * REFILL_EVERY) or K % G:
+            raise SystemExit("--graph-steps must be a multiple of 32 that divides --steps")
+        try:
+            torch.cuda.synchronize(dev)
+            ply_base.fill_(W)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                cap = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+                run(0, G, cap)
+                ply_base.add_(G)
+            mode = f"hipGraph replays of {G} steps"
+        except Exception as exc:  # capture unsupported: time eager launches instead
+            print(f"graph capture failed ({exc}); timing eager launches", file=sys.stderr)
+            graph, G = None, 0
     barrier(dev)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    run(args.warmup, args.warmup + K, ev)
+    if graph is not None:
+        for _ in range(K // G):
+            graph.replay()
+        ev = None
+    else:
+        ev = ([torch.cuda.Event(enable_timing=True) for _ in range(K)],
+              [torch.cuda.Event(enable_timing=True) for _ in range(K)])
+        run(W, W + K, stream, ev)
     torch.cuda.synchronize(dev)
     barrier(dev)
     elapsed = time.perf_counter() - t0
     elapsed_max = max_over_ranks(elapsed, device=dev)
-    kern_ms = [ev[0][k].elapsed_time(ev[1][k]) for k in range(K)]
-    kern_avg_s = sum(kern_ms) / K / 1e3
+    if ev is None:
+        # ROCm rejects timing events as graph nodes ("External events are disallowed"), so the
+        # step-kernel duration comes from HIP events around each launch of an eager window of
+        # the same loop, run right after the timed replays on the same stream and state.
+        nwin = 64
+        ev = ([torch.cuda.Event(enable_timing=True) for _ in range(nwin)],
+              [torch.cuda.Event(enable_timing=True) for _ in range(nwin)])
+        ply_base.fill_(W + K + 1)
+        run(0, nwin, stream, ev)
+        torch.cuda.synchronize(dev)
+    nev = len(ev[0])
+    kern_ms = [ev[0][k].elapsed_time(ev[1][k]) for k in range(nev)]
+    kern_avg_s = sum(kern_ms) / nev / 1e3
     # correctness canaries on the measured run: no error flags, episodes completed
     bad = int(((eng.flags & (_native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT)) != 0).sum().item())
     rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
@@ -187,11 +226,13 @@ def main():
             "config": {"workload": f"{P}-player SplendorEnv.step x {T} tables per GPU, legal mask + uniform-random "
                                    "policy, same-step autoreset, obs int32[297] + mask int8[45] per table-step",
                        "tables_per_gpu": T, "players": P, "parallelism": f"table-sharded x{world}",
-                       "refill_every": REFILL_EVERY},
+                       "refill_every": REFILL_EVERY, "launch": mode},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": f"spl::k_step<{P}>", "kernel_avg_us": round(kern_avg_s * 1e6, 2),
+                         "kernel_timing": ("HIP events around each launch in the timed region" if mode == "eager" else
+                                           f"HIP events around each of {nev} eager launches right after the timed replays"),
                          "algo_bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,
             "episodes": episodes,

@@ -68,6 +68,7 @@ typedef struct spl_arena_s {
     int32_t n;            /* tables */
     int32_t players;      /* 2..4 */
     int64_t steps;        /* maintained by the library: spl_step calls since the last reset */
+    int64_t epoch;        /* maintained by the library: pool refills so far (list parity) */
 } spl_arena_t;
 
 /* Batched step arguments (all device pointers; [n] = one entry per table). */
@@ -82,6 +83,7 @@ typedef struct spl_step_args_s {
     int32_t *final_obs;      /* [n][297] or NULL: terminal obs, written on SPL_F_RESET rows  */
     int32_t autoreset;       /* 1: terminated tables are re-dealt in the same step          */
     int32_t *next_actions;   /* [n] or NULL: fused uniform-random policy over the new mask   */
+    const uint64_t *ply_base; /* device, nullable: added to `ply` (lets a captured graph replay) */
     uint64_t policy_seed;    /* Philox key for next_actions                                  */
     uint64_t ply;            /* Philox counter for next_actions                              */
     int64_t table0;          /* global id of table 0 (sharding: streams keyed by global id) */

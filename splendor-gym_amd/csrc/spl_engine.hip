@@ -34,8 +34,9 @@ struct KArena {
     uint32_t *planes;
     uint8_t *slots;
     uint8_t *pcg;
-    uint32_t *needy;  // [0] = count, [1..n] = table ids
+    uint32_t *needy;  // [0], [1] = list counts; lists of table ids at needy + 64 (+ n for list 1)
     int n;
+    int epoch;        // parity selects the list that steps append to and the refill consumes
 };
 
 struct KTables {
@@ -56,6 +57,7 @@ struct KStep {
     int32_t *next_actions;
     float *ep_return;
     uint32_t *ep_count;
+    const uint64_t *ply_base;  // nullable: device counter added to `ply` (graph replays)
     uint64_t policy_seed;
     uint64_t ply;
     int64_t table0;
@@ -63,6 +65,14 @@ struct KStep {
 };
 
 constexpr int kObsDim = 297;
+
+// Ablation switches for profiling builds only (tools/ablate.py); the product build defines none.
+#ifndef SPL_ABL
+#define SPL_ABL 0
+#endif
+constexpr int ABL_LEGAL_PRE = 1, ABL_APPLY = 2, ABL_LEGAL_POST = 4, ABL_FINAL = 8, ABL_RESET = 16, ABL_ENCODE = 32,
+              ABL_STORE = 64;
+__device__ __forceinline__ bool abl(int bit) { return (SPL_ABL & bit) != 0; }
 constexpr int kScratchStride = 112;  // per-lane deal scratch in LDS (16-aligned)
 
 struct __align__(16) BlockLDS {
@@ -221,6 +231,40 @@ __device__ __forceinline__ uint64_t legal_mask(const uint32_t *sw, const Pl &p, 
     for (int i = 0; i < 3; ++i)  // :89-91
         m |= (uint64_t)(i < p.nres && afford(p, card_rec(L, p.res[i]))) << (42 + i);
     return m;
+}
+
+// engine/rules.py:40-93 restricted to one action (the env only needs mask[a]) ...
+__device__ __forceinline__ bool action_legal(const uint32_t *sw, const Pl &p, const int bank[6], int a,
+                                             const BlockLDS &L) {
+    if (a < 10) {
+        uint32_t avail = 0;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) avail |= (bank[c] >= 1 ? 1u : 0u) << c;
+        const int nav = __popc(avail);
+        const uint32_t cm = take3_mask(a);
+        return nav >= 3 ? ((cm & avail) == cm) : (nav >= 1 && (avail & cm) == avail);
+    }
+    if (a < 15) {
+        const int c = a - 10;
+        const int b = c == 0 ? bank[0] : (c == 1 ? bank[1] : (c == 2 ? bank[2] : (c == 3 ? bank[3] : bank[4])));
+        return b >= 4;
+    }
+    if (a < 27) {
+        const int id = board_get(sw, a - 15);
+        return id != 0xFF && afford(p, card_rec(L, id));
+    }
+    if (a < 39) return p.nres < 3 && board_get(sw, a - 27) != 0xFF;
+    if (a < 42) return p.nres < 3 && bget(sw[SW_DECK], a - 39) > 0;
+    const int i = a - 42;
+    const int r0 = opaque(p.res[0]), r1 = opaque(p.res[1]), r2 = opaque(p.res[2]);
+    return i < p.nres && afford(p, card_rec(L, i == 0 ? r0 : (i == 1 ? r1 : r2)));
+}
+
+// ... and whether ANY move is legal: with a non-gold colour in the bank some take-3 always is
+// (rules.py:45-58), otherwise fall back to the full mask (rare).
+__device__ __forceinline__ bool any_legal(const uint32_t *sw, const Pl &p, const int bank[6], const BlockLDS &L) {
+    const bool some_colour = bank[0] > 0 || bank[1] > 0 || bank[2] > 0 || bank[3] > 0 || bank[4] > 0;
+    return some_colour || legal_mask(sw, p, bank, L) != 0ull;
 }
 
 // engine/rules.py:101-122 _pay_for_card
@@ -574,11 +618,25 @@ __device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *row, const 
 }
 
 // Block store of this wave's staged rows: obs[t0 .. t0+rows) as int32, 16 B per lane-store.
+// LDS reads are issued in groups of 5 before their stores: one read-wait per store halves the
+// store rate (tools/microbench_store.hip: 2.7 -> 5.2 TB/s).
 __device__ __forceinline__ void store_obs_block(const BlockLDS &L, int rows, int32_t *dst) {
     const int nbytes = rows * kObsDim;
     const int full = nbytes >> 2;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(L.rows);
-    for (int d = lane_id(); d < full; d += 64) {
+    constexpr int U = 5;
+    int d = lane_id();
+    for (; d + 64 * (U - 1) < full; d += 64 * U) {
+        uint32_t w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            *reinterpret_cast<int4 *>(dst + 4 * (d + 64 * u)) =
+                make_int4((int)(w[u] & 0xFFu), (int)((w[u] >> 8) & 0xFFu), (int)((w[u] >> 16) & 0xFFu),
+                          (int)(w[u] >> 24));
+    }
+    for (; d < full; d += 64) {
         const uint32_t w = src[d];
         *reinterpret_cast<int4 *>(dst + 4 * d) =
             make_int4((int)(w & 0xFFu), (int)((w >> 8) & 0xFFu), (int)((w >> 16) & 0xFFu), (int)(w >> 24));
@@ -586,23 +644,35 @@ __device__ __forceinline__ void store_obs_block(const BlockLDS &L, int rows, int
     for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) dst[b] = (int32_t)L.rows[b];
 }
 
-// Block store of this wave's masks: mask[t0 .. t0+rows) as int8 [rows][45].
+// Block store of this wave's masks: mask[t0 .. t0+rows) as int8 [rows][45], 4 bytes per lane-store.
+__device__ __forceinline__ uint32_t mask_dword(const BlockLDS &L, int d, int nbytes) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int b = 4 * d + q;
+        const int r = b / 45, c = b - 45 * r;
+        const uint32_t bit = b < nbytes ? (uint32_t)((L.mask[r < 64 ? r : 63] >> c) & 1ull) : 0u;
+        v |= bit << (8 * q);
+    }
+    return v;
+}
+
 __device__ __forceinline__ void store_mask_block(const BlockLDS &L, int rows, int8_t *dst) {
     const int nbytes = rows * 45;
-    for (int d = lane_id(); 4 * d < nbytes; d += 64) {
-        uint32_t v = 0;
+    const int full = nbytes >> 2;
+    constexpr int U = 4;
+    int d = lane_id();
+    for (; d + 64 * (U - 1) < full; d += 64 * U) {
+        uint32_t v[U];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int b = 4 * d + q;
-            const int r = b / 45, c = b - 45 * r;
-            const uint32_t bit = b < nbytes ? (uint32_t)((L.mask[r < 64 ? r : 63] >> c) & 1ull) : 0u;
-            v |= bit << (8 * q);
-        }
-        if (4 * d + 3 < nbytes) {
-            *reinterpret_cast<uint32_t *>(dst + 4 * d) = v;
-        } else {
-            for (int q = 0; 4 * d + q < nbytes; ++q) dst[4 * d + q] = (int8_t)(v >> (8 * q));
-        }
+        for (int u = 0; u < U; ++u) v[u] = mask_dword(L, d + 64 * u, nbytes);
+#pragma unroll
+        for (int u = 0; u < U; ++u) *reinterpret_cast<uint32_t *>(dst + 4 * (d + 64 * u)) = v[u];
+    }
+    for (; d < full; d += 64) *reinterpret_cast<uint32_t *>(dst + 4 * d) = mask_dword(L, d, nbytes);
+    for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) {
+        const int r = b / 45;
+        dst[b] = (int8_t)((L.mask[r] >> (b - 45 * r)) & 1ull);
     }
 }
 
@@ -619,28 +689,27 @@ __device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec
     ms.init(seed);
     int d = 0, base = 0, i = 39;
     uint32_t flags = 0;
+    uint32_t y = ms.next(0);
     for (int j = 0;; ++j) {
-        const bool done = d >= 4;
-        if (!__any(!done)) break;
+        if (!__any(d < 4)) break;
         if (j >= MTStream::kMaxOut) {
-            if (!done) flags |= SPL_F_RNG_LIMIT;
+            if (d < 4) flags |= SPL_F_RNG_LIMIT;
             break;
         }
-        const uint32_t y = ms.next(j);
-        if (!done) {
-            const int n = i + 1;
-            const int r = (int)(y >> (32 - bit_length((uint32_t)n)));
-            if (r < n) {
-                const uint8_t xi = scr[base + i], xr = scr[base + r];
-                scr[base + i] = xr;
-                scr[base + r] = xi;
-                if (--i == 0) {
-                    ++d;
-                    base = d == 1 ? 40 : (d == 2 ? 70 : 90);
-                    i = d == 1 ? 29 : (d == 2 ? 19 : 9);
-                }
-            }
-        }
+        // _randbelow(i + 1) on output j; a rejected draw (or a finished lane) swaps x[i] with itself
+        const int n = i + 1;
+        const int r = (int)(y >> (32 - bit_length((uint32_t)n)));
+        const bool acc = d < 4 && r < n;
+        const int ai = base + i, ar = base + (acc ? r : i);
+        const uint8_t xi = scr[ai], xr = scr[ar];
+        if (j + 1 < MTStream::kMaxOut) y = ms.next(j + 1);  // overlaps the LDS reads
+        scr[ai] = xr;
+        scr[ar] = xi;
+        const int i2 = acc ? i - 1 : i;
+        const bool adv = acc && i2 == 0;  // deck finished: tier 2, tier 3, then the nobles
+        d += adv ? 1 : 0;
+        base = adv ? (d == 1 ? 40 : (d == 2 ? 70 : 90)) : base;
+        i = adv ? (d == 1 ? 29 : (d == 2 ? 19 : 9)) : i2;
     }
     // deck bytes (list order; the 4 dealt cards per tier sit past deck_len)
     const uint4 *s4 = reinterpret_cast<const uint4 *>(scr);
@@ -707,16 +776,22 @@ __device__ __forceinline__ void store_pcg(const KArena &A, int t, const Pcg64 &g
     q[1] = g.u32;
 }
 
-// queue `t` for a pool refill (wave-aggregated: one atomic per wave)
-__device__ __forceinline__ void push_needy(uint32_t *needy, bool want, uint32_t t) {
+__device__ __forceinline__ uint32_t *needy_list(const KArena &A, int parity) {
+    return A.needy + 64 + (size_t)parity * A.n;
+}
+
+// queue `t` for the next pool refill (wave-aggregated: one atomic per wave).  Refill epochs
+// alternate between two lists so the refill kernel can zero the other list's count itself.
+__device__ __forceinline__ void push_needy(const KArena &A, bool want, uint32_t t) {
     const uint64_t b = __ballot(want);
     if (b == 0) return;
     const int leader = __ffsll((unsigned long long)b) - 1;
+    const int par = A.epoch & 1;
     uint32_t base = 0;
-    if (lane_id() == leader) base = atomicAdd(&needy[0], (uint32_t)__popcll(b));
+    if (lane_id() == leader) base = atomicAdd(&A.needy[par], (uint32_t)__popcll(b));
     base = __shfl(base, leader);
     const int rank = __popcll(b & ((1ull << lane_id()) - 1ull));
-    if (want) needy[1 + base + rank] = t;
+    if (want) needy_list(A, par)[base + rank] = t;
 }
 
 // reset() without a seed / same-step autoreset: the next episode is the pool deal
@@ -855,21 +930,29 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
         if (is_terminal(T.sw)) {                                  // :53-54 RuntimeError
             flags = SPL_F_AFTER_TERMINAL;
         } else {
-            const uint64_t m = legal_of(T, L);                    // :55
-            if (m == 0) {                                         // :56-61 no legal move: draw
+            // :55 mask = legal_moves(state): only "any legal?" and mask[action] are needed here
+            uint32_t pw4[4];
+            get_player(T, get_to_play(T.sw), pw4);
+            const Pl cur = unpack_pl(pw4);
+            int bank[6];
+            get_bank(T.sw, bank);
+            const bool in_range = action >= 0 && action < SPL_NUM_ACTIONS;
+            const bool anyl = abl(ABL_LEGAL_PRE) || any_legal(T.sw, cur, bank, L);
+            const bool ok = abl(ABL_LEGAL_PRE) || (in_range && action_legal(T.sw, cur, bank, action, L));
+            if (!anyl) {                                          // :56-61 no legal move: draw
                 T.sw[SW_MISC] = (T.sw[SW_MISC] | ST_GAME_OVER) & 0x00FFFFFFu;
                 T.sw[SW_BANK1] &= 0xFF00FFFFu;                    // to_play = 0
                 term = true;
                 flags = SPL_F_DRAW;
-            } else if (action < 0 || action >= SPL_NUM_ACTIONS) { // :62-63 ValueError
+            } else if (!in_range) {                               // :62-63 ValueError
                 flags = SPL_F_OOB;
-                outmask = m;
-            } else if (!((m >> action) & 1ull)) {                 // :64-66 illegal
+                outmask = legal_mask(T.sw, cur, bank, L);
+            } else if (!ok) {                                     // :64-66 illegal
                 flags = SPL_F_ILLEGAL;
                 reward = -0.01f;
-                outmask = m;
+                outmask = legal_mask(T.sw, cur, bank, L);
             } else {
-                apply_action(T, action, live, L, Tb.lut, flags);  // :68
+                if (!abl(ABL_APPLY)) apply_action(T, action, live, L, Tb.lut, flags);  // :68
                 term = is_terminal(T.sw);                         // :70
                 if (term) {                                       // :71-80
                     const int w = get_winner(T.sw);
@@ -877,15 +960,36 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
                     reward = (w < 0 && tl) ? -0.1f : (w < 0 ? 0.0f : (w == P - 1 ? 1.0f : -1.0f));
                     flags |= tl ? SPL_F_TURN_LIMIT : 0u;          // :82-83
                 } else {
-                    outmask = legal_of(T, L);                     // :81
+                    outmask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);  // :81
                 }
             }
         }
     }
     const int8_t wnr = (int8_t)get_winner(T.sw);
 
+    // same-step autoreset: start the pool-record loads and the refill-queue slot now, consume
+    // them after the final-observation block so their latency hides behind it
+    const bool do_reset = valid && term && S.autoreset && !abl(ABL_RESET);
+    const int nxt = ((T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0) ^ 1;
+    uint8_t *prec = slot_rec(A, do_reset ? t : 0, nxt);
+    uint32_t p_ready = 1u;
+    uint4 p_tail0 = make_uint4(0u, 0u, 0u, 0u), p_tail1 = make_uint4(0u, 0u, 0u, 0u);
+    if (do_reset) {
+        p_ready = reinterpret_cast<const uint32_t *>(prec)[kRecReady / 4];
+        p_tail0 = *reinterpret_cast<const uint4 *>(prec + kRecBoard);
+        p_tail1 = *reinterpret_cast<const uint4 *>(prec + kRecNob0);
+    }
+    const bool push = do_reset && !(T.sw[SW_MISC] & ST_PENDING);
+    const uint64_t pushb = __ballot(push);
+    const int par = A.epoch & 1;
+    uint32_t qbase = 0;
+    if (pushb) {
+        const int leader = __ffsll((unsigned long long)pushb) - 1;
+        if (lane == leader) qbase = atomicAdd(&A.needy[par], (uint32_t)__popcll(pushb));
+    }
+
     // terminal observations for gymnasium's info["final_observation"]
-    const bool want_final = S.autoreset && S.final_obs != nullptr;
+    const bool want_final = S.autoreset && S.final_obs != nullptr && !abl(ABL_FINAL);
     const uint64_t fin = __ballot(valid && term && want_final);
     if (fin) {
         if (valid && term) encode_row(T, &L.rows[lane * kObsDim], L);
@@ -908,22 +1012,36 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
         if (S.ep_count) S.ep_count[t] += 1u;
         if (want_final && get_moves(T.sw) > 255) S.final_obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
     }
-    // same-step autoreset from the pool
-    bool push = false;
-    if (valid && term && S.autoreset) {
-        flags |= SPL_F_RESET | reset_from_pool(T, A, t, &L.rows[lane * kScratchStride], push);
+    if (pushb) {  // refill queue entry (wave-aggregated atomic issued above)
+        const int leader = __ffsll((unsigned long long)pushb) - 1;
+        qbase = __shfl(qbase, leader);
+        if (push) needy_list(A, par)[qbase + __popcll(pushb & ((1ull << lane) - 1ull))] = (uint32_t)t;
+    }
+    if (do_reset) {  // envs/splendor_env.py:43-44 with the continued np_random stream
+        if (p_ready == 0u) {  // pool not refilled yet: deal inline (correct, just slower)
+            Pcg64 g = load_pcg(A, t);
+            const uint32_t seed = g.engine_seed();
+            store_pcg(A, t, g);
+            flags |= deal_into(seed, P, prec, &L.rows[lane * kScratchStride]);
+            p_tail0 = *reinterpret_cast<const uint4 *>(prec + kRecBoard);
+            p_tail1 = *reinterpret_cast<const uint4 *>(prec + kRecNob0);
+        }
+        reinterpret_cast<uint32_t *>(prec)[kRecReady / 4] = 0u;  // now live
+        fresh_state(T, (nxt ? ST_ACTIVE : 0u) | ST_PENDING, p_tail0, p_tail1);
+        flags |= SPL_F_RESET;
         outmask = legal_of(T, L);
     }
-    push_needy(A.needy, push, (uint32_t)t);
     __syncthreads();  // deal scratch (rows) free again
 
     // observation + mask of the current state, block stores
-    encode_row(T, &L.rows[lane * kObsDim], L);
+    if (!abl(ABL_ENCODE)) encode_row(T, &L.rows[lane * kObsDim], L);
     L.mask[lane] = outmask;
     __syncthreads();
     int32_t *obs_dst = S.obs + (size_t)t0 * kObsDim;
-    store_obs_block(L, rows, obs_dst);
-    store_mask_block(L, rows, S.mask + (size_t)t0 * 45);
+    if (!abl(ABL_STORE)) {
+        store_obs_block(L, rows, obs_dst);
+        store_mask_block(L, rows, S.mask + (size_t)t0 * 45);
+    }
     if (__any(valid && get_moves(T.sw) > 255)) {
         __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): block store of this dword has left
         if (valid && get_moves(T.sw) > 255) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
@@ -933,8 +1051,10 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
         S.terminated[t] = term ? 1 : 0;
         S.flags[t] = (uint8_t)flags;
         if (S.winner) S.winner[t] = wnr;
-        if (S.next_actions)
-            S.next_actions[t] = sample_uniform(outmask, S.policy_seed, (uint64_t)(S.table0 + t), S.ply);
+        if (S.next_actions) {
+            const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
+            S.next_actions[t] = sample_uniform(outmask, S.policy_seed, (uint64_t)(S.table0 + t), ply);
+        }
         store_tab(T, A, t);
     }
 }
@@ -981,7 +1101,7 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
             reset_from_pool(T, A, t, scr, push);
         }
     }
-    push_needy(A.needy, push, (uint32_t)t);
+    push_needy(A, push, (uint32_t)t);
     __syncthreads();
     if (obs || mask_out) {
         encode_row(T, &L.rows[lane * kObsDim], L);
@@ -999,11 +1119,13 @@ template <int P>
 __global__ __launch_bounds__(64) void k_refill(KArena A) {
     __shared__ uint8_t scr_all[64 * kScratchStride] __attribute__((aligned(16)));
     const int lane = lane_id();
-    const uint32_t count = A.needy[0];
+    const int par = A.epoch & 1;
+    const uint32_t count = A.needy[par];
+    if (blockIdx.x == 0 && lane == 0) A.needy[par ^ 1] = 0u;  // the next epoch appends there
     const uint32_t e = blockIdx.x * 64u + (uint32_t)lane;
     if (blockIdx.x * 64u >= count) return;  // whole wave idle
     if (e < count) {
-        const int t = (int)A.needy[1 + e];
+        const int t = (int)needy_list(A, par)[e];
         const size_t mi = (size_t)SW_MISC * A.n + t;
         const uint32_t misc = A.planes[mi];
         const int nxt = ((misc & ST_ACTIVE) ? 1 : 0) ^ 1;
@@ -1228,7 +1350,7 @@ static KArena karena(const spl_arena_t *a) {
     const ArenaLayout L = arena_layout(a->n, a->players);
     uint8_t *b = static_cast<uint8_t *>(a->base);
     return KArena{reinterpret_cast<uint32_t *>(b + L.planes), b + L.slots, b + L.pcg,
-                  reinterpret_cast<uint32_t *>(b + L.needy), a->n};
+                  reinterpret_cast<uint32_t *>(b + L.needy), a->n, (int)(a->epoch & 1)};
 }
 
 static int launch_check() {
@@ -1356,6 +1478,7 @@ int spl_arena_init(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
     HIP_TRY(hipMemsetAsync(arena->base, 0, (size_t)spl_arena_bytes(arena->n, arena->players),
                            static_cast<hipStream_t>(stream)));
     arena->steps = 0;
+    arena->epoch = 0;
     return SPL_OK;
 }
 
@@ -1365,7 +1488,7 @@ int spl_refill(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
     hipStream_t s = static_cast<hipStream_t>(stream);
     DISPATCH_P(arena->players, hipLaunchKernelGGL(k_refill<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A));
     if (int r = launch_check()) return r;
-    HIP_TRY(hipMemsetAsync(A.needy, 0, sizeof(uint32_t), s));
+    arena->epoch += 1;
     return SPL_OK;
 }
 
@@ -1388,6 +1511,7 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     S.next_actions = a->next_actions;
     S.ep_return = a->ep_return;
     S.ep_count = a->ep_count;
+    S.ply_base = a->ply_base;
     S.policy_seed = a->policy_seed;
     S.ply = a->ply;
     S.table0 = a->table0;

@@ -77,7 +77,7 @@ __host__ __device__ inline ArenaLayout arena_layout(int64_t n, int P) {
     L.slots = align256(L.planes + (int64_t)num_words(P) * n * 4);
     L.pcg = align256(L.slots + n * 2 * kSlotBytes);
     L.needy = align256(L.pcg + n * kPcgBytes);
-    L.total = align256(L.needy + (n + 1) * 4);
+    L.total = align256(L.needy + (64 + 2 * n) * 4);  // 2 counts (+pad), 2 lists
     return L;
 }
 

@@ -24,7 +24,10 @@ struct MTBase {
         for (int i = 1; i < 624; ++i) v[i] = 1812433253u * (v[i - 1] ^ (v[i - 1] >> 30)) + (uint32_t)i;
     }
 };
-__constant__ MTBase kMTBase = MTBase();
+// Only three entries are ever needed directly (cursor start points); the rest is regenerated.
+constexpr uint32_t kMTB0 = MTBase().v[0];
+constexpr uint32_t kMTB1 = MTBase().v[1];
+constexpr uint32_t kMTB396 = MTBase().v[396];
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     y ^= (y >> 11);
@@ -39,14 +42,22 @@ __device__ __forceinline__ uint32_t mt_tw(uint32_t x, uint32_t y) {
     return ((((x & 0x80000000u) | (y & 0x7fffffffu)) >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u));
 }
 
+// init_genrand's recurrence: b_i from b_{i-1}.  Cursors regenerate the base table on the fly
+// instead of loading it: b is wave-uniform, so it lives in SGPRs and runs on the scalar unit
+// beside the vector chains (a scalar load per step would expose its latency every iteration).
+__device__ __forceinline__ uint32_t mt_base_next(uint32_t b, int i) {
+    return 1812433253u * (b ^ (b >> 30)) + (uint32_t)i;
+}
+
 // Cursor over the post-init_by_array state s[i], i >= 2, produced in increasing i.
 //   loop 1:  a_i = (b_i ^ ((a_{i-1} ^ a_{i-1} >> 30) * 1664525)) + key[j] + j,  j = (i-1) % keylen
 //   loop 2:  c_i = (a_i ^ ((c_{i-1} ^ c_{i-1} >> 30) * 1566083941)) - i        (= s_i, i >= 2)
 struct MTCursor {
-    uint32_t a, c;
+    uint32_t b, a, c;  // b = b_{i-1} (uniform), a = a_{i-1}, c = c_{i-1}
     __device__ __forceinline__ uint32_t step(int i, uint32_t add_even, uint32_t add_odd) {
         const uint32_t add = ((i - 1) & 1) ? add_odd : add_even;
-        a = (kMTBase.v[i] ^ ((a ^ (a >> 30)) * 1664525u)) + add;
+        b = mt_base_next(b, i);
+        a = (b ^ ((a ^ (a >> 30)) * 1664525u)) + add;
         c = (a ^ ((c ^ (c >> 30)) * 1566083941u)) - (uint32_t)i;
         return c;
     }
@@ -69,25 +80,27 @@ struct MTStream {
         add_even = k0;
         add_odd = two ? k1 + 1u : k0;
         // loop 1 to the end: a_623
-        a1 = (kMTBase.v[1] ^ ((kMTBase.v[0] ^ (kMTBase.v[0] >> 30)) * 1664525u)) + k0;
-        uint32_t a = a1;
+        a1 = (kMTB1 ^ ((kMTB0 ^ (kMTB0 >> 30)) * 1664525u)) + k0;
+        uint32_t a = a1, b = kMTB1;
 #pragma unroll 8
         for (int i = 2; i < 624; ++i) {
             const uint32_t add = ((i - 1) & 1) ? add_odd : add_even;
-            a = (kMTBase.v[i] ^ ((a ^ (a >> 30)) * 1664525u)) + add;
+            b = mt_base_next(b, i);
+            a = (b ^ ((a ^ (a >> 30)) * 1664525u)) + add;
         }
         // 624th loop-1 iteration wraps to i = 1 with mt[0] = a_623, j = 623 % keylen
         a1p = (a1 ^ ((a ^ (a >> 30)) * 1664525u)) + (two ? k1 + 1u : k0);
         // loop 2 to the end: c_623, remembering (a_396, c_396)
-        MTCursor cur{a1, a1p};
-#pragma unroll 8
-        for (int i = 2; i < 624; ++i) {
-            cur.step(i, add_even, add_odd);
-            if (i == 396) { r_a0 = cur.a; r_c0 = cur.c; }
-        }
+        MTCursor cur{kMTB1, a1, a1p};
+#pragma unroll 4
+        for (int i = 2; i < 397; ++i) cur.step(i, add_even, add_odd);
+        r_a0 = cur.a;  // (a_396, c_396)
+        r_c0 = cur.c;
+#pragma unroll 4
+        for (int i = 397; i < 624; ++i) cur.step(i, add_even, add_odd);
         s1 = (a1p ^ ((cur.c ^ (cur.c >> 30)) * 1566083941u)) - 1u;
-        L = MTCursor{a1, a1p};
-        R = MTCursor{r_a0, r_c0};
+        L = MTCursor{kMTB1, a1, a1p};
+        R = MTCursor{kMTB396, r_a0, r_c0};
         sj = 0x80000000u;  // s_0
     }
 
@@ -99,8 +112,8 @@ struct MTStream {
             y = R.step(j + 397, add_even, add_odd) ^ mt_tw(sj, sj1);
         } else {
             if (j == 227) {  // phase B: mt_new[j] = s_{j+170} ^ tw(s_{j-227}, s_{j-226}) ^ tw(s_j, s_{j+1})
-                R = MTCursor{r_a0, r_c0};
-                M = MTCursor{a1, a1p};
+                R = MTCursor{kMTB396, r_a0, r_c0};
+                M = MTCursor{kMTB1, a1, a1p};
                 smj = 0x80000000u;
             }
             const uint32_t smj1 = (j == 227) ? s1 : M.step(j - 226, add_even, add_odd);

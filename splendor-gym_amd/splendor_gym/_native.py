@@ -25,7 +25,7 @@ c_void_p, c_int32, c_int64, c_uint64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c
 class ArenaDesc(ctypes.Structure):
     """spl_arena_t"""
     _fields_ = [("base", c_void_p), ("bytes", c_int64), ("n", c_int32), ("players", c_int32),
-                ("steps", c_int64)]
+                ("steps", c_int64), ("epoch", c_int64)]
 
 
 class StepArgs(ctypes.Structure):
@@ -33,7 +33,7 @@ class StepArgs(ctypes.Structure):
     _fields_ = [("actions", c_void_p), ("obs", c_void_p), ("mask", c_void_p), ("reward", c_void_p),
                 ("terminated", c_void_p), ("flags", c_void_p), ("winner", c_void_p),
                 ("final_obs", c_void_p), ("autoreset", c_int32), ("next_actions", c_void_p),
-                ("policy_seed", c_uint64), ("ply", c_uint64), ("table0", c_int64),
+                ("ply_base", c_void_p), ("policy_seed", c_uint64), ("ply", c_uint64), ("table0", c_int64),
                 ("ep_return", c_void_p), ("ep_count", c_void_p)]
 
 

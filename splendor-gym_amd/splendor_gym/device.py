@@ -45,7 +45,7 @@ class Engine:
         self._arena_raw = torch.zeros(nbytes + 256, dtype=torch.uint8, device=dev)
         off = (-self._arena_raw.data_ptr()) % 256
         self.arena = self._arena_raw[off:off + nbytes]
-        self.desc = ArenaDesc(self.arena.data_ptr(), nbytes, self.n, self.P, 0)
+        self.desc = ArenaDesc(self.arena.data_ptr(), nbytes, self.n, self.P, 0, 0)
         n = self.n
         self.obs = torch.zeros((n, OBS_DIM), dtype=torch.int32, device=dev)
         self.mask = torch.zeros((n, NUM_ACTIONS), dtype=torch.int8, device=dev)
@@ -99,7 +99,7 @@ class Engine:
         return self.obs, self.mask
 
     def step(self, actions=None, autoreset=True, final_obs=True, next_actions=None, policy_seed=0, ply=0,
-             ep_return=None, ep_count=None):
+             ep_return=None, ep_count=None, ply_base=None):
         """One env step on every table (SplendorEnv.step semantics per table)."""
         torch = self.torch
         if actions is None:
@@ -115,6 +115,7 @@ class Engine:
                      final_obs=self.final_obs.data_ptr() if (final_obs and autoreset) else None,
                      autoreset=1 if autoreset else 0,
                      next_actions=None if next_actions is None else next_actions.data_ptr(),
+                     ply_base=None if ply_base is None else ply_base.data_ptr(),
                      policy_seed=int(policy_seed) & (2**64 - 1), ply=int(ply) & (2**64 - 1), table0=self.table0,
                      ep_return=None if ep_return is None else ep_return.data_ptr(),
                      ep_count=None if ep_count is None else ep_count.data_ptr())

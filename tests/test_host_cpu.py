@@ -40,7 +40,7 @@ def test_abi_host_side_errors():
     assert lib.spl_ctx_create(0, None, None, ctypes.byref(out)) == -1
     assert b"null" in lib.spl_last_error()
     assert lib.spl_arena_bytes(0, 2) == -1 and lib.spl_arena_bytes(10, 5) == -1
-    arena = _native.ArenaDesc(None, 0, 10, 2, 0)
+    arena = _native.ArenaDesc(None, 0, 10, 2, 0, 0)
     assert lib.spl_step(None, ctypes.byref(arena), None, None) == -1
 
 
@@ -52,8 +52,8 @@ def test_arena_layout_sizes():
             words = 9 + 4 * P
             b = int(lib.spl_arena_bytes(n, P))
             # planes + 2 deck slots x 128 B + 64 B PCG record + refill list, 256-aligned regions
-            assert b >= words * 4 * n + 256 * n + 64 * n + 4 * (n + 1)
-            assert b % 256 == 0 and b <= words * 4 * n + 320 * n + 4 * n + 4 * 256 + 4
+            assert b >= words * 4 * n + 256 * n + 64 * n + 4 * (2 * n + 64)
+            assert b % 256 == 0 and b <= words * 4 * n + 320 * n + 8 * n + 4 * 256 + 256
 
 
 def test_table_dtype_matches_oracle_struct():

@@ -1,0 +1,84 @@
+"""Summarise rocprofv3 --pmc passes (tools/pmc.sh) per kernel and write the per-launch HBM
+traffic of the step kernel for bench.py's roofline.traffic.
+
+    python tools/pmc_summary.py gpurun_out/pmc_<tag> profiles/<round>/pmc_summary.json [--tables 65536 --players 2]
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE counts exactly half the bytes of a wide (16 B/lane) coalesced read and other widths
+are uncalibrated.  The step kernel's reads are 4 B/lane planes + 4 B gathers, so we report the
+raw FETCH_SIZE bytes and, separately, the TCC_EA0_RDREQ x 64 B / WRREQ x 64 B request bytes.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def load(pmc_dir):
+    per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [value per dispatch]
+    dur = defaultdict(list)
+    for f in sorted(glob.glob(os.path.join(pmc_dir, "p*", "run_counter_collection.csv"))):
+        acc = defaultdict(float)  # (kernel, dispatch, counter) -> summed value
+        times = {}
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"]
+            k = "k_step" if "k_step" in name else ("k_refill" if "k_refill" in name else name)
+            key = (k, int(r["Dispatch_Id"]), r["Counter_Name"])
+            acc[key] += float(r["Counter_Value"])
+            times[(k, int(r["Dispatch_Id"]))] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        for (k, d, c), v in acc.items():
+            per[k][c].append(v)
+        for (k, d), t in times.items():
+            dur[k].append(t)
+    return per, dur
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("pmc_dir")
+    ap.add_argument("out")
+    ap.add_argument("--tables", type=int, default=65536)
+    ap.add_argument("--players", type=int, default=2)
+    a = ap.parse_args()
+    per, dur = load(a.pmc_dir)
+    summary = {"tables": a.tables, "players": a.players, "source": a.pmc_dir, "kernels": {}}
+    for k, cs in per.items():
+        mean = {c: sum(v) / len(v) for c, v in cs.items()}
+        d = {"counters_mean_per_dispatch": mean, "dispatches_per_pass": max(len(v) for v in cs.values())}
+        if "GRBM_GUI_ACTIVE" in mean and dur.get(k):
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md DVFS note)
+            d["clock_ghz_est"] = mean["GRBM_GUI_ACTIVE"] / 8 / (sum(dur[k]) / len(dur[k]))
+        if "SQ_WAVE_CYCLES" in mean and "SQ_WAVES" in mean and mean["SQ_WAVES"]:
+            d["wave_cycles_each"] = 4 * mean["SQ_WAVE_CYCLES"] / mean["SQ_WAVES"]  # quad-cycles -> cycles
+            for part in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if part in mean:
+                    d[part + "_frac"] = mean[part] / mean["SQ_WAVE_CYCLES"]
+            for ins in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+                        "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH"):
+                if ins in mean:
+                    d[ins + "_per_wave"] = mean[ins] / mean["SQ_WAVES"]
+        if "FETCH_SIZE" in mean:
+            d["fetch_bytes"] = mean["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in mean:
+            d["write_bytes"] = mean["WRITE_SIZE"] * 1024
+        if "TCC_EA0_RDREQ" in mean:
+            d["rdreq_bytes_64B"] = mean["TCC_EA0_RDREQ"] * 64
+            d["wrreq_bytes_64B"] = mean.get("TCC_EA0_WRREQ", 0) * 64
+        summary["kernels"][k] = d
+    st = summary["kernels"].get("k_step", {})
+    if "fetch_bytes" in st and "write_bytes" in st:
+        summary["hbm_bytes_per_launch"] = round(st["fetch_bytes"] + st["write_bytes"])
+        summary["hbm_bytes_note"] = ("FETCH_SIZE + WRITE_SIZE (KiB x 1024) per k_step launch, uncorrected: the "
+                                     "kernel's reads are 4-byte-per-lane, outside the guide's 16 B/lane calibration")
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(summary, f, indent=1, sort_keys=True)
+    print(json.dumps({k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()
+                          if kk != "counters_mean_per_dispatch"} for k, v in summary["kernels"].items()}, indent=1))
+    print("hbm_bytes_per_launch", summary.get("hbm_bytes_per_launch"))
+
+
+if __name__ == "__main__":
+    main()
