@@ -88,6 +88,10 @@ def load_library():
     global _LIB
     if _LIB is not None:
         return _LIB
+    # torch bundles its own HIP runtime (SONAME libamdhip64.so.7).  Load it FIRST so this
+    # library binds to the same runtime; dlopen-ing ours first would pull /opt/rocm's runtime
+    # in beside torch's and leave one of them without devices.
+    import torch  # noqa: F401
     path = lib_path()
     if not os.path.exists(path):
         raise ImportError(f"splendor_gym: HIP engine library not found at {path}; build it with "

@@ -47,14 +47,20 @@ class Engine:
         self.arena = self._arena_raw[off:off + nbytes]
         self.desc = ArenaDesc(self.arena.data_ptr(), nbytes, self.n, self.P, 0, 0)
         n = self.n
-        self.obs = torch.zeros((n, OBS_DIM), dtype=torch.int32, device=dev)
-        self.mask = torch.zeros((n, NUM_ACTIONS), dtype=torch.int8, device=dev)
-        self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
-        self.terminated = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self.flags = torch.zeros(n, dtype=torch.uint8, device=dev)
-        self.winner = torch.zeros(n, dtype=torch.int8, device=dev)
-        self.final_obs = torch.zeros((n, OBS_DIM), dtype=torch.int32, device=dev)
-        self.actions = torch.zeros(n, dtype=torch.int32, device=dev)
+        # one contiguous I/O block: per-step outputs first (a single copy fetches a small batch)
+        specs = [("obs", torch.int32, (n, OBS_DIM)), ("mask", torch.int8, (n, NUM_ACTIONS)),
+                 ("reward", torch.float32, (n,)), ("terminated", torch.uint8, (n,)), ("flags", torch.uint8, (n,)),
+                 ("winner", torch.int8, (n,)), ("actions", torch.int32, (n,)),
+                 ("final_obs", torch.int32, (n, OBS_DIM))]
+        offs, off = [], 0
+        for name, dt, shape in specs:
+            nb = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+            offs.append((name, dt, shape, off, nb))
+            off = (off + nb + 255) // 256 * 256
+        self.io = torch.zeros(off, dtype=torch.uint8, device=dev)
+        for name, dt, shape, o, nb in offs:
+            setattr(self, name, self.io[o:o + nb].view(dt).view(shape))
+        self.io_step_bytes = offs[6][3]  # obs .. winner
         with torch.cuda.device(dev):
             check(self.lib, self.lib.spl_arena_init(self.ctx, ctypes.byref(self.desc), self.stream()))
 

@@ -39,14 +39,25 @@ class SplendorEnv(Env):
     def _engine(self):
         if self._eng is None:
             from ..device import Engine
-            self._eng = Engine(1, self.num_players, device=self._device, refill_period=0)
+            e = Engine(1, self.num_players, device=self._device, refill_period=0)
+            import torch
+            self._host = torch.empty(e.io_step_bytes, dtype=torch.uint8).pin_memory()
+            self._eng = e
         return self._eng
 
     def _fetch(self):
+        """One device->host copy of this table's step outputs (obs, mask, reward, flags, ...)."""
         e = self._eng
-        obs = e.obs[0].cpu().numpy()
-        mask = e.mask[0].cpu().numpy()
-        return obs, mask
+        self._host.copy_(e.io[:e.io_step_bytes])  # synchronising copy
+        h = self._host.numpy()
+        base = e.io.data_ptr()
+
+        def view(t, dt, count):
+            o = t.data_ptr() - base
+            return np.frombuffer(h, dtype=dt, count=count, offset=o)
+        self._out = dict(reward=float(view(e.reward, np.float32, 1)[0]), terminated=int(view(e.terminated, np.uint8, 1)[0]),
+                         flags=int(view(e.flags, np.uint8, 1)[0]), winner=int(view(e.winner, np.int8, 1)[0]))
+        return view(e.obs, np.int32, 297).copy(), view(e.mask, np.int8, 45).copy()
 
     def reset(self, *, seed: Optional[int] = None, options: Optional[Dict[str, Any]] = None):
         super().reset(seed=seed)
@@ -72,12 +83,13 @@ class SplendorEnv(Env):
         a = max(min(a, 2**31 - 1), -(2**31))
         e.actions.fill_(a)
         e.step(e.actions, autoreset=False)
-        flags = int(e.flags[0].item())
+        obs, mask = self._fetch()
+        o = self._out
+        flags = o["flags"]
         if flags & _native.F_AFTER_TERMINAL:  # envs/splendor_env.py:53-54
             raise RuntimeError("Cannot call step() after episode termination. Call reset().")
         if flags & _native.F_OOB:             # :62-63
             raise ValueError("Action out of bounds for action_space")
-        obs, mask = self._fetch()
         to_play = int(obs[294])
         self.current_player = to_play
         if flags & _native.F_DRAW:            # :56-61
@@ -86,14 +98,14 @@ class SplendorEnv(Env):
                                            "to_play": to_play, "draw": True}
         if flags & _native.F_ILLEGAL:         # :64-66
             return obs, -0.01, False, False, {"illegal_action": True, "action_mask": mask, "to_play": to_play}
-        reward = float(e.reward[0].item())
-        terminated = bool(e.terminated[0].item())
+        reward = o["reward"]
+        terminated = bool(o["terminated"])
         info = {"action_mask": mask, "to_play": to_play}
         if terminated:
             self._terminal = True
             if flags & _native.F_TURN_LIMIT:
                 info["turn_limit"] = True
-            info["final_rewards"] = self._final_rewards(int(e.winner[0].item()), bool(flags & _native.F_TURN_LIMIT))
+            info["final_rewards"] = self._final_rewards(o["winner"], bool(flags & _native.F_TURN_LIMIT))
         return obs, reward, terminated, False, info
 
     def _final_rewards(self, w, turn_limit):
@@ -118,6 +130,12 @@ class SplendorEnv(Env):
 
     def set_state(self, state: SplendorState) -> None:
         self._engine().upload(state.to_record())
+
+    def legal_mask(self) -> np.ndarray:
+        """engine legal_moves(self.state) as int8[45], computed on the device (rules.py:40-93)."""
+        e = self._engine()
+        e.legal()
+        return e.mask[0].cpu().numpy()
 
     def render(self):
         if self.render_mode not in ("human", None):

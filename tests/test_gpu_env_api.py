@@ -1,0 +1,244 @@
+"""The reference's own env tests, run against the drop-in SplendorEnv / SplendorVectorEnv on the
+GPU (reference tests: splendor_gym/tests/test_env.py, test_gym_compat.py, test_draw_rule.py,
+test_take_reduced_colors.py, test_reserved_card_observation.py, test_properties.py,
+test_afford_nobles_obs.py, test_rules.py), plus single-env parity against the oracle."""
+import time
+
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle, OracleVec
+
+pytestmark = pytest.mark.gpu
+
+
+def make_env():
+    from splendor_gym.envs import SplendorEnv
+    return SplendorEnv(num_players=2)
+
+
+def first_legal(mask):
+    return int(np.flatnonzero(mask)[0])
+
+
+def test_reset_and_step_shapes():  # test_env.py:8-25, test_gym_compat.py:18-41
+    env = make_env()
+    obs, info = env.reset(seed=123)
+    assert isinstance(obs, np.ndarray) and obs.shape == (297,) and obs.dtype == np.int32
+    assert info["action_mask"].shape == (45,) and info["action_mask"].dtype == np.int8
+    assert env.action_space.n == 45 and env.observation_space.shape == (297,)
+    obs, r, term, trunc, info = env.step(first_legal(info["action_mask"]))
+    assert isinstance(r, float) and isinstance(term, bool) and isinstance(trunc, bool)
+    assert obs.shape == (297,) and "action_mask" in info
+
+
+def test_random_rollout_no_crash():  # test_env.py:28-37
+    env = make_env()
+    obs, info = env.reset(seed=0)
+    rs = np.random.default_rng(0)
+    for _ in range(200):
+        if info["action_mask"].sum() == 0:
+            break
+        obs, r, term, trunc, info = env.step(int(rs.choice(np.flatnonzero(info["action_mask"]))))
+        if term:
+            obs, info = env.reset()
+
+
+def test_deterministic_reset_and_scripted_prefix():  # test_gym_compat.py:44-76, test_properties.py:23-36
+    e1, e2 = make_env(), make_env()
+    o1, i1 = e1.reset(seed=999)
+    o2, i2 = e2.reset(seed=999)
+    np.testing.assert_array_equal(o1, o2)
+    for _ in range(20):
+        a1, a2 = first_legal(i1["action_mask"]), first_legal(i2["action_mask"])
+        assert a1 == a2
+        o1, r1, t1, _, i1 = e1.step(a1)
+        o2, r2, t2, _, i2 = e2.step(a2)
+        np.testing.assert_array_equal(o1, o2)
+        assert (r1, t1) == (r2, t2)
+
+
+def test_step_after_terminated_raises():  # test_gym_compat.py:89-108
+    env = make_env()
+    obs, info = env.reset(seed=123)
+    for _ in range(2000):
+        m = info["action_mask"]
+        obs, r, term, trunc, info = env.step(first_legal(m) if m.any() else 0)
+        if term:
+            break
+    assert term
+    with pytest.raises(RuntimeError):
+        env.step(0)
+    assert env.get_final_rewards() in ({0: 1.0, 1: -1.0}, {0: -1.0, 1: 1.0}, {0: 0.0, 1: 0.0}, {0: -0.1, 1: -0.1})
+
+
+def test_illegal_action_penalty_and_oob():  # test_gym_compat.py:111-124, splendor_env.py:62-66
+    env = make_env()
+    obs, info = env.reset(seed=321)
+    illegal = int(np.flatnonzero(info["action_mask"] == 0)[0])
+    obs2, r, term, trunc, info2 = env.step(illegal)
+    assert r == pytest.approx(-0.01) and not term and info2.get("illegal_action")
+    np.testing.assert_array_equal(obs, obs2)
+    with pytest.raises(ValueError):
+        env.step(45)
+    with pytest.raises(ValueError):
+        env.step(-1)
+
+
+def test_render_no_crash(capsys):  # test_gym_compat.py:127-132
+    env = make_env()
+    env.render_mode = "human"
+    env.reset(seed=0)
+    env.render()
+    assert "Bank" in capsys.readouterr().out
+
+
+def test_no_legal_move_draw():  # test_draw_rule.py:7-24
+    env = make_env()
+    env.reset(seed=0)
+    s = env.state
+    s.bank[:] = [0, 0, 0, 0, 0, 0]
+    p = s.players[s.to_play]
+    p.tokens[:] = [10, 0, 0, 0, 0, 0]
+    p.reserved = s.decks[1][:3]
+    p.revealed_reserved = [False] * 3
+    for t in (1, 2, 3):
+        s.board[t] = [None] * 4
+    env.set_state(s)
+    assert not env.legal_mask().any()
+    obs, r, term, trunc, info = env.step(0)
+    assert term and r == 0 and info.get("draw") and env.state.winner_index is None
+
+
+@pytest.mark.parametrize("bank,n_legal,taken", [([1, 0, 2, 0, 0, 0], 3, 2), ([0, 0, 0, 0, 3, 0], 6, 1)])
+def test_take_reduced_colours(bank, n_legal, taken):  # test_take_reduced_colors.py:7-36
+    env = make_env()
+    env.reset(seed=123)
+    s = env.state
+    s.bank[:] = bank
+    env.set_state(s)
+    m = env.legal_mask()
+    legal = [i for i in range(10) if m[i]]
+    assert len(legal) == n_legal
+    env.step(legal[0])
+    s = env.state
+    last = s.players[(s.to_play - 1) % s.num_players]
+    assert sum(last.tokens) == taken
+
+
+def test_reserved_card_visibility():  # test_reserved_card_observation.py:85-371
+    env = make_env()
+    obs, info = env.reset(seed=42)
+    a = [i for i in range(27, 39) if info["action_mask"][i]][0]
+    obs, _, _, _, info = env.step(a)                     # P0 reserves a visible card
+    assert obs[18] == 0 and obs[31] == 1                  # P1 to play: own 0, opponent 1
+    assert obs[230] == 1 and obs[230 + 13] == 1           # revealed to the opponent
+    obs, _, _, _, info = env.step(first_legal(info["action_mask"]))  # P1 any move
+    obs, _, _, _, info = env.step(39)                     # P0 blind-reserves tier 1
+    assert obs[31] == 2 and obs[230 + 14:230 + 28].sum() == 0   # hidden slot is all zeros
+    assert obs[230] == 1                                   # the visible one still shows
+
+
+def test_mask_invariants():  # test_properties.py:39-57
+    env = make_env()
+    obs, info = env.reset(seed=7)
+    s, m = env.state, info["action_mask"]
+    for c in range(5):
+        assert (m[10 + c] == 1) == (s.bank[c] >= 4)
+    p = s.players[s.to_play]
+    for t in (1, 2, 3):
+        assert (m[38 + t] == 1) == (len(s.decks[t]) > 0 and len(p.reserved) < 3)
+
+
+def test_token_return_to_ten():  # test_afford_nobles_obs.py:58-71, test_rules.py:37-43
+    env = make_env()
+    obs, info = env.reset(seed=7)
+    s = env.state
+    s.players[s.to_play].tokens = [3, 3, 3, 3, 3, 0]
+    env.set_state(s)
+    bank_before = sum(env.state.bank)
+    env.step(first_legal(env.legal_mask()))
+    s = env.state
+    assert sum(s.players[(s.to_play - 1) % 2].tokens) == 10 and sum(s.bank) >= bank_before
+
+
+def test_single_env_matches_oracle_with_stream_continuation():
+    """SplendorEnv episodes (reset(seed) then reset() continuing the np_random stream) equal the
+    oracle step for step."""
+    orc = Oracle()
+    env = make_env()
+    vec = OracleVec(orc, 1, 2, [2024])
+    obs, info = env.reset(seed=2024)
+    np.testing.assert_array_equal(obs, vec.obs[0])
+    rs = np.random.default_rng(5)
+    episodes = 0
+    while episodes < 3:
+        legal = np.flatnonzero(info["action_mask"])
+        a = int(rs.choice(legal)) if len(legal) else 0
+        obs, r, term, trunc, info = env.step(a)
+        ref = vec.step(np.array([a], np.int32), want_final=True)
+        np.testing.assert_array_equal(obs, ref["final_obs"][0] if term else ref["obs"][0])
+        assert np.float32(r) == ref["reward"][0]
+        if term:
+            episodes += 1
+            obs, info = env.reset()
+            np.testing.assert_array_equal(obs, ref["obs"][0])
+
+
+def test_vector_env_matches_single_envs_and_autoresets():
+    import torch
+    from splendor_gym import SplendorVectorEnv
+    n = 8
+    vec = SplendorVectorEnv(n, device="cuda:0")
+    obs, info = vec.reset(seed=100)
+    singles = [make_env() for _ in range(n)]
+    for i, e in enumerate(singles):
+        o, _ = e.reset(seed=100 + i)
+        np.testing.assert_array_equal(obs[i].cpu().numpy(), o)
+    saw_final = False
+    for k in range(300):
+        acts = vec.sample_actions(seed=3, ply=k).clone()
+        obs, rew, term, trunc, info = vec.step(acts)
+        for i, e in enumerate(singles):
+            o, r, t, _, _ = e.step(int(acts[i]))
+            if t:
+                np.testing.assert_array_equal(info["final_observation"][i].cpu().numpy(), o)
+                o, _ = e.reset()
+                saw_final = True
+            np.testing.assert_array_equal(obs[i].cpu().numpy(), o)
+            assert np.float32(rew[i].item()) == np.float32(r) and bool(term[i]) == t
+    assert saw_final
+
+
+def test_vector_env_numpy_mode():
+    from splendor_gym import SplendorVectorEnv
+    vec = SplendorVectorEnv(16, device="cuda:0", to_numpy=True)
+    obs, info = vec.reset(seed=0)
+    assert isinstance(obs, np.ndarray) and obs.shape == (16, 297) and info["action_mask"].shape == (16, 45)
+    done = 0
+    for k in range(400):
+        acts = vec.sample_actions(seed=1, ply=k).cpu().numpy()
+        obs, rew, term, trunc, info = vec.step(acts)
+        if term.any():
+            i = int(np.flatnonzero(term)[0])
+            assert info["_final_observation"][i] and info["final_observation"][i].shape == (297,)
+            assert "final_rewards" in info["final_info"][i]
+            done += 1
+    assert done > 0
+
+
+@pytest.mark.slow
+def test_rollout_perf_smoke():  # test_gym_compat.py:135-157 (threshold 6000 SPS)
+    env = make_env()
+    obs, info = env.reset(seed=123)
+    n, steps = 5000, 0
+    t0 = time.time()
+    while steps < n:
+        m = info["action_mask"]
+        obs, r, term, trunc, info = env.step(first_legal(m) if m.any() else 0)
+        steps += 1
+        if term:
+            obs, info = env.reset(seed=steps)
+    sps = steps / (time.time() - t0)
+    print(f"SPS={sps:.0f}")
+    assert sps > 6000

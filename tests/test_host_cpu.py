@@ -160,3 +160,16 @@ def test_gloo_two_ranks_gather_returns():
         assert ret == [i * 0.5 for i in range(1001)]
         assert cnt == [i % 7 for i in range(1001)]
         assert t == 1.25
+
+
+def test_single_hip_runtime_after_load():
+    """The engine library must share torch's HIP runtime (one libamdhip64 in the process)."""
+    import re
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from splendor_gym import _native; _native.load_library(); "
+            "import re; m = open('/proc/self/maps').read(); "
+            "print(len(set(re.findall(r'\\S*libamdhip64\\S*', m))))") % os.path.join(REPO, "splendor-gym_amd")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1] == "1"
