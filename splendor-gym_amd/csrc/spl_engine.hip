@@ -73,13 +73,30 @@ constexpr int kObsDim = 297;
 constexpr int ABL_LEGAL_PRE = 1, ABL_APPLY = 2, ABL_LEGAL_POST = 4, ABL_FINAL = 8, ABL_RESET = 16, ABL_ENCODE = 32,
               ABL_STORE = 64;
 __device__ __forceinline__ bool abl(int bit) { return (SPL_ABL & bit) != 0; }
+
+// Phase stamps for the diagnostic build only (-DSPL_STAMPS, tools/stamps.py): lane 0 of every
+// wave records s_memrealtime (100 MHz) at phase boundaries of k_step.  Never in the product build.
+#ifdef SPL_STAMPS
+__device__ uint64_t *g_stamps;
+#define STAMP(i)                                                                                 \
+    do {                                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        if (threadIdx.x == 0) g_stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+    } while (0)
+#else
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#endif
 constexpr int kScratchStride = 112;  // per-lane deal scratch in LDS (16-aligned)
 
 struct __align__(16) BlockLDS {
     uint4 cards[90];
     uint2 nobles[10];
     uint64_t mask[64];
-    uint8_t rows[64 * kObsDim];  // observation staging; also the deal scratch (64 x 112 B)
+    uint8_t rows[64 * kObsDim];   // observation staging; also the deal scratch (64 x 112 B)
+    uint8_t frows[64 * kObsDim];  // terminal observations (k_step): stored with everything else at the end
 };
 
 // ------------------------------------------------------------------------------------------
@@ -90,6 +107,16 @@ __device__ __forceinline__ uint32_t bset(uint32_t w, int k, uint32_t v) {
     return (w & ~(0xFFu << (8 * k))) | ((v & 0xFFu) << (8 * k));
 }
 __device__ __forceinline__ int lane_id() { return threadIdx.x; }
+
+// Cross-lane LDS hand-off inside ONE wave (every workgroup here is a single wave).
+// __syncthreads() would also emit s_waitcnt vmcnt(0): the wave would stall until its pending
+// global stores drain behind every other wave's observation traffic.  LDS executes one wave's
+// operations in order, so ordering the compiler (wavefront fence) and the LDS counter suffices.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only
+    __builtin_amdgcn_wave_barrier();
+}
 
 // Launder a value through an empty asm so that a select chain over struct members stays a
 // select of VALUES: otherwise LLVM folds "c ? s.a : s.b" into a load at a selected offset,
@@ -909,6 +936,7 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     const int t = t0 + lane;
     const bool valid = t < A.n;
     const int rows = min(64, A.n - t0);
+    STAMP(0);
     load_tables_lds(L, Tb);
 
     Tab<P> T;
@@ -919,7 +947,8 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     } else {
         fresh_state(T, 0u, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u), make_uint4(0xFFFFFFFFu, 0xFFu, 0u, 0u));
     }
-    __syncthreads();
+    wave_lds_sync();
+    STAMP(1);
 
     uint32_t flags = 0;
     float reward = 0.0f;
@@ -952,7 +981,9 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
                 reward = -0.01f;
                 outmask = legal_mask(T.sw, cur, bank, L);
             } else {
+                STAMP(2);
                 if (!abl(ABL_APPLY)) apply_action(T, action, live, L, Tb.lut, flags);  // :68
+                STAMP(3);
                 term = is_terminal(T.sw);                         // :70
                 if (term) {                                       // :71-80
                     const int w = get_winner(T.sw);
@@ -966,6 +997,7 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
         }
     }
     const int8_t wnr = (int8_t)get_winner(T.sw);
+    STAMP(4);
 
     // same-step autoreset: start the pool-record loads and the refill-queue slot now, consume
     // them after the final-observation block so their latency hides behind it
@@ -988,35 +1020,28 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
         if (lane == leader) qbase = atomicAdd(&A.needy[par], (uint32_t)__popcll(pushb));
     }
 
-    // terminal observations for gymnasium's info["final_observation"]
+    STAMP(5);
+    // episode statistics (player 0's final reward, envs/splendor_env.py:92-115): read now
+    float ep_r = 0.0f;
+    uint32_t ep_c = 0u;
+    if (valid && term) {
+        if (S.ep_return) ep_r = S.ep_return[t];
+        if (S.ep_count) ep_c = S.ep_count[t];
+    }
+    // terminal observation for gymnasium's info["final_observation"], staged in LDS: this wave
+    // issues no store before its block stores (a store issued mid-kernel stalls behind the
+    // other waves' observation drain and the wave falls behind)
     const bool want_final = S.autoreset && S.final_obs != nullptr && !abl(ABL_FINAL);
     const uint64_t fin = __ballot(valid && term && want_final);
-    if (fin) {
-        if (valid && term) encode_row(T, &L.rows[lane * kObsDim], L);
-        __syncthreads();
-        uint64_t b = fin;
-        while (b) {
-            const int r = __ffsll((unsigned long long)b) - 1;
-            b &= b - 1;
-            int32_t *dst = S.final_obs + (size_t)(t0 + r) * kObsDim;
-            for (int e = lane; e < kObsDim; e += 64) dst[e] = (int32_t)L.rows[r * kObsDim + e];
-        }
-        __syncthreads();
-    }
-    // episode statistics (player 0's final reward, envs/splendor_env.py:92-115)
+    if (valid && term && want_final) encode_row(T, &L.frows[lane * kObsDim], L);
+    const int fin_moves = get_moves(T.sw);
+    float ep_add = 0.0f;
     if (valid && term) {
         const int w = get_winner(T.sw);
         const bool tl = (T.sw[SW_MISC] & ST_TURN_LIMIT) != 0;
-        const float r0 = w < 0 ? (tl ? -0.1f : 0.0f) : (w == 0 ? 1.0f : -1.0f);
-        if (S.ep_return) S.ep_return[t] += r0;
-        if (S.ep_count) S.ep_count[t] += 1u;
-        if (want_final && get_moves(T.sw) > 255) S.final_obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
+        ep_add = w < 0 ? (tl ? -0.1f : 0.0f) : (w == 0 ? 1.0f : -1.0f);
     }
-    if (pushb) {  // refill queue entry (wave-aggregated atomic issued above)
-        const int leader = __ffsll((unsigned long long)pushb) - 1;
-        qbase = __shfl(qbase, leader);
-        if (push) needy_list(A, par)[qbase + __popcll(pushb & ((1ull << lane) - 1ull))] = (uint32_t)t;
-    }
+    STAMP(6);
     if (do_reset) {  // envs/splendor_env.py:43-44 with the continued np_random stream
         if (p_ready == 0u) {  // pool not refilled yet: deal inline (correct, just slower)
             Pcg64 g = load_pcg(A, t);
@@ -1026,22 +1051,48 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
             p_tail0 = *reinterpret_cast<const uint4 *>(prec + kRecBoard);
             p_tail1 = *reinterpret_cast<const uint4 *>(prec + kRecNob0);
         }
-        reinterpret_cast<uint32_t *>(prec)[kRecReady / 4] = 0u;  // now live
         fresh_state(T, (nxt ? ST_ACTIVE : 0u) | ST_PENDING, p_tail0, p_tail1);
         flags |= SPL_F_RESET;
         outmask = legal_of(T, L);
     }
-    __syncthreads();  // deal scratch (rows) free again
+    STAMP(7);
+    wave_lds_sync();  // deal scratch (rows) free again
 
     // observation + mask of the current state, block stores
     if (!abl(ABL_ENCODE)) encode_row(T, &L.rows[lane * kObsDim], L);
     L.mask[lane] = outmask;
-    __syncthreads();
+    // land the remaining loads (queue slot, episode stats) before the first store of this wave
+    qbase = opaque(qbase);
+    ep_r = __uint_as_float(opaque(__float_as_uint(ep_r)));
+    ep_c = opaque(ep_c);
+    STAMP(8);
+    wave_lds_sync();
+    STAMP(9);
     int32_t *obs_dst = S.obs + (size_t)t0 * kObsDim;
     if (!abl(ABL_STORE)) {
         store_obs_block(L, rows, obs_dst);
+        STAMP(10);
         store_mask_block(L, rows, S.mask + (size_t)t0 * 45);
     }
+    uint64_t b = fin;  // terminal rows of this wave (about one per wave per step)
+    while (b) {
+        const int r = __ffsll((unsigned long long)b) - 1;
+        b &= b - 1;
+        int32_t *dst = S.final_obs + (size_t)(t0 + r) * kObsDim;
+        for (int e = lane; e < kObsDim; e += 64) dst[e] = (int32_t)L.frows[r * kObsDim + e];
+    }
+    if (valid && term) {
+        if (S.ep_return) S.ep_return[t] = ep_r + ep_add;
+        if (S.ep_count) S.ep_count[t] = ep_c + 1u;
+        if (want_final && fin_moves > 255) S.final_obs[(size_t)t * kObsDim + 295] = fin_moves;
+    }
+    if (pushb) {  // refill queue entry (wave-aggregated atomic issued above)
+        const int leader = __ffsll((unsigned long long)pushb) - 1;
+        qbase = __shfl(qbase, leader);
+        if (push) needy_list(A, par)[qbase + __popcll(pushb & ((1ull << lane) - 1ull))] = (uint32_t)t;
+    }
+    if (do_reset) reinterpret_cast<uint32_t *>(prec)[kRecReady / 4] = 0u;  // pool record now live
+    STAMP(11);
     if (__any(valid && get_moves(T.sw) > 255)) {
         __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): block store of this dword has left
         if (valid && get_moves(T.sw) > 255) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
@@ -1057,6 +1108,7 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
         }
         store_tab(T, A, t);
     }
+    STAMP(12);
 }
 
 // Explicit reset (SplendorEnv.reset / VectorEnv.reset), then observation + mask of all tables.
@@ -1073,7 +1125,7 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
     Tab<P> T;
     if (valid) load_tab(T, A, t);
     else fresh_state(T, 0u, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u), make_uint4(0xFFFFFFFFu, 0xFFu, 0u, 0u));
-    __syncthreads();
+    wave_lds_sync();
     const bool doit = valid && (mask_in == nullptr || mask_in[t] != 0);
     uint8_t *scr = &L.rows[lane * kScratchStride];
     bool push = false;
@@ -1102,11 +1154,11 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
         }
     }
     push_needy(A, push, (uint32_t)t);
-    __syncthreads();
+    wave_lds_sync();
     if (obs || mask_out) {
         encode_row(T, &L.rows[lane * kObsDim], L);
         L.mask[lane] = (valid && !is_terminal(T.sw)) ? legal_of(T, L) : 0ull;  // env info mask
-        __syncthreads();
+        wave_lds_sync();
         if (obs) store_obs_block(L, rows, obs + (size_t)t0 * kObsDim);
         if (mask_out) store_mask_block(L, rows, mask_out + (size_t)t0 * 45);
     }
@@ -1153,10 +1205,10 @@ __global__ __launch_bounds__(64) void k_observe(KArena A, KTables Tb, int32_t *o
     Tab<P> T;
     if (valid) load_tab(T, A, t);
     else fresh_state(T, 0u, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u), make_uint4(0xFFFFFFFFu, 0xFFu, 0u, 0u));
-    __syncthreads();
+    wave_lds_sync();
     if (obs) encode_row(T, &L.rows[lane * kObsDim], L);
     L.mask[lane] = valid ? legal_of(T, L) : 0ull;  // engine legal_moves (no terminal check)
-    __syncthreads();
+    wave_lds_sync();
     if (obs) {
         store_obs_block(L, rows, obs + (size_t)t0 * kObsDim);
         if (__any(valid && get_moves(T.sw) > 255)) {
@@ -1364,6 +1416,13 @@ static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 63) / 64);
 extern "C" {
 
 int spl_abi_version(void) { return SPL_ABI_VERSION; }
+
+#ifdef SPL_STAMPS
+int spl_debug_set_stamps(void *buf) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)));
+    return SPL_OK;
+}
+#endif
 
 const char *spl_last_error(void) { return g_err.c_str(); }
 
