@@ -68,7 +68,7 @@ typedef struct spl_arena_s {
     int32_t n;            /* tables */
     int32_t players;      /* 2..4 */
     int64_t steps;        /* maintained by the library: spl_step calls since the last reset */
-    int64_t epoch;        /* maintained by the library: pool refills so far (list parity) */
+    int64_t epoch;        /* maintained by the library: pool refills launched so far */
 } spl_arena_t;
 
 /* Batched step arguments (all device pointers; [n] = one entry per table). */
@@ -102,7 +102,9 @@ int spl_ctx_destroy(spl_ctx_t *ctx);
 int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period);
 
 int64_t spl_arena_bytes(int32_t n, int32_t players);
-/* Zero the arena (must precede the first spl_reset of a fresh allocation). */
+/* Zero the arena and mark every table's pool as not dealt (must precede the first spl_reset
+ * of a fresh allocation).  A table that was never reset with a seed has no engine-seed stream:
+ * an unseeded reset or a refill deals it from engine seed 0. */
 int spl_arena_init(spl_ctx_t *ctx, spl_arena_t *arena, void *stream);
 
 /* Reset tables.  pcg (device, nullable): 4 x uint64 per table = numpy PCG64 state
@@ -116,7 +118,8 @@ int spl_reset(spl_ctx_t *ctx, spl_arena_t *arena, const uint64_t *pcg, const uin
 
 int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *args, void *stream);
 
-/* Pool maintenance: deal the next episode of every table whose pool slot was consumed. */
+/* Pool maintenance: deal the next episode of every table whose pool slot was consumed
+ * (status bit ST_PENDING).  Tables it has not reached deal inline at their next reset. */
 int spl_refill(spl_ctx_t *ctx, spl_arena_t *arena, void *stream);
 
 int spl_encode(spl_ctx_t *ctx, spl_arena_t *arena, int32_t *obs, void *stream);

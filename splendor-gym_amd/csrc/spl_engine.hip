@@ -31,12 +31,11 @@ namespace spl {
 // kernel parameter blocks
 // ------------------------------------------------------------------------------------------
 struct KArena {
-    uint32_t *planes;
-    uint8_t *slots;
-    uint8_t *pcg;
-    uint32_t *needy;  // [0], [1] = list counts; lists of table ids at needy + 64 (+ n for list 1)
+    uint32_t *planes;  // [num_words(P)][n] table state
+    uint32_t *pool;    // [PL_COUNT][n] pool deal's board / noble words
+    uint8_t *slots;    // [n][2][128] deck records
+    uint8_t *pcg;      // [n][64] engine-seed streams
     int n;
-    int epoch;        // parity selects the list that steps append to and the refill consumes
 };
 
 struct KTables {
@@ -71,7 +70,8 @@ constexpr int kObsDim = 297;
 #define SPL_ABL 0
 #endif
 constexpr int ABL_LEGAL_PRE = 1, ABL_APPLY = 2, ABL_LEGAL_POST = 4, ABL_FINAL = 8, ABL_RESET = 16, ABL_ENCODE = 32,
-              ABL_STORE = 64;
+              ABL_STORE = 64, ABL_MASK_STORE = 128, ABL_SMALL_OUT = 256, ABL_TAB_STORE = 512, ABL_OBS_STORE = 1024,
+              ABL_LOAD = 2048;
 __device__ __forceinline__ bool abl(int bit) { return (SPL_ABL & bit) != 0; }
 
 // Phase stamps for the diagnostic build only (-DSPL_STAMPS, tools/stamps.py): lane 0 of every
@@ -91,10 +91,13 @@ __device__ uint64_t *g_stamps;
 #endif
 constexpr int kScratchStride = 112;  // per-lane deal scratch in LDS (16-aligned)
 
+constexpr int kMaskStreamWords = 64 * 45 / 32;  // 90
+
 struct __align__(16) BlockLDS {
     uint4 cards[90];
     uint2 nobles[10];
     uint64_t mask[64];
+    uint32_t mbits[96];  // the wave's 64 x 45 mask bits as one stream (store_mask_block)
     uint8_t rows[64 * kObsDim];   // observation staging; also the deal scratch (64 x 112 B)
     uint8_t frows[64 * kObsDim];  // terminal observations (k_step): stored with everything else at the end
 };
@@ -319,12 +322,24 @@ __device__ __forceinline__ uint8_t *slot_rec(const KArena &A, int t, int slot) {
     return A.slots + ((size_t)t * 2 + slot) * kSlotBytes;
 }
 
-// engine/rules.py:125-129 _refill_slot / deck.pop(): top of tier t from the live record
-__device__ __forceinline__ uint32_t deck_pop(uint32_t *sw, const uint8_t *rec, int t) {
+// engine/rules.py:125-129 _refill_slot / deck.pop() of tier t.  `top` is the card at
+// deck_len-1 of that tier, gathered from the live record at the top of the step (one action
+// pops at most one card, from the tier the action names: pop_tier()).
+__device__ __forceinline__ uint32_t deck_pop(uint32_t *sw, uint32_t top, int t) {
     const int len = (int)bget(sw[SW_DECK], t);
     if (len <= 0) return 0xFFu;
     sw[SW_DECK] = bset(sw[SW_DECK], t, (uint32_t)(len - 1));
-    return rec[tier_base(t) + len - 1];
+    return top;
+}
+
+// legal_moves of every fresh deal (engine/rules.py:40-93 on state.py:181-211's table): every
+// take-3 and take-2 (bank 4 of each colour), every visible and blind reserve, no purchase
+constexpr uint64_t kFreshDealMask = ((1ull << 15) - 1ull) | (((1ull << 15) - 1ull) << 27);
+
+// tier an action pops from: buy visible (:216-225) and reserve visible (:226-240) refill the
+// slot's tier, reserve blind (:241-249) draws from its tier; -1 for every other action
+__device__ __forceinline__ int pop_tier(int a) {
+    return (a >= 15 && a < 27) ? (a - 15) >> 2 : ((a >= 27 && a < 39) ? (a - 27) >> 2 : ((a >= 39 && a < 42) ? a - 39 : -1));
 }
 
 // pick the r-th colour (ascending) among non-gold colours the player holds
@@ -378,19 +393,51 @@ __device__ __forceinline__ void token_return_mt(Pl &p, int bank[6], int remainin
     }
 }
 
-// engine/rules.py:188-193 _enforce_token_limit -> :150-185 auto_return_tokens
+// token-return table index of (turn_count, to_play, sum(tokens), sum(bank)), -1 outside it
+__device__ __forceinline__ int lut_key(int turn_count, int to_play, int total, int bank_total) {
+    const bool in_lut = turn_count < kLutTc && to_play < kLutTp && total >= 11 && total <= 13 && bank_total < kLutSb;
+    return in_lut ? ((turn_count * kLutTp + to_play) * kLutSt + (total - 11)) * kLutSb + bank_total : -1;
+}
+
+// The table entry action `a` will consult, predicted from the pre-action state so its load
+// can start with the state loads: takes and reserves move tokens bank -> player exactly as
+// apply_action does; buys only lower the mover's total (-1: no prediction).
+__device__ __forceinline__ int predict_lut_key(const Pl &p, const int bank[6], int a, int turn_count, int to_play) {
+    int total = 0, bank_total = 0, delta = 0;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        total += p.tok[c];
+        bank_total += bank[c];
+    }
+    if (a < 10) {
+        const uint32_t cm = take3_mask(a);
+#pragma unroll
+        for (int c = 0; c < 5; ++c) delta += (((cm >> c) & 1u) && bank[c] >= 1) ? 1 : 0;
+    } else if (a < 15) {
+        delta = 2;
+    } else if (a >= 27 && a < 42) {
+        delta = bank[5] > 0 ? 1 : 0;
+    } else {
+        return -1;
+    }
+    return total + delta > 10 ? lut_key(turn_count, to_play, total + delta, bank_total - delta) : -1;
+}
+
+// engine/rules.py:188-193 _enforce_token_limit -> :150-185 auto_return_tokens.  `pre_key` /
+// `pre_e` are the prefetched table entry (predict_lut_key); any other key is loaded here.
 __device__ __forceinline__ void enforce_token_limit(Pl &p, int bank[6], int turn_count, int to_play,
-                                                    const uint4 *lut, uint32_t &flags) {
+                                                    const uint4 *lut, int pre_key, uint4 pre_e, uint32_t &flags) {
     int total = 0, bank_total = 0;
 #pragma unroll
     for (int c = 0; c < 6; ++c) total += p.tok[c];
     if (total <= 10) return;
 #pragma unroll
     for (int c = 0; c < 6; ++c) bank_total += bank[c];
-    const bool in_lut = turn_count < kLutTc && to_play < kLutTp && total <= 13 && bank_total < kLutSb;
+    const int key = lut_key(turn_count, to_play, total, bank_total);
+    const bool in_lut = key >= 0;
     bool need_mt = !in_lut;
     if (in_lut) {
-        const uint4 e = lut[((turn_count * kLutTp + to_play) * kLutSt + (total - 11)) * kLutSb + bank_total];
+        const uint4 e = key == pre_key ? pre_e : lut[key];
         Pl p2 = p;
         int bank2[6];
 #pragma unroll
@@ -490,8 +537,8 @@ __device__ __forceinline__ bool is_terminal(const uint32_t *sw) {
 
 // engine/rules.py:196-287 apply_action on the current player (action known legal)
 template <int P>
-__device__ __forceinline__ void apply_action(Tab<P> &T, int a, const uint8_t *live_rec, const BlockLDS &L,
-                                             const uint4 *lut, uint32_t &flags) {
+__device__ __forceinline__ void apply_action(Tab<P> &T, int a, uint32_t top, const BlockLDS &L, const uint4 *lut,
+                                             int pre_key, uint4 pre_e, uint32_t &flags) {
     uint32_t *sw = T.sw;
     const int tp = get_to_play(sw);
     uint32_t w[4];
@@ -516,7 +563,7 @@ __device__ __forceinline__ void apply_action(Tab<P> &T, int a, const uint8_t *li
     } else if (a < 27) {  // :216-225 buy visible, refill
         const int k = a - 15;
         pay_for_card(p, bank, card_rec(L, board_get(sw, k)));
-        board_set(sw, k, deck_pop(sw, live_rec, k >> 2));
+        board_set(sw, k, deck_pop(sw, top, k >> 2));
     } else if (a < 39) {  // :226-240 reserve visible, gold if any, refill
         const int k = a - 27;
         const int card = board_get(sw, k);
@@ -527,9 +574,9 @@ __device__ __forceinline__ void apply_action(Tab<P> &T, int a, const uint8_t *li
         const bool gold = bank[5] > 0;
         bank[5] -= gold ? 1 : 0;
         p.tok[5] += gold ? 1 : 0;
-        board_set(sw, k, deck_pop(sw, live_rec, k >> 2));
+        board_set(sw, k, deck_pop(sw, top, k >> 2));
     } else if (a < 42) {  // :241-249 reserve blind (hidden), gold if any
-        const int card = (int)deck_pop(sw, live_rec, a - 39);
+        const int card = (int)deck_pop(sw, top, a - 39);
 #pragma unroll
         for (int i = 0; i < 3; ++i) p.res[i] = p.nres == i ? card : p.res[i];
         p.rev &= ~(1 << p.nres);
@@ -549,7 +596,7 @@ __device__ __forceinline__ void apply_action(Tab<P> &T, int a, const uint8_t *li
         pay_for_card(p, bank, card_rec(L, card));
     }
     grant_noble(sw, p, tp, L);                                              // :260
-    enforce_token_limit(p, bank, get_turn(sw), tp, lut, flags);             // :261
+    enforce_token_limit(p, bank, get_turn(sw), tp, lut, pre_key, pre_e, flags);  // :261
     uint32_t misc = sw[SW_MISC];
     if (p.pres >= 15) misc |= ST_GAME_OVER;                                 // :264-265
     pack_pl(p, w);
@@ -647,60 +694,73 @@ __device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *row, const 
 // Block store of this wave's staged rows: obs[t0 .. t0+rows) as int32, 16 B per lane-store.
 // LDS reads are issued in groups of 5 before their stores: one read-wait per store halves the
 // store rate (tools/microbench_store.hip: 2.7 -> 5.2 TB/s).
+// One 16-byte store per lane per instruction, typed as a native 4 x i32 vector indexed in vector
+// units: with `int4` and 32-bit element indexing the compiler versions the loop and, in the
+// unrolled copy, splits every store into four strided dword stores (half the store bandwidth).
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4i expand4(uint32_t w) {
+    v4i v = {(int)(w & 0xFFu), (int)((w >> 8) & 0xFFu), (int)((w >> 16) & 0xFFu), (int)(w >> 24)};
+    return v;
+}
+
+// Block store of this wave's observation rows: LDS bytes [rows][297] -> int32 [rows][297] at
+// dst (16-byte aligned: 64-row blocks are 76032 B).  Dword d of the block is LDS word d.
 __device__ __forceinline__ void store_obs_block(const BlockLDS &L, int rows, int32_t *dst) {
     const int nbytes = rows * kObsDim;
     const int full = nbytes >> 2;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(L.rows);
+    v4i *out = reinterpret_cast<v4i *>(dst);
     constexpr int U = 5;
     int d = lane_id();
-    for (; d + 64 * (U - 1) < full; d += 64 * U) {
+    if (rows == 64) {  // every wave but a ragged last one: compile-time trip count
+        constexpr int kFull = 64 * kObsDim / 4;  // 4752 = 14 x 320 + 272
+#pragma unroll 1
+        for (int it = 0; it < kFull / (64 * U); ++it, d += 64 * U) {
+            uint32_t w[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
+#pragma unroll
+            for (int u = 0; u < U; ++u) out[d + 64 * u] = expand4(w[u]);
+        }
         uint32_t w[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
+        for (int u = 0; u < U; ++u) w[u] = (d + 64 * u < kFull) ? src[d + 64 * u] : 0u;
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            *reinterpret_cast<int4 *>(dst + 4 * (d + 64 * u)) =
-                make_int4((int)(w[u] & 0xFFu), (int)((w[u] >> 8) & 0xFFu), (int)((w[u] >> 16) & 0xFFu),
-                          (int)(w[u] >> 24));
+            if (d + 64 * u < kFull) out[d + 64 * u] = expand4(w[u]);
+        return;
     }
-    for (; d < full; d += 64) {
-        const uint32_t w = src[d];
-        *reinterpret_cast<int4 *>(dst + 4 * d) =
-            make_int4((int)(w & 0xFFu), (int)((w >> 8) & 0xFFu), (int)((w >> 16) & 0xFFu), (int)(w >> 24));
-    }
+    for (; d < full; d += 64) out[d] = expand4(src[d]);
     for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) dst[b] = (int32_t)L.rows[b];
 }
 
-// Block store of this wave's masks: mask[t0 .. t0+rows) as int8 [rows][45], 4 bytes per lane-store.
-__device__ __forceinline__ uint32_t mask_dword(const BlockLDS &L, int d, int nbytes) {
-    uint32_t v = 0;
+// Block store of this wave's masks: mask[t0 .. t0+rows) as int8 [rows][45].  The 64 x 45 mask
+// bits are first laid out as ONE bit stream in LDS (row r at bits 45r..45r+44; each stream
+// dword is cut from at most two rows), so every output dword is one nibble of the stream,
+// spread to 4 bytes by a multiply: bit i of n moves to bit 8i in n * 0x204081.
+__device__ __forceinline__ void store_mask_block(BlockLDS &L, int rows, int8_t *dst) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int b = 4 * d + q;
-        const int r = b / 45, c = b - 45 * r;
-        const uint32_t bit = b < nbytes ? (uint32_t)((L.mask[r < 64 ? r : 63] >> c) & 1ull) : 0u;
-        v |= bit << (8 * q);
+    for (int k = 0; k < 2; ++k) {
+        const int w = lane_id() + 64 * k;  // stream dword w: bits 32w .. 32w+31
+        if (w < kMaskStreamWords) {
+            const int r0 = (32 * w) / 45, c0 = 32 * w - 45 * r0;  // first bit: row r0, column c0
+            const uint64_t m0 = L.mask[r0], m1 = r0 + 1 < 64 ? L.mask[r0 + 1] : 0ull;
+            // columns c0..44 of row r0, then row r0+1 from column 0
+            const uint64_t lo = m0 >> c0, hi = (c0 > 13) ? (m1 << (45 - c0)) : 0ull;
+            L.mbits[w] = (uint32_t)(lo | hi);
+        }
     }
-    return v;
-}
-
-__device__ __forceinline__ void store_mask_block(const BlockLDS &L, int rows, int8_t *dst) {
+    wave_lds_sync();
     const int nbytes = rows * 45;
     const int full = nbytes >> 2;
-    constexpr int U = 4;
-    int d = lane_id();
-    for (; d + 64 * (U - 1) < full; d += 64 * U) {
-        uint32_t v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = mask_dword(L, d + 64 * u, nbytes);
-#pragma unroll
-        for (int u = 0; u < U; ++u) *reinterpret_cast<uint32_t *>(dst + 4 * (d + 64 * u)) = v[u];
+    uint32_t *out = reinterpret_cast<uint32_t *>(dst);
+    for (int d = lane_id(); d < full; d += 64) {
+        const uint32_t nib = (L.mbits[d >> 3] >> (4 * (d & 7))) & 0xFu;
+        out[d] = (nib * 0x00204081u) & 0x01010101u;
     }
-    for (; d < full; d += 64) *reinterpret_cast<uint32_t *>(dst + 4 * d) = mask_dword(L, d, nbytes);
-    for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) {
-        const int r = b / 45;
-        dst[b] = (int8_t)((L.mask[r] >> (b - 45 * r)) & 1ull);
-    }
+    for (int b = (full << 2) + lane_id(); b < nbytes; b += 64)
+        dst[b] = (int8_t)((L.mbits[b >> 5] >> (b & 31)) & 1u);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -710,7 +770,12 @@ __device__ __forceinline__ void store_mask_block(const BlockLDS &L, int rows, in
 // uniform loop over MT outputs: every lane advances its own stream by one output per
 // iteration and its own shuffle state machine accepts or rejects it (_randbelow), so the cost
 // is the wave's maximum output count, not the sum of per-draw maxima.
-__device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec, uint8_t *scr) {
+struct Deal {
+    uint32_t board[3], nob0, nob1;  // SW_BOARD.., SW_NOB0, SW_NOB1 of the dealt table
+};
+__device__ __forceinline__ Deal empty_deal() { return Deal{{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, 0xFFFFFFFFu, 0xFFu}; }
+
+__device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec, uint8_t *scr, Deal &out) {
     for (int i = 0; i < 100; ++i) scr[i] = (uint8_t)(i < 90 ? i : i - 90);
     MTStream ms;
     ms.init(seed);
@@ -743,36 +808,33 @@ __device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec
     uint4 *r4 = reinterpret_cast<uint4 *>(rec);
 #pragma unroll
     for (int q = 0; q < 6; ++q) r4[q] = s4[q];
-    uint32_t board[3];
 #pragma unroll
     for (int t = 0; t < 3; ++t) {  // board[tier][i] = deck.pop()
         const int b = tier_base(t), n = tier_size(t);
-        board[t] = (uint32_t)scr[b + n - 1] | ((uint32_t)scr[b + n - 2] << 8) | ((uint32_t)scr[b + n - 3] << 16) |
-                   ((uint32_t)scr[b + n - 4] << 24);
+        out.board[t] = (uint32_t)scr[b + n - 1] | ((uint32_t)scr[b + n - 2] << 8) | ((uint32_t)scr[b + n - 3] << 16) |
+                       ((uint32_t)scr[b + n - 4] << 24);
     }
     const int nn = P + 1 < 10 ? P + 1 : 10;  // state.py:194 (<= 5 for P <= 4)
-    uint32_t nob0 = 0, nob1;
+    out.nob0 = 0;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) nob0 |= (s < nn ? (uint32_t)scr[90 + s] : 0xFFu) << (8 * s);
-    nob1 = nn > 4 ? (uint32_t)scr[94] : 0xFFu;
-    uint4 tail0 = make_uint4(board[0], board[1], board[2], 36u | (26u << 8) | (16u << 16) | ((uint32_t)nn << 24));
-    uint4 tail1 = make_uint4(nob0, nob1, 1u, seed);
-    r4[6] = tail0;
-    r4[7] = tail1;
+    for (int s = 0; s < 4; ++s) out.nob0 |= (s < nn ? (uint32_t)scr[90 + s] : 0xFFu) << (8 * s);
+    out.nob1 = nn > 4 ? (uint32_t)scr[94] : 0xFFu;
+    reinterpret_cast<uint32_t *>(rec)[kRecSeed / 4] = seed;
     return flags;
 }
 
 template <int P>
-__device__ __forceinline__ void fresh_state(Tab<P> &T, uint32_t status, uint4 tail0, uint4 tail1) {
+__device__ __forceinline__ void fresh_state(Tab<P> &T, uint32_t status, const Deal &d) {
+    constexpr uint32_t nn = P + 1 < 10 ? P + 1 : 10;
     T.sw[SW_BANK0] = 0x04040404u;                       // DEFAULT_BANK, state.py:26-33
     T.sw[SW_BANK1] = 4u | (5u << 8) | (0u << 16) | (1u << 24);  // to_play 0, turn_count 1
     T.sw[SW_MISC] = status;                              // move_count 0, winner None
-    T.sw[SW_BOARD] = tail0.x;
-    T.sw[SW_BOARD + 1] = tail0.y;
-    T.sw[SW_BOARD + 2] = tail0.z;
-    T.sw[SW_DECK] = tail0.w;
-    T.sw[SW_NOB0] = tail1.x;
-    T.sw[SW_NOB1] = tail1.y;
+    T.sw[SW_BOARD] = d.board[0];
+    T.sw[SW_BOARD + 1] = d.board[1];
+    T.sw[SW_BOARD + 2] = d.board[2];
+    T.sw[SW_DECK] = 36u | (26u << 8) | (16u << 16) | (nn << 24);  // 40, 30, 20 minus the 4 dealt
+    T.sw[SW_NOB0] = d.nob0;
+    T.sw[SW_NOB1] = d.nob1;
 #pragma unroll
     for (int q = 0; q < P; ++q) {
         T.pw[q][0] = T.pw[q][1] = T.pw[q][2] = 0u;
@@ -803,47 +865,34 @@ __device__ __forceinline__ void store_pcg(const KArena &A, int t, const Pcg64 &g
     q[1] = g.u32;
 }
 
-__device__ __forceinline__ uint32_t *needy_list(const KArena &A, int parity) {
-    return A.needy + 64 + (size_t)parity * A.n;
+__device__ __forceinline__ Deal load_pool(const KArena &A, int t) {
+    Deal d;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d.board[k] = A.pool[(size_t)(PL_BOARD + k) * A.n + t];
+    d.nob0 = A.pool[(size_t)PL_NOB0 * A.n + t];
+    d.nob1 = A.pool[(size_t)PL_NOB1 * A.n + t];
+    return d;
+}
+__device__ __forceinline__ void store_pool(const KArena &A, int t, const Deal &d) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) A.pool[(size_t)(PL_BOARD + k) * A.n + t] = d.board[k];
+    A.pool[(size_t)PL_NOB0 * A.n + t] = d.nob0;
+    A.pool[(size_t)PL_NOB1 * A.n + t] = d.nob1;
 }
 
-// queue `t` for the next pool refill (wave-aggregated: one atomic per wave).  Refill epochs
-// alternate between two lists so the refill kernel can zero the other list's count itself.
-__device__ __forceinline__ void push_needy(const KArena &A, bool want, uint32_t t) {
-    const uint64_t b = __ballot(want);
-    if (b == 0) return;
-    const int leader = __ffsll((unsigned long long)b) - 1;
-    const int par = A.epoch & 1;
-    uint32_t base = 0;
-    if (lane_id() == leader) base = atomicAdd(&A.needy[par], (uint32_t)__popcll(b));
-    base = __shfl(base, leader);
-    const int rank = __popcll(b & ((1ull << lane_id()) - 1ull));
-    if (want) needy_list(A, par)[base + rank] = t;
-}
-
-// reset() without a seed / same-step autoreset: the next episode is the pool deal
-// (envs/splendor_env.py:43-44 continued np_random stream).  Returns SPL_F_* bits.
+// Deal the next episode into slot record `slot` from the table's engine-seed stream
+// (envs/splendor_env.py:43-44: reset() continues self.np_random).  Returns SPL_F_* bits.
+// A table never reset with a seed has no stream: it deals engine seed 0 (documented in
+// splendor_amd.h) and its record stays unseeded.
 template <int P>
-__device__ __forceinline__ uint32_t reset_from_pool(Tab<P> &T, const KArena &A, int t, uint8_t *scr, bool &push) {
-    const uint32_t misc = T.sw[SW_MISC];
-    const int nxt = ((misc & ST_ACTIVE) ? 1 : 0) ^ 1;
-    uint8_t *rec = slot_rec(A, t, nxt);
-    uint32_t *rw = reinterpret_cast<uint32_t *>(rec);
-    uint32_t flags = 0;
-    if (rw[kRecReady / 4] == 0u) {  // pool not refilled yet: deal inline (correct, just slower)
-        Pcg64 g = load_pcg(A, t);
-        const uint32_t seed = g.engine_seed();
+__device__ __forceinline__ uint32_t deal_next(const KArena &A, int t, int slot, uint8_t *scr, Deal &d) {
+    Pcg64 g = load_pcg(A, t);
+    uint32_t seed = 0u;
+    if (g.valid()) {
+        seed = g.engine_seed();
         store_pcg(A, t, g);
-        flags |= deal_into(seed, P, rec, scr);
     }
-    const uint4 tail0 = *reinterpret_cast<const uint4 *>(rec + kRecBoard);
-    const uint4 tail1 = *reinterpret_cast<const uint4 *>(rec + kRecNob0);
-    rw[kRecReady / 4] = 0u;  // now live
-    const bool pending = (misc & ST_PENDING) != 0;
-    push = !pending;
-    const uint32_t status = (nxt ? ST_ACTIVE : 0u) | ST_PENDING;
-    fresh_state(T, status, tail0, tail1);
-    return flags;
+    return deal_into(seed, P, slot_rec(A, t, slot), scr, d);
 }
 
 template <int P>
@@ -928,6 +977,12 @@ __global__ __launch_bounds__(64) void k_build_lut(uint4 *lut) {
 }
 
 // SplendorEnv.step for every table (envs/splendor_env.py:51-90) + same-step autoreset.
+//
+// Every global load of the step (state, action, pool deal words, the deck card the action
+// pops, the token-return table entry it consults) is issued in the first microseconds, before
+// any wave has started its stores; from there to the block stores at the end the wave touches
+// only registers and LDS.  A load issued later would queue behind the other waves' observation
+// writes (tens of MB in flight) and its wave would become the kernel's tail.
 template <int P>
 __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     __shared__ BlockLDS L;
@@ -941,11 +996,35 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
 
     Tab<P> T;
     int action = 0;
-    if (valid) {
+    Deal pool = empty_deal();
+    if (valid && !abl(ABL_LOAD)) {
         load_tab(T, A, t);
         action = S.actions[t];
+        if (S.autoreset) pool = load_pool(A, t);
     } else {
-        fresh_state(T, 0u, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u), make_uint4(0xFFFFFFFFu, 0xFFu, 0u, 0u));
+        fresh_state(T, 0u, empty_deal());
+    }
+    const bool live_tab = valid && !is_terminal(T.sw);
+    const bool in_range = action >= 0 && action < SPL_NUM_ACTIONS;
+    const int tp = get_to_play(T.sw);
+    uint32_t pw4[4];
+    get_player(T, tp, pw4);
+    const Pl cur = unpack_pl(pw4);
+    int bank[6];
+    get_bank(T.sw, bank);
+    // dependent prefetches: the card this action pops, the table entry it consults
+    const int ptier = pop_tier(action);
+    uint32_t top = 0xFFu;
+    if (live_tab && ptier >= 0) {
+        const int len = (int)bget(T.sw[SW_DECK], ptier);
+        const uint8_t *live = slot_rec(A, t, (T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0);
+        if (len > 0) top = live[tier_base(ptier) + len - 1];
+    }
+    int pre_key = -1;
+    uint4 pre_e = make_uint4(0u, 0u, 0u, 0u);
+    if (live_tab && in_range) {
+        pre_key = predict_lut_key(cur, bank, action, get_turn(T.sw), tp);
+        if (pre_key >= 0) pre_e = Tb.lut[pre_key];
     }
     wave_lds_sync();
     STAMP(1);
@@ -953,19 +1032,12 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     uint32_t flags = 0;
     float reward = 0.0f;
     bool term = false;
-    uint64_t outmask = 0;
-    const uint8_t *live = slot_rec(A, valid ? t : 0, (T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0);
+    bool want_mask = false;  // info["action_mask"] of the table's state after this step
     if (valid) {
-        if (is_terminal(T.sw)) {                                  // :53-54 RuntimeError
+        if (!live_tab) {                                          // :53-54 RuntimeError
             flags = SPL_F_AFTER_TERMINAL;
         } else {
             // :55 mask = legal_moves(state): only "any legal?" and mask[action] are needed here
-            uint32_t pw4[4];
-            get_player(T, get_to_play(T.sw), pw4);
-            const Pl cur = unpack_pl(pw4);
-            int bank[6];
-            get_bank(T.sw, bank);
-            const bool in_range = action >= 0 && action < SPL_NUM_ACTIONS;
             const bool anyl = abl(ABL_LEGAL_PRE) || any_legal(T.sw, cur, bank, L);
             const bool ok = abl(ABL_LEGAL_PRE) || (in_range && action_legal(T.sw, cur, bank, action, L));
             if (!anyl) {                                          // :56-61 no legal move: draw
@@ -973,16 +1045,16 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
                 T.sw[SW_BANK1] &= 0xFF00FFFFu;                    // to_play = 0
                 term = true;
                 flags = SPL_F_DRAW;
-            } else if (!in_range) {                               // :62-63 ValueError
+            } else if (!in_range) {                               // :62-63 ValueError, mask of the unchanged state
                 flags = SPL_F_OOB;
-                outmask = legal_mask(T.sw, cur, bank, L);
-            } else if (!ok) {                                     // :64-66 illegal
+                want_mask = true;
+            } else if (!ok) {                                     // :64-66 illegal, mask of the unchanged state
                 flags = SPL_F_ILLEGAL;
                 reward = -0.01f;
-                outmask = legal_mask(T.sw, cur, bank, L);
+                want_mask = true;
             } else {
                 STAMP(2);
-                if (!abl(ABL_APPLY)) apply_action(T, action, live, L, Tb.lut, flags);  // :68
+                if (!abl(ABL_APPLY)) apply_action(T, action, top, L, Tb.lut, pre_key, pre_e, flags);  // :68
                 STAMP(3);
                 term = is_terminal(T.sw);                         // :70
                 if (term) {                                       // :71-80
@@ -991,88 +1063,53 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
                     reward = (w < 0 && tl) ? -0.1f : (w < 0 ? 0.0f : (w == P - 1 ? 1.0f : -1.0f));
                     flags |= tl ? SPL_F_TURN_LIMIT : 0u;          // :82-83
                 } else {
-                    outmask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);  // :81
+                    want_mask = true;                             // :81
                 }
             }
         }
     }
+    // one legal_moves evaluation per lane (a single call site keeps one copy in the code)
+    uint64_t outmask = 0;
+    if (want_mask) outmask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);
     const int8_t wnr = (int8_t)get_winner(T.sw);
     STAMP(4);
 
-    // same-step autoreset: start the pool-record loads and the refill-queue slot now, consume
-    // them after the final-observation block so their latency hides behind it
-    const bool do_reset = valid && term && S.autoreset && !abl(ABL_RESET);
-    const int nxt = ((T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0) ^ 1;
-    uint8_t *prec = slot_rec(A, do_reset ? t : 0, nxt);
-    uint32_t p_ready = 1u;
-    uint4 p_tail0 = make_uint4(0u, 0u, 0u, 0u), p_tail1 = make_uint4(0u, 0u, 0u, 0u);
-    if (do_reset) {
-        p_ready = reinterpret_cast<const uint32_t *>(prec)[kRecReady / 4];
-        p_tail0 = *reinterpret_cast<const uint4 *>(prec + kRecBoard);
-        p_tail1 = *reinterpret_cast<const uint4 *>(prec + kRecNob0);
-    }
-    const bool push = do_reset && !(T.sw[SW_MISC] & ST_PENDING);
-    const uint64_t pushb = __ballot(push);
-    const int par = A.epoch & 1;
-    uint32_t qbase = 0;
-    if (pushb) {
-        const int leader = __ffsll((unsigned long long)pushb) - 1;
-        if (lane == leader) qbase = atomicAdd(&A.needy[par], (uint32_t)__popcll(pushb));
-    }
-
-    STAMP(5);
-    // episode statistics (player 0's final reward, envs/splendor_env.py:92-115): read now
-    float ep_r = 0.0f;
-    uint32_t ep_c = 0u;
-    if (valid && term) {
-        if (S.ep_return) ep_r = S.ep_return[t];
-        if (S.ep_count) ep_c = S.ep_count[t];
-    }
-    // terminal observation for gymnasium's info["final_observation"], staged in LDS: this wave
-    // issues no store before its block stores (a store issued mid-kernel stalls behind the
-    // other waves' observation drain and the wave falls behind)
+    // terminal observation for gymnasium's info["final_observation"], staged in LDS and stored
+    // with everything else at the end
     const bool want_final = S.autoreset && S.final_obs != nullptr && !abl(ABL_FINAL);
     const uint64_t fin = __ballot(valid && term && want_final);
     if (valid && term && want_final) encode_row(T, &L.frows[lane * kObsDim], L);
     const int fin_moves = get_moves(T.sw);
-    float ep_add = 0.0f;
+    float ep_add = 0.0f;  // player 0's final reward (envs/splendor_env.py:92-115)
     if (valid && term) {
         const int w = get_winner(T.sw);
         const bool tl = (T.sw[SW_MISC] & ST_TURN_LIMIT) != 0;
         ep_add = w < 0 ? (tl ? -0.1f : 0.0f) : (w == 0 ? 1.0f : -1.0f);
     }
-    STAMP(6);
-    if (do_reset) {  // envs/splendor_env.py:43-44 with the continued np_random stream
-        if (p_ready == 0u) {  // pool not refilled yet: deal inline (correct, just slower)
-            Pcg64 g = load_pcg(A, t);
-            const uint32_t seed = g.engine_seed();
-            store_pcg(A, t, g);
-            flags |= deal_into(seed, P, prec, &L.rows[lane * kScratchStride]);
-            p_tail0 = *reinterpret_cast<const uint4 *>(prec + kRecBoard);
-            p_tail1 = *reinterpret_cast<const uint4 *>(prec + kRecNob0);
-        }
-        fresh_state(T, (nxt ? ST_ACTIVE : 0u) | ST_PENDING, p_tail0, p_tail1);
+    STAMP(5);
+    const bool do_reset = valid && term && S.autoreset && !abl(ABL_RESET);
+    if (do_reset) {  // envs/splendor_env.py:43-44: the pool deal continues the np_random stream
+        const int nxt = ((T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0) ^ 1;
+        if (T.sw[SW_MISC] & ST_PENDING)  // pool not refilled yet: deal inline (correct, slower)
+            flags |= deal_next<P>(A, t, nxt, &L.rows[lane * kScratchStride], pool);
+        fresh_state(T, (nxt ? ST_ACTIVE : 0u) | ST_PENDING, pool);
         flags |= SPL_F_RESET;
-        outmask = legal_of(T, L);
+        outmask = kFreshDealMask;
     }
-    STAMP(7);
+    STAMP(6);
     wave_lds_sync();  // deal scratch (rows) free again
 
     // observation + mask of the current state, block stores
     if (!abl(ABL_ENCODE)) encode_row(T, &L.rows[lane * kObsDim], L);
     L.mask[lane] = outmask;
-    // land the remaining loads (queue slot, episode stats) before the first store of this wave
-    qbase = opaque(qbase);
-    ep_r = __uint_as_float(opaque(__float_as_uint(ep_r)));
-    ep_c = opaque(ep_c);
-    STAMP(8);
+    STAMP(7);
     wave_lds_sync();
-    STAMP(9);
+    STAMP(8);
     int32_t *obs_dst = S.obs + (size_t)t0 * kObsDim;
     if (!abl(ABL_STORE)) {
-        store_obs_block(L, rows, obs_dst);
-        STAMP(10);
-        store_mask_block(L, rows, S.mask + (size_t)t0 * 45);
+        if (!abl(ABL_OBS_STORE)) store_obs_block(L, rows, obs_dst);
+        STAMP(9);
+        if (!abl(ABL_MASK_STORE)) store_mask_block(L, rows, S.mask + (size_t)t0 * 45);
     }
     uint64_t b = fin;  // terminal rows of this wave (about one per wave per step)
     while (b) {
@@ -1081,34 +1118,34 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
         int32_t *dst = S.final_obs + (size_t)(t0 + r) * kObsDim;
         for (int e = lane; e < kObsDim; e += 64) dst[e] = (int32_t)L.frows[r * kObsDim + e];
     }
-    if (valid && term) {
-        if (S.ep_return) S.ep_return[t] = ep_r + ep_add;
-        if (S.ep_count) S.ep_count[t] = ep_c + 1u;
-        if (want_final && fin_moves > 255) S.final_obs[(size_t)t * kObsDim + 295] = fin_moves;
+    STAMP(10);
+    if (valid && term) {  // no-return atomics: nothing to wait for
+        if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_add);
+        if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
     }
-    if (pushb) {  // refill queue entry (wave-aggregated atomic issued above)
-        const int leader = __ffsll((unsigned long long)pushb) - 1;
-        qbase = __shfl(qbase, leader);
-        if (push) needy_list(A, par)[qbase + __popcll(pushb & ((1ull << lane) - 1ull))] = (uint32_t)t;
-    }
-    if (do_reset) reinterpret_cast<uint32_t *>(prec)[kRecReady / 4] = 0u;  // pool record now live
-    STAMP(11);
-    if (__any(valid && get_moves(T.sw) > 255)) {
-        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): block store of this dword has left
-        if (valid && get_moves(T.sw) > 255) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
+    // move_count above 255 (crafted states only) does not fit the byte staging: patch it after
+    // this wave's block stores of the same dwords have left
+    const bool patch = valid && get_moves(T.sw) > 255;
+    const bool fpatch = valid && term && want_final && fin_moves > 255;
+    if (__any(patch || fpatch)) {
+        __builtin_amdgcn_s_waitcnt(0);
+        if (patch) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
+        if (fpatch) S.final_obs[(size_t)t * kObsDim + 295] = fin_moves;
     }
     if (valid) {
-        S.reward[t] = reward;
-        S.terminated[t] = term ? 1 : 0;
-        S.flags[t] = (uint8_t)flags;
-        if (S.winner) S.winner[t] = wnr;
+        if (!abl(ABL_SMALL_OUT)) {
+            S.reward[t] = reward;
+            S.terminated[t] = term ? 1 : 0;
+            S.flags[t] = (uint8_t)flags;
+            if (S.winner) S.winner[t] = wnr;
+        }
         if (S.next_actions) {
             const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
             S.next_actions[t] = sample_uniform(outmask, S.policy_seed, (uint64_t)(S.table0 + t), ply);
         }
-        store_tab(T, A, t);
+        if (!abl(ABL_TAB_STORE)) store_tab(T, A, t);
     }
-    STAMP(12);
+    STAMP(11);
 }
 
 // Explicit reset (SplendorEnv.reset / VectorEnv.reset), then observation + mask of all tables.
@@ -1124,11 +1161,10 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
     load_tables_lds(L, Tb);
     Tab<P> T;
     if (valid) load_tab(T, A, t);
-    else fresh_state(T, 0u, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u), make_uint4(0xFFFFFFFFu, 0xFFu, 0u, 0u));
+    else fresh_state(T, 0u, empty_deal());
     wave_lds_sync();
     const bool doit = valid && (mask_in == nullptr || mask_in[t] != 0);
     uint8_t *scr = &L.rows[lane * kScratchStride];
-    bool push = false;
     if (doit) {
         if (pcg_in) {  // reset(seed=...): restart this table's np_random stream, deal 2 episodes
             Pcg64 g;
@@ -1138,22 +1174,22 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
             g.inc_lo = pcg_in[4 * (size_t)t + 3];
             g.has32 = 0;
             g.u32 = 0;
-            uint8_t *r0 = slot_rec(A, t, 0), *r1 = slot_rec(A, t, 1);
+            Deal d0, d1;
             const uint32_t seed0 = g.engine_seed();
-            deal_into(seed0, P, r0, scr);
+            deal_into(seed0, P, slot_rec(A, t, 0), scr, d0);
             const uint32_t seed1 = g.engine_seed();
-            deal_into(seed1, P, r1, scr);
+            deal_into(seed1, P, slot_rec(A, t, 1), scr, d1);
             store_pcg(A, t, g);
-            const uint4 tail0 = *reinterpret_cast<const uint4 *>(r0 + kRecBoard);
-            const uint4 tail1 = *reinterpret_cast<const uint4 *>(r0 + kRecNob0);
-            reinterpret_cast<uint32_t *>(r0)[kRecReady / 4] = 0u;
-            // keep ST_PENDING: a queued refill entry (if any) must stay unique
-            fresh_state(T, T.sw[SW_MISC] & ST_PENDING, tail0, tail1);
+            store_pool(A, t, d1);
+            fresh_state(T, 0u, d0);  // record 0 live, record 1 the ready pool
         } else {       // reset() without a seed: continue the stream (pool deal)
-            reset_from_pool(T, A, t, scr, push);
+            const int nxt = ((T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0) ^ 1;
+            Deal d;
+            if (T.sw[SW_MISC] & ST_PENDING) deal_next<P>(A, t, nxt, scr, d);
+            else d = load_pool(A, t);
+            fresh_state(T, (nxt ? ST_ACTIVE : 0u) | ST_PENDING, d);
         }
     }
-    push_needy(A, push, (uint32_t)t);
     wave_lds_sync();
     if (obs || mask_out) {
         encode_row(T, &L.rows[lane * kObsDim], L);
@@ -1165,31 +1201,26 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
     if (valid) store_tab(T, A, t);
 }
 
-// Pool refill: deal the next episode of every queued table (compacted list; the grid covers
-// the worst case and idle waves exit at once).
+// Pool refill: deal the next episode of every table whose pool was consumed (ST_PENDING).
+// Waves without such a table exit after one coalesced read of the status plane.
+// The deal is one long serial chain per lane (CPython init_by_array + the shuffle's MT
+// outputs), so a wave's time is latency-bound and the same whether it carries 5 or 64 pending
+// tables: the scratch is padded to a quarter of the CU's LDS so the dispatcher spreads the
+// waves one per SIMD over the whole chip instead of stacking them on a few CUs.
+constexpr int kRefillLds = 40 * 1024;
 template <int P>
 __global__ __launch_bounds__(64) void k_refill(KArena A) {
-    __shared__ uint8_t scr_all[64 * kScratchStride] __attribute__((aligned(16)));
-    const int lane = lane_id();
-    const int par = A.epoch & 1;
-    const uint32_t count = A.needy[par];
-    if (blockIdx.x == 0 && lane == 0) A.needy[par ^ 1] = 0u;  // the next epoch appends there
-    const uint32_t e = blockIdx.x * 64u + (uint32_t)lane;
-    if (blockIdx.x * 64u >= count) return;  // whole wave idle
-    if (e < count) {
-        const int t = (int)needy_list(A, par)[e];
-        const size_t mi = (size_t)SW_MISC * A.n + t;
-        const uint32_t misc = A.planes[mi];
-        const int nxt = ((misc & ST_ACTIVE) ? 1 : 0) ^ 1;
-        uint8_t *rec = slot_rec(A, t, nxt);
-        if (reinterpret_cast<const uint32_t *>(rec)[kRecReady / 4] == 0u) {
-            Pcg64 g = load_pcg(A, t);
-            const uint32_t seed = g.engine_seed();
-            store_pcg(A, t, g);
-            deal_into(seed, P, rec, &scr_all[lane * kScratchStride]);
-        }
-        A.planes[mi] = misc & ~ST_PENDING;
-    }
+    __shared__ uint8_t scr_all[kRefillLds] __attribute__((aligned(16)));
+    const int t = blockIdx.x * 64 + lane_id();
+    if (t >= A.n) return;
+    const size_t mi = (size_t)SW_MISC * A.n + t;
+    const uint32_t misc = A.planes[mi];
+    if (!(misc & ST_PENDING)) return;
+    const int nxt = ((misc & ST_ACTIVE) ? 1 : 0) ^ 1;
+    Deal d;
+    deal_next<P>(A, t, nxt, &scr_all[lane_id() * kScratchStride], d);
+    store_pool(A, t, d);
+    A.planes[mi] = misc & ~ST_PENDING;
 }
 
 // Observation and/or mask of the current state (spl_encode / spl_legal).
@@ -1204,7 +1235,7 @@ __global__ __launch_bounds__(64) void k_observe(KArena A, KTables Tb, int32_t *o
     load_tables_lds(L, Tb);
     Tab<P> T;
     if (valid) load_tab(T, A, t);
-    else fresh_state(T, 0u, make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0u), make_uint4(0xFFFFFFFFu, 0xFFu, 0u, 0u));
+    else fresh_state(T, 0u, empty_deal());
     wave_lds_sync();
     if (obs) encode_row(T, &L.rows[lane * kObsDim], L);
     L.mask[lane] = valid ? legal_of(T, L) : 0ull;  // engine legal_moves (no terminal check)
@@ -1353,7 +1384,6 @@ __global__ __launch_bounds__(64) void k_upload(KArena A, int first, int count, c
     uint8_t *rec = slot_rec(A, t, (old_misc & ST_ACTIVE) ? 1 : 0);
     for (int tt = 0; tt < 3; ++tt)
         for (int k = 0; k < tier_size(tt); ++k) rec[tier_base(tt) + k] = (uint8_t)(k < v.deck_len[tt] ? v.decks[tt][k] : 0xFF);
-    reinterpret_cast<uint32_t *>(rec)[kRecReady / 4] = 0u;
 }
 
 }  // namespace spl
@@ -1401,8 +1431,8 @@ static int check_arena(const spl_ctx_t *ctx, const spl_arena_t *a) {
 static KArena karena(const spl_arena_t *a) {
     const ArenaLayout L = arena_layout(a->n, a->players);
     uint8_t *b = static_cast<uint8_t *>(a->base);
-    return KArena{reinterpret_cast<uint32_t *>(b + L.planes), b + L.slots, b + L.pcg,
-                  reinterpret_cast<uint32_t *>(b + L.needy), a->n, (int)(a->epoch & 1)};
+    return KArena{reinterpret_cast<uint32_t *>(b + L.planes), reinterpret_cast<uint32_t *>(b + L.pool), b + L.slots,
+                  b + L.pcg, a->n};
 }
 
 static int launch_check() {
@@ -1534,8 +1564,12 @@ int spl_reset(spl_ctx_t *ctx, spl_arena_t *arena, const uint64_t *pcg, const uin
 
 int spl_arena_init(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
     if (int r = check_arena(ctx, arena)) return r;
-    HIP_TRY(hipMemsetAsync(arena->base, 0, (size_t)spl_arena_bytes(arena->n, arena->players),
-                           static_cast<hipStream_t>(stream)));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipMemsetAsync(arena->base, 0, (size_t)spl_arena_bytes(arena->n, arena->players), s));
+    // no pool deal yet: a reset() without seed deals inline, the refill kernel deals it
+    const KArena A = karena(arena);
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(A.planes + (size_t)SW_MISC * arena->n), (int)ST_PENDING,
+                              (size_t)arena->n, s));
     arena->steps = 0;
     arena->epoch = 0;
     return SPL_OK;

@@ -21,8 +21,10 @@
 // Deck storage: two 128-byte SLOT RECORDS per table (AoS, [n][2][128]).  The active record
 // holds the live deck (bytes 0..89: tier 1 at 0, tier 2 at 40, tier 3 at 70, list order, top
 // = deck_len-1); the other is the POOL: the next episode's deal, prepared ahead from the
-// table's engine-seed stream.  Record bytes 96..123 hold the deal's board / deck / noble words
-// (SW_BOARD.., SW_DECK, SW_NOB0, SW_NOB1), a ready word and the engine seed.
+// table's engine-seed stream.  The pool deal's board and noble words sit in their own word
+// planes (PL_*), read with the state at the top of every step, so a same-step autoreset needs
+// no late gather.  ST_PENDING marks a table whose pool was consumed (the refill kernel deals
+// it again); record bytes 124..127 keep the deal's engine seed (diagnostic).
 #pragma once
 #include <stdint.h>
 
@@ -45,15 +47,13 @@ __host__ __device__ constexpr int pw_index(int p, int k) { return SW_COUNT + 4 *
 constexpr uint32_t ST_GAME_OVER = 1u << 16;
 constexpr uint32_t ST_TURN_LIMIT = 1u << 17;
 constexpr uint32_t ST_ACTIVE = 1u << 18;   // which slot record holds the live deck
-constexpr uint32_t ST_PENDING = 1u << 19;  // table is queued for a pool refill
+constexpr uint32_t ST_PENDING = 1u << 19;  // pool consumed (or never dealt): refill deals it
 
 constexpr int kSlotBytes = 128;
-constexpr int kRecBoard = 96;   // 3 words: board at deal
-constexpr int kRecDeck = 108;   // SW_DECK at deal
-constexpr int kRecNob0 = 112;   // SW_NOB0 at deal
-constexpr int kRecNob1 = 116;   // SW_NOB1 at deal
-constexpr int kRecReady = 120;  // 1 = dealt and unused
 constexpr int kRecSeed = 124;   // engine seed of the deal (diagnostic)
+
+// pool planes: the pool deal's SW_BOARD.. and SW_NOB0/1 words (SW_DECK at deal is a constant)
+enum : int { PL_BOARD = 0, PL_NOB0 = 3, PL_NOB1 = 4, PL_COUNT = 5 };
 constexpr int kPcgBytes = 64;   // per-table numpy PCG64 record: s_hi s_lo inc_hi inc_lo has32 u32
 
 __host__ __device__ constexpr int tier_base(int t) { return t == 0 ? 0 : (t == 1 ? 40 : 70); }
@@ -66,7 +66,7 @@ constexpr int kLutEntries = kLutTc * kLutTp * kLutSt * kLutSb;
 constexpr int kLutOutputs = 40;  // top 3 bits of the first 40 MT outputs, 10 per word
 
 struct ArenaLayout {
-    int64_t planes, slots, pcg, needy, total;
+    int64_t planes, pool, slots, pcg, total;
 };
 
 __host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
@@ -74,10 +74,10 @@ __host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) & ~int
 __host__ __device__ inline ArenaLayout arena_layout(int64_t n, int P) {
     ArenaLayout L;
     L.planes = 0;
-    L.slots = align256(L.planes + (int64_t)num_words(P) * n * 4);
+    L.pool = align256(L.planes + (int64_t)num_words(P) * n * 4);
+    L.slots = align256(L.pool + (int64_t)PL_COUNT * n * 4);
     L.pcg = align256(L.slots + n * 2 * kSlotBytes);
-    L.needy = align256(L.pcg + n * kPcgBytes);
-    L.total = align256(L.needy + (64 + 2 * n) * 4);  // 2 counts (+pad), 2 lists
+    L.total = align256(L.pcg + n * kPcgBytes);
     return L;
 }
 

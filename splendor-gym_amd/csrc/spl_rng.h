@@ -153,14 +153,19 @@ struct Pcg64 {
         u32 = (uint32_t)(n >> 32);
         return (uint32_t)n;
     }
-    // Generator.integers(0, 2**31 - 1) -> buffered_bounded_lemire_uint32(rng = 2**31 - 2)
+    // numpy's stream increment is (initseq << 1) | 1: an even one is an unseeded (zeroed) record
+    __device__ __forceinline__ bool valid() const { return (inc_lo & 1u) != 0; }
+
+    // Generator.integers(0, 2**31 - 1) -> buffered_bounded_lemire_uint32(rng = 2**31 - 2).
+    // A draw is rejected with probability 2 / 2**32, so the retry bound (never reached by a
+    // seeded stream: 2**-992) only keeps an invalid record from spinning forever.
     __device__ __forceinline__ uint32_t engine_seed() {
         const uint32_t rng_excl = 2147483647u;
         uint64_t m = (uint64_t)next32() * rng_excl;
         uint32_t left = (uint32_t)m;
         if (left < rng_excl) {
             const uint32_t threshold = (0xFFFFFFFFu - 2147483646u) % rng_excl;
-            while (left < threshold) {
+            for (int tries = 0; left < threshold && tries < 32; ++tries) {
                 m = (uint64_t)next32() * rng_excl;
                 left = (uint32_t)m;
             }

@@ -180,3 +180,19 @@ def test_sharded_equals_whole():
         got = torch.cat([parts[0].obs, parts[1].obs])
         assert torch.equal(got, whole.obs), k
         assert torch.equal(torch.cat([parts[0].flags, parts[1].flags]), whole.flags), k
+
+
+def test_unseeded_tables_deal_engine_seed_zero(orc):
+    """A table never reset with a seed has no engine-seed stream (zeroed PCG64 record): the
+    refill and an unseeded reset must terminate and deal engine seed 0 (splendor_amd.h)."""
+    n = 130
+    e = engine(n, 2)
+    e.refill()             # every table pending and unseeded
+    e.reset(seeds=None)    # flips to the pool deal
+    want = canon(orc.initial_state(2, 0))
+    recs = e.download()
+    for t in (0, 64, n - 1):
+        assert canon(table_to_view(recs[t])) == want, t
+    e.reset(seeds=None)    # pool consumed, not refilled: inline deal, same seed
+    recs = e.download()
+    assert canon(table_to_view(recs[5])) == want

@@ -51,9 +51,9 @@ def test_arena_layout_sizes():
         for P in (2, 3, 4):
             words = 9 + 4 * P
             b = int(lib.spl_arena_bytes(n, P))
-            # planes + 2 deck slots x 128 B + 64 B PCG record + refill list, 256-aligned regions
-            assert b >= words * 4 * n + 256 * n + 64 * n + 4 * (2 * n + 64)
-            assert b % 256 == 0 and b <= words * 4 * n + 320 * n + 8 * n + 4 * 256 + 256
+            # state planes + 5 pool planes + 2 deck slots x 128 B + 64 B PCG record, 256-aligned
+            assert b >= (words + 5) * 4 * n + 256 * n + 64 * n
+            assert b % 256 == 0 and b <= (words + 5) * 4 * n + 320 * n + 4 * 256
 
 
 def test_table_dtype_matches_oracle_struct():
@@ -173,3 +173,17 @@ def test_single_hip_runtime_after_load():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip().splitlines()[-1] == "1"
+
+
+def test_fresh_deal_mask_constant():
+    """k_step's autoreset mask is the constant kFreshDealMask (spl_engine.hip): legal_moves of
+    every fresh deal, checked here on the oracle over many deals and player counts."""
+    import re
+    from oracle.oracle import Oracle
+    src = open(os.path.join(REPO, "splendor-gym_amd", "csrc", "spl_engine.hip")).read()
+    assert re.search(r"kFreshDealMask = \(\(1ull << 15\) - 1ull\) \| \(\(\(1ull << 15\) - 1ull\) << 27\)", src)
+    want = ((1 << 15) - 1) | (((1 << 15) - 1) << 27)
+    o = Oracle()
+    for P in (2, 3, 4):
+        for s in range(0, 200000, 1999):
+            assert o.legal(o.initial_state(P, s)) == want, (P, s)

@@ -13,13 +13,18 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "splendor-gym_amd", "csrc")
 OUTD = os.path.join(REPO, "splendor-gym_amd", "ablate")
+IO = 1 | 2 | 4 | 8 | 16 | 32  # every compute phase compiled out: loads + stores only
 VARIANTS = {"full": 0, "no_legal_pre": 1, "no_apply": 2, "no_legal_post": 4, "no_final": 8, "no_reset": 16,
-            "no_encode": 32, "no_store": 64, "no_encode_store": 96, "only_io": 1 | 2 | 4 | 8 | 16 | 32}
+            "no_encode": 32, "no_store": 64, "no_encode_store": 96, "only_io": IO,
+            "only_io_no_mask": IO | 128, "only_io_no_small": IO | 256, "only_io_no_tab": IO | 512,
+            "only_io_no_obs": IO | 1024, "only_obs": IO | 128 | 256 | 512, "only_obs_noload": IO | 128 | 256 | 512 | 2048}
 
 
 def build():
     os.makedirs(OUTD, exist_ok=True)
-    for name, bits in VARIANTS.items():
+    names = [a for a in sys.argv[1:] if not a.startswith("--")] or list(VARIANTS)
+    for name in names:
+        bits = VARIANTS[name]
         out = os.path.join(OUTD, f"lib_{name}.so")
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", f"-DSPL_ABL={bits}",
                         "-shared", "-o", out, os.path.join(CSRC, "spl_engine.hip")], check=True)
@@ -51,7 +56,8 @@ print(json.dumps({"avg_us": 1000 * sum(ms) / len(ms), "min_us": 1000 * min(ms)})
 
 def run():
     res = {}
-    for name in VARIANTS:
+    names = [a for a in sys.argv[1:] if not a.startswith("--")] or list(VARIANTS)
+    for name in names:
         env = dict(os.environ, SPLENDOR_AMD_LIB=os.path.join(OUTD, f"lib_{name}.so"))
         r = subprocess.run([sys.executable, "-c", CHILD, REPO], env=env, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:

@@ -59,6 +59,13 @@ def main():
                         "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH"):
                 if ins in mean:
                     d[ins + "_per_wave"] = mean[ins] / mean["SQ_WAVES"]
+        if mean.get("SQC_ICACHE_REQ"):
+            d["icache_hit_rate"] = mean.get("SQC_ICACHE_HITS", 0) / mean["SQC_ICACHE_REQ"]
+            d["icache_misses_per_wave"] = mean.get("SQC_ICACHE_MISSES", 0) / max(mean.get("SQ_WAVES", 1), 1)
+        if mean.get("SQ_IFETCH"):
+            d["ifetch_per_wave"] = mean["SQ_IFETCH"] / max(mean.get("SQ_WAVES", 1), 1)
+            if "SQ_IFETCH_LEVEL" in mean:
+                d["ifetch_level_avg"] = mean["SQ_IFETCH_LEVEL"] / mean["SQ_IFETCH"]
         if "FETCH_SIZE" in mean:
             d["fetch_bytes"] = mean["FETCH_SIZE"] * 1024
         if "WRITE_SIZE" in mean:

@@ -1,7 +1,7 @@
 """Per-phase timeline of k_step from in-kernel s_memrealtime stamps (diagnostic build only).
 
     python tools/stamps.py            # build lib_stamps.so (-DSPL_STAMPS) and run on the GPU
-Lane 0 of every wave stamps 13 phase boundaries (see STAMP(i) in spl_engine.hip); we report, per
+Lane 0 of every wave stamps 12 phase boundaries (see STAMP(i) in spl_engine.hip); we report, per
 phase, the median and max over waves of the time since the kernel's first stamp (10 ns ticks).
 Stamped builds fence the scheduler around each stamp: read the SHARES, not the absolute length.
 """
@@ -12,8 +12,8 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "splendor-gym_amd", "ablate", "lib_stamps.so")
-NAMES = ["start", "loaded", "pre-legal", "applied", "step logic", "reset loads issued", "final obs",
-         "reset done", "encoded", "barrier", "obs stored", "mask stored", "end"]
+NAMES = ["start", "loaded+prefetched", "pre-apply", "applied", "step logic", "final obs", "reset done",
+         "encoded", "barrier", "obs stored", "mask+final stored", "end"]
 
 CHILD = r'''
 import sys, os, ctypes, json
@@ -57,7 +57,7 @@ def main():
     import numpy as np
     rows = []
     for run in runs:
-        a = np.array(run, dtype=np.int64)[:, :13]
+        a = np.array(run, dtype=np.int64)[:, :len(NAMES)]
         t0 = a[:, 0].min()
         rows.append(a - t0)
     a = np.concatenate(rows).astype(np.float64) * 0.01  # 100 MHz ticks -> microseconds
