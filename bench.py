@@ -1,21 +1,27 @@
 """Headline benchmark: env-steps/sec, 2-player Splendor, 65536 tables per MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--tables T] [--players P]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--tables T] [--players P] [--mode step|rollout] [--also]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 One "step" = one SplendorEnv.step on every table of the batch (BASELINE.json config 3: legal
 mask + uniform-random policy, same-step autoreset, obs int32[297] + mask int8[45] + reward +
-terminated written per table).  Actions are drawn on the device by the step kernel itself
-(fused Philox policy over the new mask), so the timed loop is spl_step launches plus the pool
-refill every 8 steps.  Inputs are resident in HBM before the timed region.
+terminated + flags written per table-step, terminal rows to final_obs).  Actions come from the
+device policy (Philox over the new mask).  Two launch shapes compute the same trajectories and
+write the same per-step outputs (tests/test_gpu_parity.py::test_rollout_equals_step_chain):
+  --mode step     one spl_step launch per env step (the drop-in step path)
+  --mode rollout  one spl_rollout launch per 16 env steps (state stays in registers; each
+                  step's stores drain while the next step computes)
+plus a pool refill every 16 steps.  Inputs are resident in HBM before the timed region; the
+timed region replays captured HIP graphs of 64 steps.
 
 Weak scaling: each rank owns `--tables` tables (global ids rank*T ...), no collective in the
 step path; after the timed region one all-gather (RCCL) collects episode returns.  value =
 tables x world x steps / max-over-ranks wall time.
 
-Printed on rank 0: ONE JSON line with the roofline of the step kernel (HIP events around every
-step launch in the timed region; algorithmic bytes per SURVEY.md §8d: 1370 B per 2-player
-table-step) and, at N=1, the CPU baseline (the C oracle port, one process per core).
+Printed on rank 0: ONE JSON line with the roofline of the mode's kernel (HIP events around each
+launch of an eager window right after the timed replays; algorithmic bytes per SURVEY.md §8d:
+1370 B per 2-player table-step) and, at N=1, the CPU baseline (the C oracle port, one process
+per core).
 """
 import argparse
 import ctypes
@@ -69,13 +75,13 @@ def cpu_baseline(players, procs, steps_per_proc):
                        "engine measured at 5.4k steps/s/core in SURVEY.md §6")}
 
 
-def load_pmc_traffic(players, tables):
-    """HBM bytes per step launch from the committed rocprofv3 PMC summary, if present."""
-    path = os.path.join(REPO, "profiles", "pmc_step_summary.json")
+def load_pmc_traffic(players, tables, mode, steps_per_launch):
+    """HBM bytes per launch of the mode's kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(REPO, "profiles", f"pmc_{mode}_summary.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("players") == players and d.get("tables") == tables:
+        if d.get("players") == players and d.get("tables") == tables and d.get("steps_per_launch", 1) == steps_per_launch:
             return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
     except (OSError, ValueError):
         pass
@@ -95,6 +101,10 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=1_000_000, help="env steps per CPU process")
     ap.add_argument("--graph-steps", type=int, default=64,
                     help="steps per captured HIP graph (multiple of 32); 0 = eager launches")
+    ap.add_argument("--mode", choices=("step", "rollout"), default="step",
+                    help="step: one spl_step launch per env step; rollout: one spl_rollout launch per "
+                         f"{REFILL_EVERY} env steps (same trajectories and outputs)")
+    ap.add_argument("--also", action="store_true", help="also measure the other mode (reported as other_mode)")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -137,87 +147,117 @@ def main():
     step_args = [mkargs(buf[0], buf[1]), mkargs(buf[1], buf[0])]
     ctx, desc = eng.ctx, ctypes.byref(eng.desc)
     stream = eng.stream()
+    R = REFILL_EVERY
 
-    def run(k0, k1, strm, ev=None):
-        """Steps k0..k1-1 (ply k+1 relative to ply_base), refill every REFILL_EVERY steps."""
-        for k in range(k0, k1):
-            sa = step_args[k & 1]
+    def run(mode, k0, k1, strm, ev=None):
+        """Steps k0..k1-1 (ply k+1 relative to ply_base), refill every R steps.  mode "step":
+        one spl_step launch per step; "rollout": one spl_rollout launch per R steps."""
+        per = 1 if mode == "step" else R
+        for i, k in enumerate(range(k0, k1, per)):
+            sa = step_args[(k // per) & 1]
             sa.ply = k + 1
             if ev is not None:
-                ev[0][k - k0].record()
-            _native.check(lib, lib.spl_step(ctx, desc, ctypes.byref(sa), strm))
+                ev[0][i].record()
+            if mode == "step":
+                _native.check(lib, lib.spl_step(ctx, desc, ctypes.byref(sa), strm))
+            else:
+                _native.check(lib, lib.spl_rollout(ctx, desc, ctypes.byref(sa), R, 0, strm))
             if ev is not None:
-                ev[1][k - k0].record()
-            if (k + 1) % REFILL_EVERY == 0:
+                ev[1][i].record()
+            if (k + per) % R == 0:
                 _native.check(lib, lib.spl_refill(ctx, desc, strm))
 
-    W = (args.warmup // (2 * REFILL_EVERY)) * (2 * REFILL_EVERY)  # action-buffer / refill-list parity
-    run(0, W, stream)
-    K = args.steps
-    G = args.graph_steps
-    graph, mode = None, "eager"
-    if G > 0:
-        if G % (2 * REFILL_EVERY) or K % G:
-            raise SystemExit("--graph-steps must be a multiple of 32 that divides --steps")
-        try:
-            torch.cuda.synchronize(dev)
-            ply_base.fill_(W)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                cap = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-                run(0, G, cap)
-                ply_base.add_(G)
-            mode = f"hipGraph replays of {G} steps"
-        except Exception as exc:  # capture unsupported: time eager launches instead
-            print(f"graph capture failed ({exc}); timing eager launches", file=sys.stderr)
-            graph, G = None, 0
-    barrier(dev)
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    if graph is not None:
-        for _ in range(K // G):
-            graph.replay()
-        ev = None
-    else:
-        ev = ([torch.cuda.Event(enable_timing=True) for _ in range(K)],
-              [torch.cuda.Event(enable_timing=True) for _ in range(K)])
-        run(W, W + K, stream, ev)
-    torch.cuda.synchronize(dev)
-    barrier(dev)
-    elapsed = time.perf_counter() - t0
-    elapsed_max = max_over_ranks(elapsed, device=dev)
-    if ev is None:
-        # ROCm rejects timing events as graph nodes ("External events are disallowed"), so the
-        # step-kernel duration comes from HIP events around each launch of an eager window of
-        # the same loop, run right after the timed replays on the same stream and state.
-        nwin = 64
-        ev = ([torch.cuda.Event(enable_timing=True) for _ in range(nwin)],
-              [torch.cuda.Event(enable_timing=True) for _ in range(nwin)])
-        ply_base.fill_(W + K + 1)
-        run(0, nwin, stream, ev)
+    def measure(mode, k_base):
+        """Warm up, capture, time K steps; returns the timing record.  Steps are numbered from
+        k_base so every measurement continues the same trajectories (ply_base)."""
+        W = (args.warmup // (2 * R)) * (2 * R)  # action-buffer parity and refill alignment
+        ply_base.fill_(k_base)
+        run(mode, 0, W, stream)
+        K, G = args.steps, args.graph_steps
+        graph, how = None, "eager"
+        if G > 0:
+            if G % (2 * R) or K % G:
+                raise SystemExit("--graph-steps must be a multiple of 32 that divides --steps")
+            try:
+                torch.cuda.synchronize(dev)
+                ply_base.fill_(k_base + W)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    run(mode, 0, G, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+                    ply_base.add_(G)
+                how = f"hipGraph replays of {G} steps"
+            except Exception as exc:  # capture unsupported: time eager launches instead
+                print(f"graph capture failed ({exc}); timing eager launches", file=sys.stderr)
+                graph, G = None, 0
+        per = 1 if mode == "step" else R
+        barrier(dev)
         torch.cuda.synchronize(dev)
-    nev = len(ev[0])
-    kern_ms = [ev[0][k].elapsed_time(ev[1][k]) for k in range(nev)]
-    kern_avg_s = sum(kern_ms) / nev / 1e3
+        t0 = time.perf_counter()
+        if graph is not None:
+            for _ in range(K // G):
+                graph.replay()
+            ev = None
+        else:
+            ev = ([torch.cuda.Event(enable_timing=True) for _ in range(K // per)],
+                  [torch.cuda.Event(enable_timing=True) for _ in range(K // per)])
+            ply_base.fill_(k_base + W)
+            run(mode, 0, K, stream, ev)
+        torch.cuda.synchronize(dev)
+        barrier(dev)
+        elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
+        if ev is None:
+            # ROCm rejects timing events as graph nodes ("External events are disallowed"), so the
+            # kernel duration comes from HIP events around each launch of an eager window of the
+            # same loop, run right after the timed replays on the same stream and state.
+            nwin = 64
+            ev = ([torch.cuda.Event(enable_timing=True) for _ in range(nwin // per)],
+                  [torch.cuda.Event(enable_timing=True) for _ in range(nwin // per)])
+            ply_base.fill_(k_base + W + K + 1)
+            run(mode, 0, nwin, stream, ev)
+            torch.cuda.synchronize(dev)
+        nev = len(ev[0])
+        launch_s = sum(ev[0][i].elapsed_time(ev[1][i]) for i in range(nev)) / nev / 1e3
+        return {"mode": mode, "elapsed": elapsed, "launch_s": launch_s, "steps_per_launch": per, "how": how,
+                "nev": nev, "k_next": k_base + W + K + 1 + 64 + 1}
+
+    main_rec = measure(args.mode, 0)
+    alt_rec = None
+    if args.also:
+        alt_rec = measure("rollout" if args.mode == "step" else "step", main_rec["k_next"])
+    K = args.steps
     # correctness canaries on the measured run: no error flags, episodes completed
     bad = int(((eng.flags & (_native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT)) != 0).sum().item())
     rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
     episodes = int(cnts.sum().item())
 
-    if rank == 0:
+    def summary(rec):
         total_steps = T * world * K
-        value = total_steps / elapsed_max
-        algo_bytes = ALGO_BYTES[P] * T
-        achieved = algo_bytes / kern_avg_s / 1e9
-        traffic, traffic_src = load_pmc_traffic(P, T)
+        algo = ALGO_BYTES[P] * T * rec["steps_per_launch"]
+        kname = f"spl::k_step<{P}>" if rec["mode"] == "step" else f"spl::k_rollout<{P}> ({R} steps per launch)"
+        return {"mode": rec["mode"], "value": round(total_steps / rec["elapsed"], 1),
+                "ms_per_step": round(rec["elapsed"] / K * 1e3, 4),
+                "roofline": {"bound": "hbm", "achieved": round(algo / rec["launch_s"] / 1e9, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(algo / rec["launch_s"] / 1e9 / HBM_PEAK_GBS, 4),
+                             "kernel": kname, "kernel_avg_us": round(rec["launch_s"] * 1e6, 2),
+                             "kernel_timing": ("HIP events around each launch in the timed region" if rec["how"] == "eager"
+                                               else f"HIP events around each of {rec['nev']} eager launches right "
+                                                    "after the timed replays"),
+                             "algo_bytes_per_launch": algo},
+                "launch": rec["how"]}
+
+    if rank == 0:
+        main = summary(main_rec)
+        traffic, traffic_src = load_pmc_traffic(P, T, main_rec["mode"], main_rec["steps_per_launch"])
+        roof = dict(main["roofline"], traffic=traffic, traffic_source=traffic_src)
         out = {
             "metric": f"env-steps/sec (whole node), {P}p {T} tables/GPU",
-            "value": round(value, 1),
+            "value": main["value"],
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed_max / K * 1e3, 4),
+            "ms_per_step": main["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -226,19 +266,15 @@ def main():
             "config": {"workload": f"{P}-player SplendorEnv.step x {T} tables per GPU, legal mask + uniform-random "
                                    "policy, same-step autoreset, obs int32[297] + mask int8[45] per table-step",
                        "tables_per_gpu": T, "players": P, "parallelism": f"table-sharded x{world}",
-                       "refill_every": REFILL_EVERY, "launch": mode},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": f"spl::k_step<{P}>", "kernel_avg_us": round(kern_avg_s * 1e6, 2),
-                         "kernel_timing": ("HIP events around each launch in the timed region" if mode == "eager" else
-                                           f"HIP events around each of {nev} eager launches right after the timed replays"),
-                         "algo_bytes_per_launch": algo_bytes},
+                       "refill_every": R, "mode": main["mode"], "launch": main["launch"]},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "episodes": episodes,
             "mean_final_reward_p0": round(float(rets.sum().item()) / max(1, episodes), 4),
             "error_flags": bad,
         }
+        if alt_rec is not None:
+            out["other_mode"] = summary(alt_rec)
         print(json.dumps(out))
     eng.close()
     if world > 1:

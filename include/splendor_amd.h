@@ -12,6 +12,8 @@
  *   spl_step           envs/splendor_env.py:51-90 SplendorEnv.step = rules.py:40-93 legal_moves,
  *                      :196-287 apply_action, encode.py:124-187 encode_observation, reward /
  *                      termination, plus gymnasium-0.29 SyncVectorEnv same-step autoreset
+ *   spl_rollout        K x spl_step under the device uniform-random policy in one launch
+ *                      (splendor_gym/scripts/random_rollout.py:15-26 loop, batched)
  *   spl_encode         engine/encode.py:124-187 encode_observation (current state)
  *   spl_legal          engine/rules.py:40-93 legal_moves (current state)
  *   spl_sample_uniform scripts/random_rollout.py:23 / wrappers/dual_step_native.py:215-223
@@ -117,6 +119,17 @@ int spl_reset(spl_ctx_t *ctx, spl_arena_t *arena, const uint64_t *pcg, const uin
               int32_t *obs, int8_t *mask, void *stream);
 
 int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *args, void *stream);
+
+/* `steps` consecutive SplendorEnv.step calls of every table under the device uniform-random
+ * policy (splendor_gym/scripts/random_rollout.py:15-26 batched): identical to `steps` spl_step calls in which
+ * next_actions of one call is the next call's actions and ply runs ply, ply+1, ...  args.actions
+ * holds the first step's actions; args.next_actions (nullable) receives the action sampled after
+ * the last step.  With per_step_outputs != 0, step k writes block k of every output array (obs
+ * [steps][n][297], mask [steps][n][45], reward/terminated/flags/winner [steps][n], final_obs
+ * [steps][n][297]; n divisible by 4); otherwise every step overwrites block 0.  A pool refill
+ * follows when the step counter crosses a multiple of the refill period (keep steps <= period). */
+int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *args, int32_t steps,
+                int32_t per_step_outputs, void *stream);
 
 /* Pool maintenance: deal the next episode of every table whose pool slot was consumed
  * (status bit ST_PENDING).  Tables it has not reached deal inline at their next reset. */

@@ -71,7 +71,7 @@ constexpr int kObsDim = 297;
 #endif
 constexpr int ABL_LEGAL_PRE = 1, ABL_APPLY = 2, ABL_LEGAL_POST = 4, ABL_FINAL = 8, ABL_RESET = 16, ABL_ENCODE = 32,
               ABL_STORE = 64, ABL_MASK_STORE = 128, ABL_SMALL_OUT = 256, ABL_TAB_STORE = 512, ABL_OBS_STORE = 1024,
-              ABL_LOAD = 2048;
+              ABL_LOAD = 2048, ABL_TOKLIM = 4096, ABL_NOBLE = 8192;
 __device__ __forceinline__ bool abl(int bit) { return (SPL_ABL & bit) != 0; }
 
 // Phase stamps for the diagnostic build only (-DSPL_STAMPS, tools/stamps.py): lane 0 of every
@@ -215,15 +215,38 @@ __device__ __forceinline__ uint4 card_rec(const BlockLDS &L, int id) { return L.
 
 __device__ __forceinline__ int card_cost(uint4 rec, int c) { return c < 4 ? (int)bget(rec.z, c) : (int)bget(rec.w, 0); }
 
-// engine/state.py:61-71 can_afford
-__device__ __forceinline__ bool afford(const Pl &p, uint4 rec) {
-    int need = 0;
-#pragma unroll
-    for (int c = 0; c < 5; ++c) {
-        const int d = max(card_cost(rec, c) - p.bon[c], 0);
-        need += max(d - p.tok[c], 0);
-    }
-    return p.tok[5] >= need;
+// Packed 16-bit arithmetic for per-colour comparisons: two colours per dword, saturating
+// subtraction in one v_pk_sub_u16 (clamp).  Byte fields are widened with one v_perm_b32.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t sat_sub16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, a),
+                                                                      __builtin_bit_cast(u16x2, b)));
+}
+// bytes i and j of w as the low and high 16-bit halves
+__device__ __forceinline__ uint32_t widen2(uint32_t w, int i, int j) {
+    return __builtin_amdgcn_perm(0u, w, 0x0C000C00u | ((uint32_t)j << 16) | (uint32_t)i);
+}
+
+// what the player can put toward each colour: tokens + bonuses, packed (w|b, g|r, k) + gold
+struct Have {
+    uint32_t wb, gr, k;
+    int gold;
+};
+__device__ __forceinline__ Have have_of(const Pl &p) {
+    Have h;
+    h.wb = (uint32_t)(p.tok[0] + p.bon[0]) | ((uint32_t)(p.tok[1] + p.bon[1]) << 16);
+    h.gr = (uint32_t)(p.tok[2] + p.bon[2]) | ((uint32_t)(p.tok[3] + p.bon[3]) << 16);
+    h.k = (uint32_t)(p.tok[4] + p.bon[4]);
+    h.gold = p.tok[5];
+    return h;
+}
+
+// engine/state.py:61-71 can_afford: sum over colours of max(cost - bonus - tokens, 0) <= gold
+// (max(max(cost - bonus, 0) - tokens, 0) == max(cost - bonus - tokens, 0) for tokens >= 0)
+__device__ __forceinline__ bool afford(const Have &h, uint4 rec) {
+    const uint32_t s = sat_sub16(widen2(rec.z, 0, 1), h.wb) + sat_sub16(widen2(rec.z, 2, 3), h.gr);
+    const int need = (int)(s & 0xFFFFu) + (int)(s >> 16) + max((int)bget(rec.w, 0) - (int)h.k, 0);
+    return h.gold >= need;
 }
 
 // take-3 colour sets in itertools.combinations(range(5), 3) order (engine/encode.py:35)
@@ -248,18 +271,19 @@ __device__ __forceinline__ uint64_t legal_mask(const uint32_t *sw, const Pl &p, 
 #pragma unroll
     for (int c = 0; c < 5; ++c) m |= (uint64_t)(bank[c] >= 4) << (10 + c);  // :61-63
     const bool can_res = p.nres < 3;
+    const Have h = have_of(p);
 #pragma unroll
     for (int k = 0; k < 12; ++k) {  // :66-80
         const int id = (int)bget(sw[SW_BOARD + k / 4], k % 4);
         const bool present = id != 0xFF;
-        m |= (uint64_t)(present && afford(p, card_rec(L, id))) << (15 + k);
+        m |= (uint64_t)(present && afford(h, card_rec(L, id))) << (15 + k);
         m |= (uint64_t)(present && can_res) << (27 + k);
     }
 #pragma unroll
     for (int t = 0; t < 3; ++t) m |= (uint64_t)(can_res && bget(sw[SW_DECK], t) > 0) << (39 + t);  // :83-86
 #pragma unroll
     for (int i = 0; i < 3; ++i)  // :89-91
-        m |= (uint64_t)(i < p.nres && afford(p, card_rec(L, p.res[i]))) << (42 + i);
+        m |= (uint64_t)(i < p.nres && afford(h, card_rec(L, p.res[i]))) << (42 + i);
     return m;
 }
 
@@ -281,13 +305,13 @@ __device__ __forceinline__ bool action_legal(const uint32_t *sw, const Pl &p, co
     }
     if (a < 27) {
         const int id = board_get(sw, a - 15);
-        return id != 0xFF && afford(p, card_rec(L, id));
+        return id != 0xFF && afford(have_of(p), card_rec(L, id));
     }
     if (a < 39) return p.nres < 3 && board_get(sw, a - 27) != 0xFF;
     if (a < 42) return p.nres < 3 && bget(sw[SW_DECK], a - 39) > 0;
     const int i = a - 42;
     const int r0 = opaque(p.res[0]), r1 = opaque(p.res[1]), r2 = opaque(p.res[2]);
-    return i < p.nres && afford(p, card_rec(L, i == 0 ? r0 : (i == 1 ? r1 : r2)));
+    return i < p.nres && afford(have_of(p), card_rec(L, i == 0 ? r0 : (i == 1 ? r1 : r2)));
 }
 
 // ... and whether ANY move is legal: with a non-gold colour in the bank some take-3 always is
@@ -423,6 +447,60 @@ __device__ __forceinline__ int predict_lut_key(const Pl &p, const int bank[6], i
     return total + delta > 10 ? lut_key(turn_count, to_play, total + delta, bank_total - delta) : -1;
 }
 
+// engine/rules.py:150-185 auto_return_tokens on the table entry `e` (top 3 bits of the first
+// 40 outputs of the seeded stream, 10 per word).  One draw per iteration for every lane still
+// returning: rng.choice -> _randbelow(n) takes the top bit_length(n) bits of one output and
+// rejects r >= n; an accepted r returns one token of the r-th held non-gold colour.  The loop
+// exit is wave-uniform and the body predicated, so divergent rejection counts cost no nested
+// control flow.  Returns false if the lane needs more than the table's 40 outputs.
+__device__ __forceinline__ bool token_return_lut(Pl &p, int bank[6], int remaining, uint4 e) {
+    // the five non-gold counts as bytes of one 64-bit word each (player, bank)
+    uint64_t tk = 0, bk = 0;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        tk |= (uint64_t)(uint32_t)p.tok[c] << (8 * c);
+        bk |= (uint64_t)(uint32_t)bank[c] << (8 * c);
+    }
+    uint32_t held = 0;  // non-gold colours the player holds
+#pragma unroll
+    for (int c = 0; c < 5; ++c) held |= (p.tok[c] > 0 ? 1u : 0u) << c;
+    int pos = 0;
+    bool active = remaining > 0 && held != 0u;
+    for (;;) {
+        active = active && pos < kLutOutputs;
+        if (!__any(active)) break;
+        const int nch = __popc(held);
+        const int kb = nch >= 4 ? 3 : (nch >= 2 ? 2 : 1);
+        const int q = (pos >= 10 ? 1 : 0) + (pos >= 20 ? 1 : 0) + (pos >= 30 ? 1 : 0);
+        const uint32_t w = q == 0 ? e.x : (q == 1 ? e.y : (q == 2 ? e.z : e.w));
+        const int r = (int)(__builtin_amdgcn_ubfe(w, 3u * (uint32_t)(pos - 10 * q), 3u) >> (3 - kb));
+        ++pos;
+        const bool acc = active && r < nch;
+        uint32_t h = held;  // drop the r lowest held colours: the r-th is the lowest left
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h = i < r ? (h & (h - 1u)) : h;
+        const uint32_t c8 = 8u * (uint32_t)__builtin_ctz(h | 0x20u);
+        const uint64_t one = acc ? (1ull << c8) : 0ull;
+        tk -= one;
+        bk += one;
+        held &= (acc && ((tk >> c8) & 0xFFull) == 0ull) ? ~(1u << (c8 >> 3)) : 0xFFFFFFFFu;
+        remaining -= acc ? 1 : 0;
+        active = active && remaining > 0 && held != 0u;
+    }
+    if (remaining > 0 && held != 0u) return false;  // table outputs exhausted
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+        p.tok[c] = (int)((tk >> (8 * c)) & 0xFFull);
+        bank[c] = (int)((bk >> (8 * c)) & 0xFFull);
+    }
+    if (remaining > 0 && p.tok[5] > 0) {              // :179-184 then gold
+        const int give = min(remaining, p.tok[5]);
+        p.tok[5] -= give;
+        bank[5] += give;
+    }
+    return true;
+}
+
 // engine/rules.py:188-193 _enforce_token_limit -> :150-185 auto_return_tokens.  `pre_key` /
 // `pre_e` are the prefetched table entry (predict_lut_key); any other key is loaded here.
 __device__ __forceinline__ void enforce_token_limit(Pl &p, int bank[6], int turn_count, int to_play,
@@ -442,30 +520,7 @@ __device__ __forceinline__ void enforce_token_limit(Pl &p, int bank[6], int turn
         int bank2[6];
 #pragma unroll
         for (int c = 0; c < 6; ++c) bank2[c] = bank[c];
-        int remaining = total - 10, pos = 0, word = 0, sub = 0;
-        bool ok = true;
-        while (remaining > 0) {
-            const int nch = non_gold_kinds(p2);
-            if (nch == 0) break;
-            const int kb = nch >= 4 ? 3 : (nch >= 2 ? 2 : 1);
-            int r = nch;
-            while (r >= nch) {
-                if (pos >= kLutOutputs) { ok = false; break; }
-                const uint32_t w = word == 0 ? e.x : (word == 1 ? e.y : (word == 2 ? e.z : e.w));
-                r = (int)(((w >> (3 * sub)) & 7u) >> (3 - kb));
-                ++pos;
-                if (++sub == 10) { sub = 0; ++word; }
-            }
-            if (!ok) break;
-            return_one(p2, bank2, r);
-            remaining -= 1;
-        }
-        if (ok) {
-            if (remaining > 0 && p2.tok[5] > 0) {
-                const int give = min(remaining, p2.tok[5]);
-                p2.tok[5] -= give;
-                bank2[5] += give;
-            }
+        if (token_return_lut(p2, bank2, total - 10, e)) {
             p = p2;
 #pragma unroll
             for (int c = 0; c < 6; ++c) bank[c] = bank2[c];
@@ -485,14 +540,18 @@ __device__ __forceinline__ void grant_noble(uint32_t *sw, Pl &p, int to_play, co
     const int nn = (int)bget(sw[SW_DECK], 3);
     uint32_t owners = (sw[SW_NOB1] >> 8) & 0x7FFFu;
     bool granted = false;
+    const uint32_t bon_wb = (uint32_t)p.bon[0] | ((uint32_t)p.bon[1] << 16);
+    const uint32_t bon_gr = (uint32_t)p.bon[2] | ((uint32_t)p.bon[3] << 16);
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
         const int idx = s < 4 ? (int)bget(sw[SW_NOB0], s) : (int)bget(sw[SW_NOB1], 0);
         const bool visible = s < nn && ((owners >> (3 * s)) & 7u) == 0 && idx < 10;
         const uint2 rec = L.nobles[idx < 10 ? idx : 0];
-        const bool meets = p.bon[0] >= (int)bget(rec.x, 1) && p.bon[1] >= (int)bget(rec.x, 2) &&
-                           p.bon[2] >= (int)bget(rec.x, 3) && p.bon[3] >= (int)bget(rec.y, 0) &&
-                           p.bon[4] >= (int)bget(rec.y, 1);
+        // requirement minus bonus, saturated, is zero in every colour
+        const uint32_t req_wb = widen2(rec.x, 1, 2);
+        const uint32_t req_gr = __builtin_amdgcn_perm(rec.y, rec.x, 0x0C040C03u);  // x.byte3 | y.byte0
+        const bool meets = (sat_sub16(req_wb, bon_wb) | sat_sub16(req_gr, bon_gr)) == 0u &&
+                           (int)bget(rec.y, 1) <= p.bon[4];
         const bool take = !granted && visible && meets;
         owners |= take ? ((uint32_t)(to_play + 1) << (3 * s)) : 0u;
         p.pres += take ? (int)bget(rec.y, 2) : 0;
@@ -595,8 +654,8 @@ __device__ __forceinline__ void apply_action(Tab<P> &T, int a, uint32_t top, con
         p.nres -= 1;
         pay_for_card(p, bank, card_rec(L, card));
     }
-    grant_noble(sw, p, tp, L);                                              // :260
-    enforce_token_limit(p, bank, get_turn(sw), tp, lut, pre_key, pre_e, flags);  // :261
+    if (!abl(ABL_NOBLE)) grant_noble(sw, p, tp, L);                         // :260
+    if (!abl(ABL_TOKLIM)) enforce_token_limit(p, bank, get_turn(sw), tp, lut, pre_key, pre_e, flags);  // :261
     uint32_t misc = sw[SW_MISC];
     if (p.pres >= 15) misc |= ST_GAME_OVER;                                 // :264-265
     pack_pl(p, w);
@@ -976,6 +1035,129 @@ __global__ __launch_bounds__(64) void k_build_lut(uint4 *lut) {
     lut[e] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// ---- one env step of one table, shared by k_step and k_rollout ----------------------------
+
+// Loads a step needs beyond the table state, issued as early as the action is known: the deck
+// card the action pops and the token-return table entry it consults (predict_lut_key).
+struct StepPre {
+    uint32_t top;
+    int key;
+    uint4 e;
+};
+
+template <int P>
+__device__ __forceinline__ StepPre step_prefetch(const Tab<P> &T, int action, bool valid, const KArena &A, int t,
+                                                 const KTables &Tb) {
+    StepPre pre{0xFFu, -1, make_uint4(0u, 0u, 0u, 0u)};
+    const bool live_tab = valid && !is_terminal(T.sw);
+    const int ptier = pop_tier(action);
+    if (live_tab && ptier >= 0) {
+        const int len = (int)bget(T.sw[SW_DECK], ptier);
+        const uint8_t *live = slot_rec(A, t, (T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0);
+        if (len > 0) pre.top = live[tier_base(ptier) + len - 1];
+    }
+    if (live_tab && action >= 0 && action < SPL_NUM_ACTIONS) {
+        const int tp = get_to_play(T.sw);
+        uint32_t pw4[4];
+        get_player(T, tp, pw4);
+        int bank[6];
+        get_bank(T.sw, bank);
+        pre.key = predict_lut_key(unpack_pl(pw4), bank, action, get_turn(T.sw), tp);
+        if (pre.key >= 0) pre.e = Tb.lut[pre.key];
+    }
+    return pre;
+}
+
+struct StepOut {
+    uint32_t flags;
+    float reward;
+    bool term;
+    uint64_t mask;  // info["action_mask"] after the step (before any autoreset)
+};
+
+// envs/splendor_env.py:51-90 on the table in registers.
+template <int P>
+__device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepPre &pre, bool valid, const BlockLDS &L,
+                                              const KTables &Tb) {
+    StepOut o{0u, 0.0f, false, 0ull};
+    bool want_mask = false;
+    if (valid) {
+        if (is_terminal(T.sw)) {                                  // :53-54 RuntimeError
+            o.flags = SPL_F_AFTER_TERMINAL;
+        } else {
+            const bool in_range = action >= 0 && action < SPL_NUM_ACTIONS;
+            uint32_t pw4[4];
+            get_player(T, get_to_play(T.sw), pw4);
+            const Pl cur = unpack_pl(pw4);
+            int bank[6];
+            get_bank(T.sw, bank);
+            // :55 mask = legal_moves(state): only "any legal?" and mask[action] are needed here
+            const bool anyl = abl(ABL_LEGAL_PRE) || any_legal(T.sw, cur, bank, L);
+            const bool ok = abl(ABL_LEGAL_PRE) || (in_range && action_legal(T.sw, cur, bank, action, L));
+            if (!anyl) {                                          // :56-61 no legal move: draw
+                T.sw[SW_MISC] = (T.sw[SW_MISC] | ST_GAME_OVER) & 0x00FFFFFFu;
+                T.sw[SW_BANK1] &= 0xFF00FFFFu;                    // to_play = 0
+                o.term = true;
+                o.flags = SPL_F_DRAW;
+            } else if (!in_range) {                               // :62-63 ValueError, mask of the unchanged state
+                o.flags = SPL_F_OOB;
+                want_mask = true;
+            } else if (!ok) {                                     // :64-66 illegal, mask of the unchanged state
+                o.flags = SPL_F_ILLEGAL;
+                o.reward = -0.01f;
+                want_mask = true;
+            } else {
+                STAMP(2);
+                if (!abl(ABL_APPLY)) apply_action(T, action, pre.top, L, Tb.lut, pre.key, pre.e, o.flags);  // :68
+                STAMP(3);
+                o.term = is_terminal(T.sw);                       // :70
+                if (o.term) {                                     // :71-80
+                    const int w = get_winner(T.sw);
+                    const bool tl = (T.sw[SW_MISC] & ST_TURN_LIMIT) != 0;
+                    o.reward = (w < 0 && tl) ? -0.1f : (w < 0 ? 0.0f : (w == P - 1 ? 1.0f : -1.0f));
+                    o.flags |= tl ? SPL_F_TURN_LIMIT : 0u;        // :82-83
+                } else {
+                    want_mask = true;                             // :81
+                }
+            }
+        }
+    }
+    // one legal_moves evaluation per lane (a single call site keeps one copy in the code)
+    if (want_mask) o.mask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);
+    return o;
+}
+
+// player 0's final reward of a finished episode (envs/splendor_env.py:92-115)
+template <int P>
+__device__ __forceinline__ float final_reward_p0(const Tab<P> &T) {
+    const int w = get_winner(T.sw);
+    const bool tl = (T.sw[SW_MISC] & ST_TURN_LIMIT) != 0;
+    return w < 0 ? (tl ? -0.1f : 0.0f) : (w == 0 ? 1.0f : -1.0f);
+}
+
+// same-step autoreset (envs/splendor_env.py:43-44: the pool deal continues the np_random
+// stream); the pool is consumed, so a second reset before the next refill deals inline
+template <int P>
+__device__ __forceinline__ void autoreset_table(Tab<P> &T, const KArena &A, int t, Deal &pool, uint8_t *scr,
+                                                StepOut &o) {
+    const int nxt = ((T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0) ^ 1;
+    if (T.sw[SW_MISC] & ST_PENDING)  // pool not refilled yet: deal inline (correct, slower)
+        o.flags |= deal_next<P>(A, t, nxt, scr, pool);
+    fresh_state(T, (nxt ? ST_ACTIVE : 0u) | ST_PENDING, pool);
+    o.flags |= SPL_F_RESET;
+    o.mask = kFreshDealMask;
+}
+
+// Terminal rows staged in L.frows (bits of `fin`) -> final_obs rows of this wave.
+__device__ __forceinline__ void store_final_rows(const BlockLDS &L, uint64_t fin, int32_t *final_obs, int t0) {
+    while (fin) {
+        const int r = __ffsll((unsigned long long)fin) - 1;
+        fin &= fin - 1;
+        int32_t *dst = final_obs + (size_t)(t0 + r) * kObsDim;
+        for (int e = lane_id(); e < kObsDim; e += 64) dst[e] = (int32_t)L.frows[r * kObsDim + e];
+    }
+}
+
 // SplendorEnv.step for every table (envs/splendor_env.py:51-90) + same-step autoreset.
 //
 // Every global load of the step (state, action, pool deal words, the deck card the action
@@ -1004,129 +1186,47 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     } else {
         fresh_state(T, 0u, empty_deal());
     }
-    const bool live_tab = valid && !is_terminal(T.sw);
-    const bool in_range = action >= 0 && action < SPL_NUM_ACTIONS;
-    const int tp = get_to_play(T.sw);
-    uint32_t pw4[4];
-    get_player(T, tp, pw4);
-    const Pl cur = unpack_pl(pw4);
-    int bank[6];
-    get_bank(T.sw, bank);
-    // dependent prefetches: the card this action pops, the table entry it consults
-    const int ptier = pop_tier(action);
-    uint32_t top = 0xFFu;
-    if (live_tab && ptier >= 0) {
-        const int len = (int)bget(T.sw[SW_DECK], ptier);
-        const uint8_t *live = slot_rec(A, t, (T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0);
-        if (len > 0) top = live[tier_base(ptier) + len - 1];
-    }
-    int pre_key = -1;
-    uint4 pre_e = make_uint4(0u, 0u, 0u, 0u);
-    if (live_tab && in_range) {
-        pre_key = predict_lut_key(cur, bank, action, get_turn(T.sw), tp);
-        if (pre_key >= 0) pre_e = Tb.lut[pre_key];
-    }
+    const StepPre pre = step_prefetch(T, action, valid, A, t, Tb);
     wave_lds_sync();
     STAMP(1);
 
-    uint32_t flags = 0;
-    float reward = 0.0f;
-    bool term = false;
-    bool want_mask = false;  // info["action_mask"] of the table's state after this step
-    if (valid) {
-        if (!live_tab) {                                          // :53-54 RuntimeError
-            flags = SPL_F_AFTER_TERMINAL;
-        } else {
-            // :55 mask = legal_moves(state): only "any legal?" and mask[action] are needed here
-            const bool anyl = abl(ABL_LEGAL_PRE) || any_legal(T.sw, cur, bank, L);
-            const bool ok = abl(ABL_LEGAL_PRE) || (in_range && action_legal(T.sw, cur, bank, action, L));
-            if (!anyl) {                                          // :56-61 no legal move: draw
-                T.sw[SW_MISC] = (T.sw[SW_MISC] | ST_GAME_OVER) & 0x00FFFFFFu;
-                T.sw[SW_BANK1] &= 0xFF00FFFFu;                    // to_play = 0
-                term = true;
-                flags = SPL_F_DRAW;
-            } else if (!in_range) {                               // :62-63 ValueError, mask of the unchanged state
-                flags = SPL_F_OOB;
-                want_mask = true;
-            } else if (!ok) {                                     // :64-66 illegal, mask of the unchanged state
-                flags = SPL_F_ILLEGAL;
-                reward = -0.01f;
-                want_mask = true;
-            } else {
-                STAMP(2);
-                if (!abl(ABL_APPLY)) apply_action(T, action, top, L, Tb.lut, pre_key, pre_e, flags);  // :68
-                STAMP(3);
-                term = is_terminal(T.sw);                         // :70
-                if (term) {                                       // :71-80
-                    const int w = get_winner(T.sw);
-                    const bool tl = (T.sw[SW_MISC] & ST_TURN_LIMIT) != 0;
-                    reward = (w < 0 && tl) ? -0.1f : (w < 0 ? 0.0f : (w == P - 1 ? 1.0f : -1.0f));
-                    flags |= tl ? SPL_F_TURN_LIMIT : 0u;          // :82-83
-                } else {
-                    want_mask = true;                             // :81
-                }
-            }
-        }
-    }
-    // one legal_moves evaluation per lane (a single call site keeps one copy in the code)
-    uint64_t outmask = 0;
-    if (want_mask) outmask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);
+    StepOut o = step_rules(T, action, pre, valid, L, Tb);
     const int8_t wnr = (int8_t)get_winner(T.sw);
     STAMP(4);
 
     // terminal observation for gymnasium's info["final_observation"], staged in LDS and stored
     // with everything else at the end
     const bool want_final = S.autoreset && S.final_obs != nullptr && !abl(ABL_FINAL);
-    const uint64_t fin = __ballot(valid && term && want_final);
-    if (valid && term && want_final) encode_row(T, &L.frows[lane * kObsDim], L);
+    const uint64_t fin = __ballot(valid && o.term && want_final);
+    if (valid && o.term && want_final) encode_row(T, &L.frows[lane * kObsDim], L);
     const int fin_moves = get_moves(T.sw);
-    float ep_add = 0.0f;  // player 0's final reward (envs/splendor_env.py:92-115)
-    if (valid && term) {
-        const int w = get_winner(T.sw);
-        const bool tl = (T.sw[SW_MISC] & ST_TURN_LIMIT) != 0;
-        ep_add = w < 0 ? (tl ? -0.1f : 0.0f) : (w == 0 ? 1.0f : -1.0f);
-    }
+    const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;
     STAMP(5);
-    const bool do_reset = valid && term && S.autoreset && !abl(ABL_RESET);
-    if (do_reset) {  // envs/splendor_env.py:43-44: the pool deal continues the np_random stream
-        const int nxt = ((T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0) ^ 1;
-        if (T.sw[SW_MISC] & ST_PENDING)  // pool not refilled yet: deal inline (correct, slower)
-            flags |= deal_next<P>(A, t, nxt, &L.rows[lane * kScratchStride], pool);
-        fresh_state(T, (nxt ? ST_ACTIVE : 0u) | ST_PENDING, pool);
-        flags |= SPL_F_RESET;
-        outmask = kFreshDealMask;
-    }
+    if (valid && o.term && S.autoreset && !abl(ABL_RESET)) autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], o);
     STAMP(6);
     wave_lds_sync();  // deal scratch (rows) free again
 
     // observation + mask of the current state, block stores
     if (!abl(ABL_ENCODE)) encode_row(T, &L.rows[lane * kObsDim], L);
-    L.mask[lane] = outmask;
+    L.mask[lane] = o.mask;
     STAMP(7);
     wave_lds_sync();
     STAMP(8);
-    int32_t *obs_dst = S.obs + (size_t)t0 * kObsDim;
     if (!abl(ABL_STORE)) {
-        if (!abl(ABL_OBS_STORE)) store_obs_block(L, rows, obs_dst);
+        if (!abl(ABL_OBS_STORE)) store_obs_block(L, rows, S.obs + (size_t)t0 * kObsDim);
         STAMP(9);
         if (!abl(ABL_MASK_STORE)) store_mask_block(L, rows, S.mask + (size_t)t0 * 45);
     }
-    uint64_t b = fin;  // terminal rows of this wave (about one per wave per step)
-    while (b) {
-        const int r = __ffsll((unsigned long long)b) - 1;
-        b &= b - 1;
-        int32_t *dst = S.final_obs + (size_t)(t0 + r) * kObsDim;
-        for (int e = lane; e < kObsDim; e += 64) dst[e] = (int32_t)L.frows[r * kObsDim + e];
-    }
+    store_final_rows(L, fin, S.final_obs, t0);
     STAMP(10);
-    if (valid && term) {  // no-return atomics: nothing to wait for
+    if (valid && o.term) {  // no-return atomics: nothing to wait for
         if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_add);
         if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
     }
     // move_count above 255 (crafted states only) does not fit the byte staging: patch it after
     // this wave's block stores of the same dwords have left
     const bool patch = valid && get_moves(T.sw) > 255;
-    const bool fpatch = valid && term && want_final && fin_moves > 255;
+    const bool fpatch = valid && o.term && want_final && fin_moves > 255;
     if (__any(patch || fpatch)) {
         __builtin_amdgcn_s_waitcnt(0);
         if (patch) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
@@ -1134,18 +1234,93 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     }
     if (valid) {
         if (!abl(ABL_SMALL_OUT)) {
-            S.reward[t] = reward;
-            S.terminated[t] = term ? 1 : 0;
-            S.flags[t] = (uint8_t)flags;
+            S.reward[t] = o.reward;
+            S.terminated[t] = o.term ? 1 : 0;
+            S.flags[t] = (uint8_t)o.flags;
             if (S.winner) S.winner[t] = wnr;
         }
         if (S.next_actions) {
             const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
-            S.next_actions[t] = sample_uniform(outmask, S.policy_seed, (uint64_t)(S.table0 + t), ply);
+            S.next_actions[t] = sample_uniform(o.mask, S.policy_seed, (uint64_t)(S.table0 + t), ply);
         }
         if (!abl(ABL_TAB_STORE)) store_tab(T, A, t);
     }
     STAMP(11);
+}
+
+// K consecutive env steps of every table with the device uniform-random policy: exactly K
+// k_step launches with next_actions fed back as the next launch's actions (plies ply ..
+// ply+K-1), without the launch boundaries.  The table state stays in registers; each step's
+// block stores are issued and left to drain while the wave computes the next step, and the
+// next step's deck-card / token-table gathers are issued a whole step ahead.  Step k's outputs
+// go to block k of each output array when `per_step` (rollout storage [K][n][...]), else every
+// step overwrites block 0.
+template <int P>
+__global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, int K, int per_step) {
+    __shared__ BlockLDS L;
+    const int lane = lane_id();
+    const int t0 = blockIdx.x * 64;
+    const int t = t0 + lane;
+    const bool valid = t < A.n;
+    const int rows = min(64, A.n - t0);
+    load_tables_lds(L, Tb);
+
+    Tab<P> T;
+    int action = 0;
+    Deal pool = empty_deal();
+    if (valid) {
+        load_tab(T, A, t);
+        action = S.actions[t];
+        if (S.autoreset) pool = load_pool(A, t);
+    } else {
+        fresh_state(T, 0u, empty_deal());
+    }
+    StepPre pre = step_prefetch(T, action, valid, A, t, Tb);
+    const uint64_t ply0 = S.ply + (S.ply_base ? *S.ply_base : 0ull);
+    const bool want_final = S.autoreset && S.final_obs != nullptr;
+    for (int k = 0; k < K; ++k) {
+        const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
+        wave_lds_sync();  // previous step's LDS reads done (rows, mask, frows)
+        StepOut o = step_rules(T, action, pre, valid, L, Tb);
+        const int8_t wnr = (int8_t)get_winner(T.sw);
+        const uint64_t fin = __ballot(valid && o.term && want_final);
+        if (valid && o.term && want_final) encode_row(T, &L.frows[lane * kObsDim], L);
+        const int fin_moves = get_moves(T.sw);
+        if (valid && o.term) {  // per termination, as k_step (same float rounding)
+            if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], final_reward_p0(T));
+            if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
+        }
+        if (valid && o.term && S.autoreset) autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], o);
+        wave_lds_sync();
+        encode_row(T, &L.rows[lane * kObsDim], L);
+        L.mask[lane] = o.mask;
+        wave_lds_sync();
+        // the policy's next action and its prefetches go out before this step's stores
+        action = sample_uniform(o.mask, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
+        if (k + 1 < K) pre = step_prefetch(T, action, valid, A, t, Tb);
+        int32_t *obs = S.obs + blk * kObsDim;
+        store_obs_block(L, rows, obs + (size_t)t0 * kObsDim);
+        store_mask_block(L, rows, S.mask + blk * 45 + (size_t)t0 * 45);
+        int32_t *fobs = want_final ? S.final_obs + blk * kObsDim : nullptr;
+        if (want_final) store_final_rows(L, fin, fobs, t0);
+        const bool patch = valid && get_moves(T.sw) > 255;
+        const bool fpatch = valid && o.term && want_final && fin_moves > 255;
+        if (__any(patch || fpatch)) {  // crafted states only (see k_step)
+            __builtin_amdgcn_s_waitcnt(0);
+            if (patch) obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
+            if (fpatch) fobs[(size_t)t * kObsDim + 295] = fin_moves;
+        }
+        if (valid) {
+            S.reward[blk + t] = o.reward;
+            S.terminated[blk + t] = o.term ? 1 : 0;
+            S.flags[blk + t] = (uint8_t)o.flags;
+            if (S.winner) S.winner[blk + t] = wnr;
+        }
+    }
+    if (valid) {
+        if (S.next_actions) S.next_actions[t] = action;
+        store_tab(T, A, t);
+    }
 }
 
 // Explicit reset (SplendorEnv.reset / VectorEnv.reset), then observation + mask of all tables.
@@ -1585,13 +1760,16 @@ int spl_refill(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
     return SPL_OK;
 }
 
-int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void *stream) {
-    if (int r = check_arena(ctx, arena)) return r;
+static int check_step_args(const spl_step_args_t *a) {
     if (!a || !a->actions || !a->obs || !a->mask || !a->reward || !a->terminated || !a->flags)
-        return fail(SPL_E_ARG, "spl_step: actions/obs/mask/reward/terminated/flags are required");
+        return fail(SPL_E_ARG, "actions/obs/mask/reward/terminated/flags are required");
     if (((uintptr_t)a->obs & 15u) || (a->final_obs && ((uintptr_t)a->final_obs & 3u)))
         return fail(SPL_E_ARG, "obs must be 16-byte aligned");
     if ((uintptr_t)a->mask & 3u) return fail(SPL_E_ARG, "mask must be 4-byte aligned");
+    return SPL_OK;
+}
+
+static KStep kstep(const spl_step_args_t *a) {
     KStep S;
     S.actions = a->actions;
     S.obs = a->obs;
@@ -1609,6 +1787,13 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     S.ply = a->ply;
     S.table0 = a->table0;
     S.autoreset = a->autoreset;
+    return S;
+}
+
+int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    if (int r = check_step_args(a)) return r;
+    const KStep S = kstep(a);
     const KArena A = karena(arena);
     hipStream_t s = static_cast<hipStream_t>(stream);
     DISPATCH_P(arena->players,
@@ -1616,6 +1801,26 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     if (int r = launch_check()) return r;
     arena->steps += 1;
     if (a->autoreset && ctx->refill_period > 0 && arena->steps % ctx->refill_period == 0)
+        return spl_refill(ctx, arena, stream);
+    return SPL_OK;
+}
+
+int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, int32_t steps, int32_t per_step_outputs,
+                void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    if (int r = check_step_args(a)) return r;
+    if (steps < 1) return fail(SPL_E_ARG, "spl_rollout: steps must be >= 1");
+    if (per_step_outputs && (arena->n & 3))
+        return fail(SPL_E_ARG, "spl_rollout: per-step outputs need a table count divisible by 4 (16-byte obs blocks)");
+    const KStep S = kstep(a);
+    const KArena A = karena(arena);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_rollout<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
+                                                  ktables(ctx), S, (int)steps, (int)(per_step_outputs != 0)));
+    if (int r = launch_check()) return r;
+    const int64_t before = arena->steps;
+    arena->steps += steps;
+    if (a->autoreset && ctx->refill_period > 0 && arena->steps / ctx->refill_period != before / ctx->refill_period)
         return spl_refill(ctx, arena, stream);
     return SPL_OK;
 }

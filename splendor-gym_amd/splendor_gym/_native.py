@@ -60,6 +60,8 @@ SIGNATURES = {
     "spl_reset": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
                   c_int32),
     "spl_step": ([c_void_p, ctypes.POINTER(ArenaDesc), ctypes.POINTER(StepArgs), c_void_p], c_int32),
+    "spl_rollout": ([c_void_p, ctypes.POINTER(ArenaDesc), ctypes.POINTER(StepArgs), c_int32, c_int32, c_void_p],
+                    c_int32),
     "spl_refill": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p], c_int32),
     "spl_encode": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p, c_void_p], c_int32),
     "spl_legal": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p, c_void_p], c_int32),

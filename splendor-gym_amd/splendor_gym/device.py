@@ -130,6 +130,42 @@ class Engine:
         self._keep_actions = actions
         return self.obs, self.mask, self.reward, self.terminated, self.flags
 
+    def rollout(self, steps, actions=None, next_actions=None, policy_seed=0, ply=0, out=None, final_obs=True,
+                ep_return=None, ep_count=None, ply_base=None):
+        """`steps` env steps of every table under the device uniform-random policy in one launch
+        (spl_rollout): the same trajectory as `steps` calls of step() with next_actions fed back
+        and ply, ply+1, ...  out=None overwrites self.obs/mask/... each step; otherwise `out` is a
+        dict of [steps, n, ...] tensors (obs, mask, reward, terminated, flags, winner, final_obs)
+        that receives every step's outputs (rollout storage)."""
+        torch = self.torch
+        actions = self.actions if actions is None else actions
+        if not (isinstance(actions, torch.Tensor) and actions.device == self.device and actions.dtype == torch.int32
+                and actions.is_contiguous() and actions.numel() == self.n):
+            raise ValueError("actions must be a contiguous int32 device tensor with one entry per table")
+        if out is None:
+            bufs, per_step = dict(obs=self.obs, mask=self.mask, reward=self.reward, terminated=self.terminated,
+                                  flags=self.flags, winner=self.winner, final_obs=self.final_obs), 0
+        else:
+            bufs, per_step = out, 1
+            for k, shape in (("obs", (steps, self.n, OBS_DIM)), ("mask", (steps, self.n, NUM_ACTIONS)),
+                             ("reward", (steps, self.n)), ("terminated", (steps, self.n)), ("flags", (steps, self.n))):
+                if k not in bufs or tuple(bufs[k].shape) != shape or not bufs[k].is_contiguous():
+                    raise ValueError(f"out[{k!r}] must be a contiguous tensor of shape {shape}")
+        a = StepArgs(actions=actions.data_ptr(), obs=bufs["obs"].data_ptr(), mask=bufs["mask"].data_ptr(),
+                     reward=bufs["reward"].data_ptr(), terminated=bufs["terminated"].data_ptr(),
+                     flags=bufs["flags"].data_ptr(), winner=ptr(bufs.get("winner")),
+                     final_obs=ptr(bufs.get("final_obs")) if final_obs else None, autoreset=1,
+                     next_actions=None if next_actions is None else next_actions.data_ptr(),
+                     ply_base=None if ply_base is None else ply_base.data_ptr(),
+                     policy_seed=int(policy_seed) & (2**64 - 1), ply=int(ply) & (2**64 - 1), table0=self.table0,
+                     ep_return=None if ep_return is None else ep_return.data_ptr(),
+                     ep_count=None if ep_count is None else ep_count.data_ptr())
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_rollout(self.ctx, ctypes.byref(self.desc), ctypes.byref(a), int(steps),
+                                                 per_step, self.stream()))
+        self._keep_actions = (actions, bufs)
+        return bufs
+
     def refill(self):
         with self.torch.cuda.device(self.device):
             check(self.lib, self.lib.spl_refill(self.ctx, ctypes.byref(self.desc), self.stream()))

@@ -196,3 +196,61 @@ def test_unseeded_tables_deal_engine_seed_zero(orc):
     e.reset(seeds=None)    # pool consumed, not refilled: inline deal, same seed
     recs = e.download()
     assert canon(table_to_view(recs[5])) == want
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_rollout_equals_step_chain(P):
+    """spl_rollout(K) is K chained spl_step calls (next_actions fed back, plies ply..ply+K-1):
+    every per-step output, the terminal rows of final_obs, episode statistics, the next action
+    and the table state match bit for bit, across launches with refills in between."""
+    import torch
+    n, K, launches, seed = 1024, 16, 5, 11
+    chain, fused = engine(n, P, refill_period=K), engine(n, P, refill_period=K)
+    chain.reset(seeds=range(n))
+    fused.reset(seeds=range(n))
+    dev = chain.device
+    a_c = torch.zeros(n, dtype=torch.int32, device=dev)
+    chain.sample_uniform(out=a_c, seed=seed, ply=0)
+    a_f = a_c.clone()
+    stats = {k: (torch.zeros(n, dtype=torch.float32, device=dev), torch.zeros(n, dtype=torch.int32, device=dev))
+             for k in ("c", "f")}
+    for launch in range(launches):
+        ply0 = 1 + launch * K
+        want = []
+        for k in range(K):
+            na = torch.empty_like(a_c)
+            chain.step(a_c, next_actions=na, policy_seed=seed, ply=ply0 + k, ep_return=stats["c"][0],
+                       ep_count=stats["c"][1])
+            want.append({name: getattr(chain, name).clone() for name in
+                         ("obs", "mask", "reward", "terminated", "flags", "winner", "final_obs")})
+            a_c = na
+        out = {"obs": torch.empty((K, n, 297), dtype=torch.int32, device=dev),
+               "mask": torch.empty((K, n, 45), dtype=torch.int8, device=dev),
+               "reward": torch.empty((K, n), dtype=torch.float32, device=dev),
+               "terminated": torch.empty((K, n), dtype=torch.uint8, device=dev),
+               "flags": torch.empty((K, n), dtype=torch.uint8, device=dev),
+               "winner": torch.empty((K, n), dtype=torch.int8, device=dev),
+               "final_obs": torch.zeros((K, n, 297), dtype=torch.int32, device=dev)}
+        na = torch.empty_like(a_f)
+        fused.rollout(K, actions=a_f, next_actions=na, policy_seed=seed, ply=ply0, out=out,
+                      ep_return=stats["f"][0], ep_count=stats["f"][1])
+        a_f = na
+        for k in range(K):
+            for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
+                assert torch.equal(out[name][k], want[k][name]), (launch, k, name)
+            term = want[k]["terminated"].bool()
+            assert torch.equal(out["final_obs"][k][term], want[k]["final_obs"][term]), (launch, k)
+        assert torch.equal(a_f, a_c), launch
+        assert int(want[-1]["terminated"].sum()) >= 0
+    assert torch.equal(stats["c"][0], stats["f"][0]) and torch.equal(stats["c"][1], stats["f"][1])
+    assert int(stats["c"][1].sum()) > 0  # episodes finished and autoreset inside the rollouts
+    assert chain.download().tobytes() == fused.download().tobytes()
+    # overwrite mode: block 0 holds the last step's outputs
+    na_c, na_f = torch.empty_like(a_c), torch.empty_like(a_f)
+    for k in range(K):
+        chain.step(a_c, next_actions=na_c, policy_seed=seed, ply=1000 + k)
+        a_c, na_c = na_c, a_c
+    fused.rollout(K, actions=a_f, next_actions=na_f, policy_seed=seed, ply=1000)
+    for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
+        assert torch.equal(getattr(chain, name), getattr(fused, name)), name
+    assert torch.equal(a_c, na_f)

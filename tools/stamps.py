@@ -11,7 +11,7 @@ import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(REPO, "splendor-gym_amd", "ablate", "lib_stamps.so")
+LIB = os.environ.get("STAMP_LIB", os.path.join(REPO, "splendor-gym_amd", "ablate", "lib_stamps.so"))
 NAMES = ["start", "loaded+prefetched", "pre-apply", "applied", "step logic", "final obs", "reset done",
          "encoded", "barrier", "obs stored", "mask+final stored", "end"]
 
@@ -43,8 +43,9 @@ print(json.dumps(out))
 def main():
     if "--run" not in sys.argv:
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
+        extra = os.environ.get("STAMP_DEFS", "").split()  # e.g. STAMP_DEFS=-DSPL_ABL=4096
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-DSPL_STAMPS",
-                        "-shared", "-o", LIB, os.path.join(REPO, "splendor-gym_amd", "csrc", "spl_engine.hip")],
+                        *extra, "-shared", "-o", LIB, os.path.join(REPO, "splendor-gym_amd", "csrc", "spl_engine.hip")],
                        check=True)
         if "--build-only" in sys.argv:
             return 0
