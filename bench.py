@@ -1,6 +1,6 @@
 """Headline benchmark: env-steps/sec, 2-player Splendor, 65536 tables per MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--tables T] [--players P] [--mode step|rollout] [--also]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--tables T] [--players P] [--mode rollout|step] [--only]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 One "step" = one SplendorEnv.step on every table of the batch (BASELINE.json config 3: legal
@@ -8,9 +8,10 @@ mask + uniform-random policy, same-step autoreset, obs int32[297] + mask int8[45
 terminated + flags written per table-step, terminal rows to final_obs).  Actions come from the
 device policy (Philox over the new mask).  Two launch shapes compute the same trajectories and
 write the same per-step outputs (tests/test_gpu_parity.py::test_rollout_equals_step_chain):
-  --mode step     one spl_step launch per env step (the drop-in step path)
-  --mode rollout  one spl_rollout launch per 16 env steps (state stays in registers; each
-                  step's stores drain while the next step computes)
+  --mode rollout  (headline) one spl_rollout launch per 16 env steps: state stays in registers
+                  and each step's stores drain while the next step computes
+  --mode step     one spl_step launch per env step (the drop-in SplendorEnv.step path);
+                  the mode not selected is measured too and reported as "other_mode"
 plus a pool refill every 16 steps.  Inputs are resident in HBM before the timed region; the
 timed region replays captured HIP graphs of 64 steps.
 
@@ -77,13 +78,15 @@ def cpu_baseline(players, procs, steps_per_proc):
 
 def load_pmc_traffic(players, tables, mode, steps_per_launch):
     """HBM bytes per launch of the mode's kernel from the committed rocprofv3 PMC summary."""
-    path = os.path.join(REPO, "profiles", f"pmc_{mode}_summary.json")
+    path = os.path.join(REPO, "profiles", "pmc_summary.json")
+    kern = "k_step" if mode == "step" else "k_rollout"
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("players") == players and d.get("tables") == tables and d.get("steps_per_launch", 1) == steps_per_launch:
-            return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
-    except (OSError, ValueError):
+        if (d.get("players") == players and d.get("tables") == tables
+                and d.get("steps_per_launch", {}).get(kern) == steps_per_launch):
+            return d.get("hbm_bytes_per_launch", {}).get(kern), os.path.relpath(path, REPO)
+    except (OSError, ValueError, AttributeError):
         pass
     return None, None
 
@@ -101,10 +104,11 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=1_000_000, help="env steps per CPU process")
     ap.add_argument("--graph-steps", type=int, default=64,
                     help="steps per captured HIP graph (multiple of 32); 0 = eager launches")
-    ap.add_argument("--mode", choices=("step", "rollout"), default="step",
-                    help="step: one spl_step launch per env step; rollout: one spl_rollout launch per "
-                         f"{REFILL_EVERY} env steps (same trajectories and outputs)")
-    ap.add_argument("--also", action="store_true", help="also measure the other mode (reported as other_mode)")
+    ap.add_argument("--mode", choices=("step", "rollout"), default="rollout",
+                    help="rollout: one spl_rollout launch per "
+                         f"{REFILL_EVERY} env steps; step: one spl_step launch per env step (same trajectories "
+                         "and per-step outputs, tests/test_gpu_parity.py::test_rollout_equals_step_chain)")
+    ap.add_argument("--only", action="store_true", help="skip measuring the other mode (reported as other_mode)")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -222,7 +226,7 @@ def main():
 
     main_rec = measure(args.mode, 0)
     alt_rec = None
-    if args.also:
+    if not args.only:
         alt_rec = measure("rollout" if args.mode == "step" else "step", main_rec["k_next"])
     K = args.steps
     # correctness canaries on the measured run: no error flags, episodes completed

@@ -1,9 +1,9 @@
 """gymnasium if installed, else a minimal stand-in with the same surface.
 
 The reference requires gymnasium>=0.29.1 (pyproject.toml:14); this image has none, and the
-package must import without it.  The stand-in covers what SplendorEnv and the
-vector env use: Env (np_random seeding as in gymnasium 0.29), spaces.Discrete, spaces.Box,
-spaces.MultiDiscrete.
+package must import without it.  The stand-in covers what SplendorEnv, the
+wrappers and the vector env use: Env (np_random seeding as in gymnasium 0.29), Wrapper,
+spaces.Discrete, spaces.Box, spaces.MultiDiscrete.
 """
 import numpy as np
 
@@ -11,6 +11,7 @@ try:  # pragma: no cover - depends on the environment
     import gymnasium as _gym
 
     Env = _gym.Env
+    Wrapper = _gym.Wrapper
     spaces = _gym.spaces
     HAVE_GYMNASIUM = True
 except ImportError:
@@ -108,3 +109,32 @@ except ImportError:
 
         def close(self):
             pass
+
+    class Wrapper(Env):
+        """gymnasium.Wrapper surface the reference wrappers rely on: `env`, delegated reset /
+        step / spaces / attributes (e.g. `state`), `unwrapped`."""
+
+        def __init__(self, env):
+            self.env = env
+
+        def reset(self, **kwargs):
+            return self.env.reset(**kwargs)
+
+        def step(self, action):
+            return self.env.step(action)
+
+        def __getattr__(self, name):
+            if name.startswith("_"):
+                raise AttributeError(name)
+            return getattr(self.env, name)
+
+        @property
+        def unwrapped(self):
+            return self.env.unwrapped
+
+        @property
+        def np_random(self):
+            return self.env.np_random
+
+        def close(self):
+            return self.env.close()

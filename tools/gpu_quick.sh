@@ -11,7 +11,7 @@ if [ -z "$NO_STAMPS" ]; then
   timeout -k 10 500 python tools/stamps.py --run > $OUT/stamps_$TAG.txt 2>&1 || { echo "stamps failed"; exit 1; }
   cat $OUT/stamps_$TAG.txt
 fi
-timeout -k 10 600 python bench.py --no-cpu-baseline --also > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { echo "bench failed"; tail -20 $OUT/bench_$TAG.err; exit 1; }
+timeout -k 10 600 python bench.py --no-cpu-baseline > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err || { echo "bench failed"; tail -20 $OUT/bench_$TAG.err; exit 1; }
 python -c "
 import json; d=json.load(open('$OUT/bench_$TAG.json'))
 print('MAIN', d['config']['mode'], 'VALUE', d['value'], 'ms/step', d['ms_per_step'], 'kernel us', d['roofline']['kernel_avg_us'], 'frac', d['roofline']['frac'])

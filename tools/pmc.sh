@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes for the step and refill kernels (one rocprofv3 --pmc pass per counter group, each
+# PMC passes for the step, rollout and refill kernels (one rocprofv3 --pmc pass per counter group, each
 # with --kernel-trace only as gpurun requires; eager launches so every dispatch is counted).
 set -o pipefail
 TAG=${1:-r01}
@@ -17,7 +17,7 @@ IFS=';' read -ra GROUPS_LIST <<< "${PMC_GROUPS:-$GROUPS_DEFAULT}"
 i=0
 for grp in "${GROUPS_LIST[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${grp} --kernel-include-regex "k_step|k_refill" \
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${grp} --kernel-include-regex "k_step|k_rollout|k_refill" \
       --output-format csv -d $OUT/p$i -o run -- $BENCH > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
 done
 echo "pmc done"

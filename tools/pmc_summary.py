@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc passes (tools/pmc.sh) per kernel and write the per-launch HBM
-traffic of the step kernel for bench.py's roofline.traffic.
+traffic of the step and rollout kernels for bench.py's roofline.traffic.
 
-    python tools/pmc_summary.py gpurun_out/pmc_<tag> profiles/<round>/pmc_summary.json [--tables 65536 --players 2]
+    python tools/pmc_summary.py gpurun_out/pmc_<tag> profiles/pmc_summary.json [--tables 65536 --players 2]
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE counts exactly half the bytes of a wide (16 B/lane) coalesced read and other widths
@@ -24,7 +24,7 @@ def load(pmc_dir):
         times = {}
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            k = "k_step" if "k_step" in name else ("k_refill" if "k_refill" in name else name)
+            k = next((kk for kk in ("k_step", "k_rollout", "k_refill") if kk in name), name)
             key = (k, int(r["Dispatch_Id"]), r["Counter_Name"])
             acc[key] += float(r["Counter_Value"])
             times[(k, int(r["Dispatch_Id"]))] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
@@ -41,6 +41,7 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--tables", type=int, default=65536)
     ap.add_argument("--players", type=int, default=2)
+    ap.add_argument("--rollout-steps", type=int, default=16, help="env steps per k_rollout launch in the run")
     a = ap.parse_args()
     per, dur = load(a.pmc_dir)
     summary = {"tables": a.tables, "players": a.players, "source": a.pmc_dir, "kernels": {}}
@@ -74,17 +75,20 @@ def main():
             d["rdreq_bytes_64B"] = mean["TCC_EA0_RDREQ"] * 64
             d["wrreq_bytes_64B"] = mean.get("TCC_EA0_WRREQ", 0) * 64
         summary["kernels"][k] = d
-    st = summary["kernels"].get("k_step", {})
-    if "fetch_bytes" in st and "write_bytes" in st:
-        summary["hbm_bytes_per_launch"] = round(st["fetch_bytes"] + st["write_bytes"])
-        summary["hbm_bytes_note"] = ("FETCH_SIZE + WRITE_SIZE (KiB x 1024) per k_step launch, uncorrected: the "
-                                     "kernel's reads are 4-byte-per-lane, outside the guide's 16 B/lane calibration")
+    summary["hbm_bytes_per_launch"] = {}
+    for k in ("k_step", "k_rollout"):
+        st = summary["kernels"].get(k, {})
+        if "fetch_bytes" in st and "write_bytes" in st:
+            summary["hbm_bytes_per_launch"][k] = round(st["fetch_bytes"] + st["write_bytes"])
+    summary["steps_per_launch"] = {"k_step": 1, "k_rollout": a.rollout_steps}
+    summary["hbm_bytes_note"] = ("FETCH_SIZE + WRITE_SIZE (KiB x 1024) per launch, uncorrected: the kernels' reads "
+                                 "are 4-byte-per-lane planes and gathers, outside the guide's 16 B/lane calibration")
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     print(json.dumps({k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()
                           if kk != "counters_mean_per_dispatch"} for k, v in summary["kernels"].items()}, indent=1))
-    print("hbm_bytes_per_launch", summary.get("hbm_bytes_per_launch"))
+    print("hbm_bytes_per_launch", summary["hbm_bytes_per_launch"])
 
 
 if __name__ == "__main__":
