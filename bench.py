@@ -12,7 +12,7 @@ write the same per-step outputs (tests/test_gpu_parity.py::test_rollout_equals_s
                   and each step's stores drain while the next step computes
   --mode step     one spl_step launch per env step (the drop-in SplendorEnv.step path);
                   the mode not selected is measured too and reported as "other_mode"
-plus a pool refill every 16 steps.  Inputs are resident in HBM before the timed region; the
+plus a pool refill every 32 steps.  Inputs are resident in HBM before the timed region; the
 timed region replays captured HIP graphs of 64 steps.
 
 Weak scaling: each rank owns `--tables` tables (global ids rank*T ...), no collective in the
@@ -38,7 +38,8 @@ for _p in (REPO, os.path.join(REPO, "splendor-gym_amd")):
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 ALGO_BYTES = {2: 1370, 3: 1408, 4: 1446}  # 2*S_P + 297*4 + 45 + 4 + 4 + 1 (3p interpolated)
-REFILL_EVERY = 16  # pool refill period; random 2p games last >= 24 plies, so no inline deals
+REFILL_EVERY = 32  # pool refill period: two pool records per table cover two resets in between
+ROLLOUT_K = 16     # env steps per spl_rollout launch
 
 
 def cpu_baseline(players, procs, steps_per_proc):
@@ -103,10 +104,10 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--cpu-steps", type=int, default=1_000_000, help="env steps per CPU process")
     ap.add_argument("--graph-steps", type=int, default=64,
-                    help="steps per captured HIP graph (multiple of 32); 0 = eager launches")
+                    help="steps per captured HIP graph (multiple of 64); 0 = eager launches")
     ap.add_argument("--mode", choices=("step", "rollout"), default="rollout",
                     help="rollout: one spl_rollout launch per "
-                         f"{REFILL_EVERY} env steps; step: one spl_step launch per env step (same trajectories "
+                         f"{ROLLOUT_K} env steps; step: one spl_step launch per env step (same trajectories "
                          "and per-step outputs, tests/test_gpu_parity.py::test_rollout_equals_step_chain)")
     ap.add_argument("--only", action="store_true", help="skip measuring the other mode (reported as other_mode)")
     args = ap.parse_args()
@@ -155,8 +156,8 @@ def main():
 
     def run(mode, k0, k1, strm, ev=None):
         """Steps k0..k1-1 (ply k+1 relative to ply_base), refill every R steps.  mode "step":
-        one spl_step launch per step; "rollout": one spl_rollout launch per R steps."""
-        per = 1 if mode == "step" else R
+        one spl_step launch per step; "rollout": one spl_rollout launch per ROLLOUT_K steps."""
+        per = 1 if mode == "step" else ROLLOUT_K
         for i, k in enumerate(range(k0, k1, per)):
             sa = step_args[(k // per) & 1]
             sa.ply = k + 1
@@ -165,7 +166,7 @@ def main():
             if mode == "step":
                 _native.check(lib, lib.spl_step(ctx, desc, ctypes.byref(sa), strm))
             else:
-                _native.check(lib, lib.spl_rollout(ctx, desc, ctypes.byref(sa), R, 0, strm))
+                _native.check(lib, lib.spl_rollout(ctx, desc, ctypes.byref(sa), ROLLOUT_K, 0, strm))
             if ev is not None:
                 ev[1][i].record()
             if (k + per) % R == 0:
@@ -181,7 +182,7 @@ def main():
         graph, how = None, "eager"
         if G > 0:
             if G % (2 * R) or K % G:
-                raise SystemExit("--graph-steps must be a multiple of 32 that divides --steps")
+                raise SystemExit(f"--graph-steps must be a multiple of {2 * R} that divides --steps")
             try:
                 torch.cuda.synchronize(dev)
                 ply_base.fill_(k_base + W)
@@ -193,7 +194,7 @@ def main():
             except Exception as exc:  # capture unsupported: time eager launches instead
                 print(f"graph capture failed ({exc}); timing eager launches", file=sys.stderr)
                 graph, G = None, 0
-        per = 1 if mode == "step" else R
+        per = 1 if mode == "step" else ROLLOUT_K
         barrier(dev)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -237,7 +238,7 @@ def main():
     def summary(rec):
         total_steps = T * world * K
         algo = ALGO_BYTES[P] * T * rec["steps_per_launch"]
-        kname = f"spl::k_step<{P}>" if rec["mode"] == "step" else f"spl::k_rollout<{P}> ({R} steps per launch)"
+        kname = f"spl::k_step<{P}>" if rec["mode"] == "step" else f"spl::k_rollout<{P}> ({ROLLOUT_K} steps per launch)"
         return {"mode": rec["mode"], "value": round(total_steps / rec["elapsed"], 1),
                 "ms_per_step": round(rec["elapsed"] / K * 1e3, 4),
                 "roofline": {"bound": "hbm", "achieved": round(algo / rec["launch_s"] / 1e9, 1),
@@ -270,7 +271,8 @@ def main():
             "config": {"workload": f"{P}-player SplendorEnv.step x {T} tables per GPU, legal mask + uniform-random "
                                    "policy, same-step autoreset, obs int32[297] + mask int8[45] per table-step",
                        "tables_per_gpu": T, "players": P, "parallelism": f"table-sharded x{world}",
-                       "refill_every": R, "mode": main["mode"], "launch": main["launch"]},
+                       "refill_every": R, "rollout_steps_per_launch": ROLLOUT_K, "mode": main["mode"],
+                       "launch": main["launch"]},
             "roofline": roof,
             "cpu_baseline": cpu,
             "episodes": episodes,

@@ -100,7 +100,8 @@ const char *spl_last_error(void);
  * nobles: 10 x 6 int32 [req w,b,g,r,k, points]   (splendor_gym/engine/data/tables.json) */
 int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_ctx_t **out);
 int spl_ctx_destroy(spl_ctx_t *ctx);
-/* Pool refill period in steps (default 8); 0 disables automatic refills (inline deals). */
+/* Pool refill period in steps (default 32; two pool deals per table cover two resets in between);
+ * 0 disables automatic refills (inline deals). */
 int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period);
 
 int64_t spl_arena_bytes(int32_t n, int32_t players);
@@ -131,8 +132,8 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *args, vo
 int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *args, int32_t steps,
                 int32_t per_step_outputs, void *stream);
 
-/* Pool maintenance: deal the next episode of every table whose pool slot was consumed
- * (status bit ST_PENDING).  Tables it has not reached deal inline at their next reset. */
+/* Pool maintenance: every table with consumed pool records gets the earliest of them re-dealt
+ * (one deal per table per call).  A reset with both pool records consumed deals inline. */
 int spl_refill(spl_ctx_t *ctx, spl_arena_t *arena, void *stream);
 
 int spl_encode(spl_ctx_t *ctx, spl_arena_t *arena, int32_t *obs, void *stream);

@@ -89,7 +89,12 @@ __device__ uint64_t *g_stamps;
     do {         \
     } while (0)
 #endif
-constexpr int kScratchStride = 112;  // per-lane deal scratch in LDS (16-aligned)
+// Per-lane deal scratch in LDS: an odd number of dwords, so lanes at the same Fisher-Yates
+// position (the common case: lanes decrement their index in step) hit 64 different banks.
+#ifndef SPL_SCRATCH_STRIDE
+#define SPL_SCRATCH_STRIDE 116
+#endif
+constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 
 constexpr int kMaskStreamWords = 64 * 45 / 32;  // 90
 
@@ -343,7 +348,16 @@ __device__ __forceinline__ void pay_for_card(Pl &p, int bank[6], uint4 rec) {
 }
 
 __device__ __forceinline__ uint8_t *slot_rec(const KArena &A, int t, int slot) {
-    return A.slots + ((size_t)t * 2 + slot) * kSlotBytes;
+    return A.slots + ((size_t)t * kSlotRecords + slot) * kSlotBytes;
+}
+// slot-record ring status (spl_layout.h)
+__device__ __forceinline__ int active_of(uint32_t misc) { return (int)((misc >> ST_ACTIVE_SHIFT) & 3u); }
+__device__ __forceinline__ int pend_of(uint32_t misc) { return (int)((misc >> ST_PEND_SHIFT) & 3u); }
+__device__ __forceinline__ uint32_t ring_bits(int active, int pend) {
+    return ((uint32_t)active << ST_ACTIVE_SHIFT) | ((uint32_t)pend << ST_PEND_SHIFT);
+}
+__device__ __forceinline__ const uint8_t *live_rec(const KArena &A, int t, uint32_t misc) {
+    return slot_rec(A, t, active_of(misc));
 }
 
 // engine/rules.py:125-129 _refill_slot / deck.pop() of tier t.  `top` is the card at
@@ -863,10 +877,10 @@ __device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec
         i = adv ? (d == 1 ? 29 : (d == 2 ? 19 : 9)) : i2;
     }
     // deck bytes (list order; the 4 dealt cards per tier sit past deck_len)
-    const uint4 *s4 = reinterpret_cast<const uint4 *>(scr);
-    uint4 *r4 = reinterpret_cast<uint4 *>(rec);
+    const uint32_t *s1 = reinterpret_cast<const uint32_t *>(scr);  // 4-byte aligned scratch
+    uint32_t *r1 = reinterpret_cast<uint32_t *>(rec);
 #pragma unroll
-    for (int q = 0; q < 6; ++q) r4[q] = s4[q];
+    for (int q = 0; q < 24; ++q) r1[q] = s1[q];
 #pragma unroll
     for (int t = 0; t < 3; ++t) {  // board[tier][i] = deck.pop()
         const int b = tier_base(t), n = tier_size(t);
@@ -878,8 +892,24 @@ __device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec
 #pragma unroll
     for (int s = 0; s < 4; ++s) out.nob0 |= (s < nn ? (uint32_t)scr[90 + s] : 0xFFu) << (8 * s);
     out.nob1 = nn > 4 ? (uint32_t)scr[94] : 0xFFu;
-    reinterpret_cast<uint32_t *>(rec)[kRecSeed / 4] = seed;
+    uint32_t *rw = reinterpret_cast<uint32_t *>(rec);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) rw[kRecTail / 4 + k] = out.board[k];
+    rw[kRecTail / 4 + 3] = out.nob0;
+    rw[kRecTail / 4 + 4] = out.nob1;
+    rw[kRecSeed / 4] = seed;
     return flags;
+}
+
+// the board / noble words of a dealt record (its bytes 96..115)
+__device__ __forceinline__ Deal rec_deal(const uint8_t *rec) {
+    const uint32_t *rw = reinterpret_cast<const uint32_t *>(rec);
+    Deal d;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d.board[k] = rw[kRecTail / 4 + k];
+    d.nob0 = rw[kRecTail / 4 + 3];
+    d.nob1 = rw[kRecTail / 4 + 4];
+    return d;
 }
 
 template <int P>
@@ -1053,7 +1083,7 @@ __device__ __forceinline__ StepPre step_prefetch(const Tab<P> &T, int action, bo
     const int ptier = pop_tier(action);
     if (live_tab && ptier >= 0) {
         const int len = (int)bget(T.sw[SW_DECK], ptier);
-        const uint8_t *live = slot_rec(A, t, (T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0);
+        const uint8_t *live = live_rec(A, t, T.sw[SW_MISC]);
         if (len > 0) pre.top = live[tier_base(ptier) + len - 1];
     }
     if (live_tab && action >= 0 && action < SPL_NUM_ACTIONS) {
@@ -1135,15 +1165,30 @@ __device__ __forceinline__ float final_reward_p0(const Tab<P> &T) {
     return w < 0 ? (tl ? -0.1f : 0.0f) : (w == 0 ? 1.0f : -1.0f);
 }
 
-// same-step autoreset (envs/splendor_env.py:43-44: the pool deal continues the np_random
-// stream); the pool is consumed, so a second reset before the next refill deals inline
+// Reset to the next episode of the table's engine-seed stream (envs/splendor_env.py:43-44:
+// reset() continues self.np_random): the live record moves to the next pool record, whose
+// board / noble words `pool` holds.  With both pool records consumed (two resets since the last
+// refill) the next one is dealt inline — correct, only slower.  When the pool record after it
+// is dealt, its words are gathered into `pool` for the next reset (the caller stores them to the
+// pool planes); returns true in that case.
+template <int P>
+__device__ __forceinline__ bool flip_to_pool(Tab<P> &T, const KArena &A, int t, Deal &pool, uint8_t *scr,
+                                             uint32_t &flags) {
+    const uint32_t misc = T.sw[SW_MISC];
+    const int a = active_of(misc), pend = pend_of(misc);
+    const int nxt = a == 2 ? 0 : a + 1;
+    if (pend >= 2) flags |= deal_next<P>(A, t, nxt, scr, pool);
+    const int pend2 = pend >= 2 ? 2 : pend + 1;  // the old live record is free now
+    fresh_state(T, ring_bits(nxt, pend2), pool);
+    if (pend2 < 2) pool = rec_deal(slot_rec(A, t, nxt == 2 ? 0 : nxt + 1));
+    return pend2 < 2;
+}
+
+// same-step autoreset of a terminal table; `pool_dirty` is set when the pool planes changed
 template <int P>
 __device__ __forceinline__ void autoreset_table(Tab<P> &T, const KArena &A, int t, Deal &pool, uint8_t *scr,
-                                                StepOut &o) {
-    const int nxt = ((T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0) ^ 1;
-    if (T.sw[SW_MISC] & ST_PENDING)  // pool not refilled yet: deal inline (correct, slower)
-        o.flags |= deal_next<P>(A, t, nxt, scr, pool);
-    fresh_state(T, (nxt ? ST_ACTIVE : 0u) | ST_PENDING, pool);
+                                                StepOut &o, bool &pool_dirty) {
+    pool_dirty |= flip_to_pool<P>(T, A, t, pool, scr, o.flags);
     o.flags |= SPL_F_RESET;
     o.mask = kFreshDealMask;
 }
@@ -1202,7 +1247,9 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     const int fin_moves = get_moves(T.sw);
     const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;
     STAMP(5);
-    if (valid && o.term && S.autoreset && !abl(ABL_RESET)) autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], o);
+    bool pool_dirty = false;
+    if (valid && o.term && S.autoreset && !abl(ABL_RESET))
+        autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], o, pool_dirty);
     STAMP(6);
     wave_lds_sync();  // deal scratch (rows) free again
 
@@ -1244,6 +1291,7 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
             S.next_actions[t] = sample_uniform(o.mask, S.policy_seed, (uint64_t)(S.table0 + t), ply);
         }
         if (!abl(ABL_TAB_STORE)) store_tab(T, A, t);
+        if (pool_dirty) store_pool(A, t, pool);
     }
     STAMP(11);
 }
@@ -1276,6 +1324,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         fresh_state(T, 0u, empty_deal());
     }
     StepPre pre = step_prefetch(T, action, valid, A, t, Tb);
+    bool pool_dirty = false;
     const uint64_t ply0 = S.ply + (S.ply_base ? *S.ply_base : 0ull);
     const bool want_final = S.autoreset && S.final_obs != nullptr;
     for (int k = 0; k < K; ++k) {
@@ -1290,7 +1339,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
             if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], final_reward_p0(T));
             if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
         }
-        if (valid && o.term && S.autoreset) autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], o);
+        if (valid && o.term && S.autoreset) autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], o, pool_dirty);
         wave_lds_sync();
         encode_row(T, &L.rows[lane * kObsDim], L);
         L.mask[lane] = o.mask;
@@ -1320,6 +1369,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
     if (valid) {
         if (S.next_actions) S.next_actions[t] = action;
         store_tab(T, A, t);
+        if (pool_dirty) store_pool(A, t, pool);
     }
 }
 
@@ -1356,13 +1406,11 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
             deal_into(seed1, P, slot_rec(A, t, 1), scr, d1);
             store_pcg(A, t, g);
             store_pool(A, t, d1);
-            fresh_state(T, 0u, d0);  // record 0 live, record 1 the ready pool
+            fresh_state(T, ring_bits(0, 1), d0);  // record 0 live, 1 the next pool, 2 for the refill
         } else {       // reset() without a seed: continue the stream (pool deal)
-            const int nxt = ((T.sw[SW_MISC] & ST_ACTIVE) ? 1 : 0) ^ 1;
-            Deal d;
-            if (T.sw[SW_MISC] & ST_PENDING) deal_next<P>(A, t, nxt, scr, d);
-            else d = load_pool(A, t);
-            fresh_state(T, (nxt ? ST_ACTIVE : 0u) | ST_PENDING, d);
+            Deal d = pend_of(T.sw[SW_MISC]) < 2 ? load_pool(A, t) : empty_deal();
+            uint32_t fl = 0;
+            if (flip_to_pool<P>(T, A, t, d, scr, fl)) store_pool(A, t, d);
         }
     }
     wave_lds_sync();
@@ -1376,12 +1424,12 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
     if (valid) store_tab(T, A, t);
 }
 
-// Pool refill: deal the next episode of every table whose pool was consumed (ST_PENDING).
-// Waves without such a table exit after one coalesced read of the status plane.
-// The deal is one long serial chain per lane (CPython init_by_array + the shuffle's MT
-// outputs), so a wave's time is latency-bound and the same whether it carries 5 or 64 pending
-// tables: the scratch is padded to a quarter of the CU's LDS so the dispatcher spreads the
-// waves one per SIMD over the whole chip instead of stacking them on a few CUs.
+// Pool refill: every table with consumed pool records gets ONE of them re-dealt per call, the
+// earliest free one in ring order (the next episode's deal comes first in the engine-seed
+// stream), so a call costs one deal per wave however many resets happened since the last one.
+// The deal is one long serial chain per lane (CPython init_by_array + the shuffle's MT outputs):
+// a wave's time is the same whether it carries 5 or 64 pending tables, so the scratch is padded
+// to a quarter of the CU's LDS and the dispatcher spreads the waves one per SIMD.
 constexpr int kRefillLds = 40 * 1024;
 template <int P>
 __global__ __launch_bounds__(64) void k_refill(KArena A) {
@@ -1390,12 +1438,14 @@ __global__ __launch_bounds__(64) void k_refill(KArena A) {
     if (t >= A.n) return;
     const size_t mi = (size_t)SW_MISC * A.n + t;
     const uint32_t misc = A.planes[mi];
-    if (!(misc & ST_PENDING)) return;
-    const int nxt = ((misc & ST_ACTIVE) ? 1 : 0) ^ 1;
+    const int pend = pend_of(misc);
+    if (pend == 0) return;
+    const int a = active_of(misc);
+    const int slot = (a + 3 - pend) % 3;  // pend 2: the next pool record, pend 1: the one after
     Deal d;
-    deal_next<P>(A, t, nxt, &scr_all[lane_id() * kScratchStride], d);
-    store_pool(A, t, d);
-    A.planes[mi] = misc & ~ST_PENDING;
+    deal_next<P>(A, t, slot, &scr_all[lane_id() * kScratchStride], d);
+    if (pend == 2) store_pool(A, t, d);   // it is the next pool: its words go to the pool planes
+    A.planes[mi] = (misc & ~ST_PEND) | ((uint32_t)(pend - 1) << ST_PEND_SHIFT);
 }
 
 // Observation and/or mask of the current state (spl_encode / spl_legal).
@@ -1478,7 +1528,7 @@ __global__ __launch_bounds__(64) void k_download(KArena A, int first, int count,
         const int id = (int)bget(sw[SW_BOARD + k / 4], k % 4);
         v.board[k] = id == 0xFF ? -1 : id;
     }
-    const uint8_t *rec = slot_rec(A, t, (sw[SW_MISC] & ST_ACTIVE) ? 1 : 0);
+    const uint8_t *rec = live_rec(A, t, sw[SW_MISC]);
     for (int tt = 0; tt < 3; ++tt) {
         const int len = (int)bget(sw[SW_DECK], tt);
         v.deck_len[tt] = len;
@@ -1512,7 +1562,7 @@ __global__ __launch_bounds__(64) void k_upload(KArena A, int first, int count, c
     sw[SW_BANK1] = ((uint32_t)v.to_play << 16) | ((uint32_t)v.turn_count << 24);
     put_bank(sw, bank);
     sw[SW_MISC] = ((uint32_t)v.move_count & 0xFFFFu) | (v.game_over ? ST_GAME_OVER : 0u) |
-                  (v.turn_limit_reached ? ST_TURN_LIMIT : 0u) | (old_misc & (ST_ACTIVE | ST_PENDING)) |
+                  (v.turn_limit_reached ? ST_TURN_LIMIT : 0u) | (old_misc & (ST_ACTIVE | ST_PEND)) |
                   ((uint32_t)(v.winner + 1) << 24);
     for (int tt = 0; tt < 3; ++tt) {
         uint32_t w = 0;
@@ -1556,7 +1606,7 @@ __global__ __launch_bounds__(64) void k_upload(KArena A, int first, int count, c
         pack_pl(p, T.pw[q]);
     }
     store_tab(T, A, t);
-    uint8_t *rec = slot_rec(A, t, (old_misc & ST_ACTIVE) ? 1 : 0);
+    uint8_t *rec = slot_rec(A, t, active_of(old_misc));
     for (int tt = 0; tt < 3; ++tt)
         for (int k = 0; k < tier_size(tt); ++k) rec[tier_base(tt) + k] = (uint8_t)(k < v.deck_len[tt] ? v.decks[tt][k] : 0xFF);
 }
@@ -1672,7 +1722,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     HIP_TRY(hipSetDevice(device));
     spl_ctx_t *c = new spl_ctx_t();
     c->device = device;
-    c->refill_period = 8;
+    c->refill_period = 32;
     if (hipMalloc(&c->cards, sizeof(uint4) * 90) != hipSuccess || hipMalloc(&c->nobles, sizeof(uint2) * 10) != hipSuccess ||
         hipMalloc(&c->lut, sizeof(uint4) * kLutEntries) != hipSuccess) {
         spl_ctx_destroy(c);
@@ -1743,7 +1793,7 @@ int spl_arena_init(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
     HIP_TRY(hipMemsetAsync(arena->base, 0, (size_t)spl_arena_bytes(arena->n, arena->players), s));
     // no pool deal yet: a reset() without seed deals inline, the refill kernel deals it
     const KArena A = karena(arena);
-    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(A.planes + (size_t)SW_MISC * arena->n), (int)ST_PENDING,
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(A.planes + (size_t)SW_MISC * arena->n), (int)(2u << ST_PEND_SHIFT),
                               (size_t)arena->n, s));
     arena->steps = 0;
     arena->epoch = 0;

@@ -18,13 +18,15 @@
 // The 13 observation bytes of a player (tokens 6, bonuses 5, prestige, n_reserved —
 // reference engine/encode.py:131-142) are exactly PW0, PW1, PW2 and (PW3 & 3).
 //
-// Deck storage: two 128-byte SLOT RECORDS per table (AoS, [n][2][128]).  The active record
-// holds the live deck (bytes 0..89: tier 1 at 0, tier 2 at 40, tier 3 at 70, list order, top
-// = deck_len-1); the other is the POOL: the next episode's deal, prepared ahead from the
-// table's engine-seed stream.  The pool deal's board and noble words sit in their own word
-// planes (PL_*), read with the state at the top of every step, so a same-step autoreset needs
-// no late gather.  ST_PENDING marks a table whose pool was consumed (the refill kernel deals
-// it again); record bytes 124..127 keep the deal's engine seed (diagnostic).
+// Deck storage: three 128-byte SLOT RECORDS per table (AoS, [n][3][128]), used as a ring.  The
+// live record (status bits ST_ACTIVE) holds the table's deck (bytes 0..89: tier 1 at 0, tier 2
+// at 40, tier 3 at 70, list order, top = deck_len-1); the next two records in ring order are the
+// POOL: the next two episodes' deals, prepared ahead from the table's engine-seed stream by the
+// refill kernel.  ST_PEND counts pool records consumed and not yet re-dealt (0..2; the LAST
+// `pend` records in ring order are the free ones).  Record bytes 96..115 hold the deal's board
+// and noble words, 124..127 its engine seed (diagnostic).  The next pool's board and noble
+// words are also kept in their own word planes (PL_*), read with the state at the top of every
+// step, so a same-step autoreset needs no late gather.
 #pragma once
 #include <stdint.h>
 
@@ -46,10 +48,14 @@ __host__ __device__ constexpr int pw_index(int p, int k) { return SW_COUNT + 4 *
 // SW_MISC status bits
 constexpr uint32_t ST_GAME_OVER = 1u << 16;
 constexpr uint32_t ST_TURN_LIMIT = 1u << 17;
-constexpr uint32_t ST_ACTIVE = 1u << 18;   // which slot record holds the live deck
-constexpr uint32_t ST_PENDING = 1u << 19;  // pool consumed (or never dealt): refill deals it
+constexpr int ST_ACTIVE_SHIFT = 18;        // 2 bits: slot record (0..2) holding the live deck
+constexpr uint32_t ST_ACTIVE = 3u << ST_ACTIVE_SHIFT;
+constexpr int ST_PEND_SHIFT = 20;          // 2 bits: pool records consumed, not yet re-dealt
+constexpr uint32_t ST_PEND = 3u << ST_PEND_SHIFT;
+constexpr int kSlotRecords = 3;
 
 constexpr int kSlotBytes = 128;
+constexpr int kRecTail = 96;    // board x3, nob0, nob1 words of the deal
 constexpr int kRecSeed = 124;   // engine seed of the deal (diagnostic)
 
 // pool planes: the pool deal's SW_BOARD.. and SW_NOB0/1 words (SW_DECK at deal is a constant)
@@ -76,7 +82,7 @@ __host__ __device__ inline ArenaLayout arena_layout(int64_t n, int P) {
     L.planes = 0;
     L.pool = align256(L.planes + (int64_t)num_words(P) * n * 4);
     L.slots = align256(L.pool + (int64_t)PL_COUNT * n * 4);
-    L.pcg = align256(L.slots + n * 2 * kSlotBytes);
+    L.pcg = align256(L.slots + n * kSlotRecords * kSlotBytes);
     L.total = align256(L.pcg + n * kPcgBytes);
     return L;
 }

@@ -1,7 +1,7 @@
 // Where does a pool deal's time go?  Per-lane CPython MT19937 init_by_array (serial chain),
 // the deal's output stream, and the full Fisher-Yates deal with its LDS scratch, each on a
 // full grid (1024 waves, one per SIMD) and on the refill's typical grid (273 waves).
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/microbench_deal.hip -o tools/microbench_deal.bin
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 [-DSPL_SCRATCH_STRIDE=112] tools/microbench_deal.hip -o ...
 #include "../splendor-gym_amd/csrc/spl_engine.hip"
 
 using namespace spl;
