@@ -12,7 +12,7 @@ write the same per-step outputs (tests/test_gpu_parity.py::test_rollout_equals_s
                   and each step's stores drain while the next step computes
   --mode step     one spl_step launch per env step (the drop-in SplendorEnv.step path);
                   the mode not selected is measured too and reported as "other_mode"
-plus a pool refill every 32 steps.  Inputs are resident in HBM before the timed region; the
+plus a pool refill every 64 steps.  Inputs are resident in HBM before the timed region; the
 timed region replays captured HIP graphs of 64 steps.
 
 Weak scaling: each rank owns `--tables` tables (global ids rank*T ...), no collective in the
@@ -38,7 +38,7 @@ for _p in (REPO, os.path.join(REPO, "splendor-gym_amd")):
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 ALGO_BYTES = {2: 1370, 3: 1408, 4: 1446}  # 2*S_P + 297*4 + 45 + 4 + 4 + 1 (3p interpolated)
-REFILL_EVERY = 32  # pool refill period: two pool records per table cover two resets in between
+REFILL_EVERY = 64  # pool refill period: three pool records per table cover three resets in between
 ROLLOUT_K = 16     # env steps per spl_rollout launch
 
 
@@ -96,15 +96,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1024)
-    ap.add_argument("--warmup", type=int, default=96)
+    ap.add_argument("--warmup", type=int, default=128)
     ap.add_argument("--tables", type=int, default=65536, help="tables per GPU")
     ap.add_argument("--players", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--cpu-steps", type=int, default=1_000_000, help="env steps per CPU process")
-    ap.add_argument("--graph-steps", type=int, default=64,
-                    help="steps per captured HIP graph (multiple of 64); 0 = eager launches")
+    ap.add_argument("--graph-steps", type=int, default=128,
+                    help="steps per captured HIP graph (multiple of 128); 0 = eager launches")
     ap.add_argument("--mode", choices=("step", "rollout"), default="rollout",
                     help="rollout: one spl_rollout launch per "
                          f"{ROLLOUT_K} env steps; step: one spl_step launch per env step (same trajectories "

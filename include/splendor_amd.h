@@ -100,7 +100,7 @@ const char *spl_last_error(void);
  * nobles: 10 x 6 int32 [req w,b,g,r,k, points]   (splendor_gym/engine/data/tables.json) */
 int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_ctx_t **out);
 int spl_ctx_destroy(spl_ctx_t *ctx);
-/* Pool refill period in steps (default 32; two pool deals per table cover two resets in between);
+/* Pool refill period in steps (default 64; three pool deals per table cover three resets in between);
  * 0 disables automatic refills (inline deals). */
 int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period);
 

@@ -1167,21 +1167,22 @@ __device__ __forceinline__ float final_reward_p0(const Tab<P> &T) {
 
 // Reset to the next episode of the table's engine-seed stream (envs/splendor_env.py:43-44:
 // reset() continues self.np_random): the live record moves to the next pool record, whose
-// board / noble words `pool` holds.  With both pool records consumed (two resets since the last
-// refill) the next one is dealt inline — correct, only slower.  When the pool record after it
-// is dealt, its words are gathered into `pool` for the next reset (the caller stores them to the
-// pool planes); returns true in that case.
+// board / noble words `pool` holds.  With every pool record consumed since the last refill the
+// next one is dealt inline — correct, only slower.  When the pool record after it is dealt, its
+// words are gathered into `pool` for the next reset (the caller stores them to the pool
+// planes); returns true in that case.
 template <int P>
 __device__ __forceinline__ bool flip_to_pool(Tab<P> &T, const KArena &A, int t, Deal &pool, uint8_t *scr,
                                              uint32_t &flags) {
+    constexpr int kPools = kSlotRecords - 1;
     const uint32_t misc = T.sw[SW_MISC];
     const int a = active_of(misc), pend = pend_of(misc);
-    const int nxt = a == 2 ? 0 : a + 1;
-    if (pend >= 2) flags |= deal_next<P>(A, t, nxt, scr, pool);
-    const int pend2 = pend >= 2 ? 2 : pend + 1;  // the old live record is free now
+    const int nxt = (a + 1) % kSlotRecords;
+    if (pend >= kPools) flags |= deal_next<P>(A, t, nxt, scr, pool);
+    const int pend2 = pend >= kPools ? kPools : pend + 1;  // the old live record is free now
     fresh_state(T, ring_bits(nxt, pend2), pool);
-    if (pend2 < 2) pool = rec_deal(slot_rec(A, t, nxt == 2 ? 0 : nxt + 1));
-    return pend2 < 2;
+    if (pend2 < kPools) pool = rec_deal(slot_rec(A, t, (nxt + 1) % kSlotRecords));
+    return pend2 < kPools;
 }
 
 // same-step autoreset of a terminal table; `pool_dirty` is set when the pool planes changed
@@ -1406,9 +1407,9 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
             deal_into(seed1, P, slot_rec(A, t, 1), scr, d1);
             store_pcg(A, t, g);
             store_pool(A, t, d1);
-            fresh_state(T, ring_bits(0, 1), d0);  // record 0 live, 1 the next pool, 2 for the refill
+            fresh_state(T, ring_bits(0, kSlotRecords - 2), d0);  // record 0 live, 1 the next pool, the rest for refills
         } else {       // reset() without a seed: continue the stream (pool deal)
-            Deal d = pend_of(T.sw[SW_MISC]) < 2 ? load_pool(A, t) : empty_deal();
+            Deal d = pend_of(T.sw[SW_MISC]) < kSlotRecords - 1 ? load_pool(A, t) : empty_deal();
             uint32_t fl = 0;
             if (flip_to_pool<P>(T, A, t, d, scr, fl)) store_pool(A, t, d);
         }
@@ -1441,10 +1442,10 @@ __global__ __launch_bounds__(64) void k_refill(KArena A) {
     const int pend = pend_of(misc);
     if (pend == 0) return;
     const int a = active_of(misc);
-    const int slot = (a + 3 - pend) % 3;  // pend 2: the next pool record, pend 1: the one after
+    const int slot = (a + kSlotRecords - pend) % kSlotRecords;  // earliest free record in ring order
     Deal d;
     deal_next<P>(A, t, slot, &scr_all[lane_id() * kScratchStride], d);
-    if (pend == 2) store_pool(A, t, d);   // it is the next pool: its words go to the pool planes
+    if (pend == kSlotRecords - 1) store_pool(A, t, d);  // it is the next pool: words to the pool planes
     A.planes[mi] = (misc & ~ST_PEND) | ((uint32_t)(pend - 1) << ST_PEND_SHIFT);
 }
 
@@ -1722,7 +1723,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     HIP_TRY(hipSetDevice(device));
     spl_ctx_t *c = new spl_ctx_t();
     c->device = device;
-    c->refill_period = 32;
+    c->refill_period = 64;
     if (hipMalloc(&c->cards, sizeof(uint4) * 90) != hipSuccess || hipMalloc(&c->nobles, sizeof(uint2) * 10) != hipSuccess ||
         hipMalloc(&c->lut, sizeof(uint4) * kLutEntries) != hipSuccess) {
         spl_ctx_destroy(c);
@@ -1793,7 +1794,8 @@ int spl_arena_init(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
     HIP_TRY(hipMemsetAsync(arena->base, 0, (size_t)spl_arena_bytes(arena->n, arena->players), s));
     // no pool deal yet: a reset() without seed deals inline, the refill kernel deals it
     const KArena A = karena(arena);
-    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(A.planes + (size_t)SW_MISC * arena->n), (int)(2u << ST_PEND_SHIFT),
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(A.planes + (size_t)SW_MISC * arena->n),
+                              (int)((uint32_t)(kSlotRecords - 1) << ST_PEND_SHIFT),
                               (size_t)arena->n, s));
     arena->steps = 0;
     arena->epoch = 0;

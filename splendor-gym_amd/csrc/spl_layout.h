@@ -18,11 +18,11 @@
 // The 13 observation bytes of a player (tokens 6, bonuses 5, prestige, n_reserved —
 // reference engine/encode.py:131-142) are exactly PW0, PW1, PW2 and (PW3 & 3).
 //
-// Deck storage: three 128-byte SLOT RECORDS per table (AoS, [n][3][128]), used as a ring.  The
-// live record (status bits ST_ACTIVE) holds the table's deck (bytes 0..89: tier 1 at 0, tier 2
-// at 40, tier 3 at 70, list order, top = deck_len-1); the next two records in ring order are the
-// POOL: the next two episodes' deals, prepared ahead from the table's engine-seed stream by the
-// refill kernel.  ST_PEND counts pool records consumed and not yet re-dealt (0..2; the LAST
+// Deck storage: kSlotRecords 128-byte SLOT RECORDS per table (AoS, [n][4][128]), used as a
+// ring.  The live record (status bits ST_ACTIVE) holds the table's deck (bytes 0..89: tier 1 at
+// 0, tier 2 at 40, tier 3 at 70, list order, top = deck_len-1); the next records in ring order
+// are the POOL: the next episodes' deals, prepared ahead from the table's engine-seed stream by
+// the refill kernel.  ST_PEND counts pool records consumed and not yet re-dealt (0..3; the LAST
 // `pend` records in ring order are the free ones).  Record bytes 96..115 hold the deal's board
 // and noble words, 124..127 its engine seed (diagnostic).  The next pool's board and noble
 // words are also kept in their own word planes (PL_*), read with the state at the top of every
@@ -52,7 +52,7 @@ constexpr int ST_ACTIVE_SHIFT = 18;        // 2 bits: slot record (0..2) holding
 constexpr uint32_t ST_ACTIVE = 3u << ST_ACTIVE_SHIFT;
 constexpr int ST_PEND_SHIFT = 20;          // 2 bits: pool records consumed, not yet re-dealt
 constexpr uint32_t ST_PEND = 3u << ST_PEND_SHIFT;
-constexpr int kSlotRecords = 3;
+constexpr int kSlotRecords = 4;            // live record + up to 3 pool deals (ST_PEND <= 3)
 
 constexpr int kSlotBytes = 128;
 constexpr int kRecTail = 96;    // board x3, nob0, nob1 words of the deal

@@ -21,7 +21,7 @@ class Engine:
     so results do not depend on how tables are split across GPUs.
     """
 
-    def __init__(self, num_tables, num_players=2, device=None, refill_period=32, table0=0):
+    def __init__(self, num_tables, num_players=2, device=None, refill_period=64, table0=0):
         torch = _native.require_gpu()
         self.torch = torch
         self.lib = _native.load_library()
