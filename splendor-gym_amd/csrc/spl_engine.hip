@@ -84,9 +84,24 @@ __device__ uint64_t *g_stamps;
         if (threadIdx.x == 0) g_stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
         __builtin_amdgcn_sched_barrier(0);                                                       \
     } while (0)
+// k_rollout keeps its stamps in registers (lane k holds step k's) so that stamping never waits
+// on the stores in flight; they are written to g_rstamps[wave][step][kRStamps] at the end.
+constexpr int kRStamps = 6;
+__device__ uint64_t *g_rstamps;
+#define RSTAMP(i, k)                                                                             \
+    do {                                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        const uint64_t tt_ = __builtin_amdgcn_s_memrealtime();                                   \
+        rst_lo[i] = lane_id() == (k) ? (int)(uint32_t)tt_ : rst_lo[i];                           \
+        rst_hi[i] = lane_id() == (k) ? (int)(uint32_t)(tt_ >> 32) : rst_hi[i];                   \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+    } while (0)
 #else
 #define STAMP(i) \
     do {         \
+    } while (0)
+#define RSTAMP(i, k) \
+    do {             \
     } while (0)
 #endif
 // Per-lane deal scratch in LDS: an odd number of dwords, so lanes at the same Fisher-Yates
@@ -777,6 +792,30 @@ __device__ __forceinline__ v4i expand4(uint32_t w) {
     return v;
 }
 
+// Part [d0, d1) (LDS words, multiples of 64*5 except the end) of a FULL wave's observation block.
+__device__ __forceinline__ void store_obs_range(const BlockLDS &L, int32_t *dst, int d0, int d1) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(L.rows);
+    v4i *out = reinterpret_cast<v4i *>(dst);
+    constexpr int U = 5;
+    int d = d0 + lane_id();
+#pragma unroll 1
+    for (; d + 64 * (U - 1) < d1; d += 64 * U) {
+        uint32_t w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) out[d + 64 * u] = expand4(w[u]);
+    }
+    uint32_t w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) w[u] = (d + 64 * u < d1) ? src[d + 64 * u] : 0u;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (d + 64 * u < d1) out[d + 64 * u] = expand4(w[u]);
+}
+constexpr int kObsBlockWords = 64 * kObsDim / 4;  // 4752 LDS words = 4752 16-byte stores per wave
+constexpr int kObsSplit = 64 * 5 * 7;             // 2240: 35 stores per lane in the first part
+
 // Block store of this wave's observation rows: LDS bytes [rows][297] -> int32 [rows][297] at
 // dst (16-byte aligned: 64-row blocks are 76032 B).  Dword d of the block is LDS word d.
 __device__ __forceinline__ void store_obs_block(const BlockLDS &L, int rows, int32_t *dst) {
@@ -825,6 +864,17 @@ __device__ __forceinline__ void store_mask_block(BlockLDS &L, int rows, int8_t *
         }
     }
     wave_lds_sync();
+    if (rows == 64 && ((uintptr_t)dst & 15u) == 0) {  // 180 x 16 B: 3 stores per lane
+        v4i *out4 = reinterpret_cast<v4i *>(dst);
+        for (int c = lane_id(); c < 180; c += 64) {
+            const uint32_t half = (L.mbits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;  // stream bits 16c..16c+15
+            v4i v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = (int)((((half >> (4 * q)) & 0xFu) * 0x00204081u) & 0x01010101u);
+            out4[c] = v;
+        }
+        return;
+    }
     const int nbytes = rows * 45;
     const int full = nbytes >> 2;
     uint32_t *out = reinterpret_cast<uint32_t *>(dst);
@@ -1328,10 +1378,23 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
     bool pool_dirty = false;
     const uint64_t ply0 = S.ply + (S.ply_base ? *S.ply_base : 0ull);
     const bool want_final = S.autoreset && S.final_obs != nullptr;
+    // A wave may have 63 memory instructions in flight; a step's ~90 stores would stall it until
+    // its own first stores drained.  So the obs block leaves in two parts: the first with the
+    // step's other outputs, the rest after the NEXT step's rules (from the same LDS rows, before
+    // anything overwrites them), and the wave computes while each part drains.
+    int32_t *obs_tail = nullptr;  // second part of the previous step's obs block, not yet issued
+#ifdef SPL_STAMPS
+    int rst_lo[kRStamps] = {0}, rst_hi[kRStamps] = {0};
+#endif
     for (int k = 0; k < K; ++k) {
         const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
         wave_lds_sync();  // previous step's LDS reads done (rows, mask, frows)
+        RSTAMP(0, k);
         StepOut o = step_rules(T, action, pre, valid, L, Tb);
+        RSTAMP(1, k);
+        if (obs_tail) store_obs_range(L, obs_tail, kObsSplit, kObsBlockWords);
+        obs_tail = nullptr;
+        RSTAMP(2, k);
         const int8_t wnr = (int8_t)get_winner(T.sw);
         const uint64_t fin = __ballot(valid && o.term && want_final);
         if (valid && o.term && want_final) encode_row(T, &L.frows[lane * kObsDim], L);
@@ -1345,17 +1408,24 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         encode_row(T, &L.rows[lane * kObsDim], L);
         L.mask[lane] = o.mask;
         wave_lds_sync();
+        RSTAMP(3, k);
         // the policy's next action and its prefetches go out before this step's stores
         action = sample_uniform(o.mask, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
         if (k + 1 < K) pre = step_prefetch(T, action, valid, A, t, Tb);
         int32_t *obs = S.obs + blk * kObsDim;
-        store_obs_block(L, rows, obs + (size_t)t0 * kObsDim);
+        const bool patch = valid && get_moves(T.sw) > 255;
+        const bool fpatch = valid && o.term && want_final && fin_moves > 255;
+        const bool split = rows == 64 && !__any(patch || fpatch);  // crafted states store at once
+        if (split) {
+            store_obs_range(L, obs + (size_t)t0 * kObsDim, 0, kObsSplit);
+            obs_tail = obs + (size_t)t0 * kObsDim;
+        } else {
+            store_obs_block(L, rows, obs + (size_t)t0 * kObsDim);
+        }
         store_mask_block(L, rows, S.mask + blk * 45 + (size_t)t0 * 45);
         int32_t *fobs = want_final ? S.final_obs + blk * kObsDim : nullptr;
         if (want_final) store_final_rows(L, fin, fobs, t0);
-        const bool patch = valid && get_moves(T.sw) > 255;
-        const bool fpatch = valid && o.term && want_final && fin_moves > 255;
-        if (__any(patch || fpatch)) {  // crafted states only (see k_step)
+        if (!split && __any(patch || fpatch)) {  // move_count > 255: crafted states only (see k_step)
             __builtin_amdgcn_s_waitcnt(0);
             if (patch) obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
             if (fpatch) fobs[(size_t)t * kObsDim + 295] = fin_moves;
@@ -1366,7 +1436,18 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
             S.flags[blk + t] = (uint8_t)o.flags;
             if (S.winner) S.winner[blk + t] = wnr;
         }
+        RSTAMP(4, k);
     }
+    if (obs_tail) store_obs_range(L, obs_tail, kObsSplit, kObsBlockWords);
+#ifdef SPL_STAMPS
+    {
+        RSTAMP(5, 0);  // kernel end for this wave (lane 0)
+        if (lane < K)
+            for (int i = 0; i < kRStamps; ++i)
+                g_rstamps[((size_t)blockIdx.x * 16 + lane) * kRStamps + i] =
+                    ((uint64_t)(uint32_t)rst_hi[i] << 32) | (uint32_t)rst_lo[i];
+    }
+#endif
     if (valid) {
         if (S.next_actions) S.next_actions[t] = action;
         store_tab(T, A, t);
@@ -1676,6 +1757,10 @@ int spl_abi_version(void) { return SPL_ABI_VERSION; }
 #ifdef SPL_STAMPS
 int spl_debug_set_stamps(void *buf) {
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)));
+    return SPL_OK;
+}
+int spl_debug_set_rollout_stamps(void *buf) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_rstamps), &buf, sizeof(buf)));
     return SPL_OK;
 }
 #endif
