@@ -81,7 +81,7 @@ __device__ uint64_t *g_stamps;
 #define STAMP(i)                                                                                 \
     do {                                                                                         \
         __builtin_amdgcn_sched_barrier(0);                                                       \
-        if (threadIdx.x == 0) g_stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
         __builtin_amdgcn_sched_barrier(0);                                                       \
     } while (0)
 // k_rollout keeps its stamps in registers (lane k holds step k's) so that stamping never waits
@@ -1155,10 +1155,12 @@ struct StepOut {
     uint64_t mask;  // info["action_mask"] after the step (before any autoreset)
 };
 
-// envs/splendor_env.py:51-90 on the table in registers.
+// envs/splendor_env.py:51-90 on the table in registers.  `known` (k_rollout after its first
+// step): `known_mask` is legal_moves of the table's current state, computed by the previous step,
+// so "any legal move?" and mask[action] need no re-evaluation.
 template <int P>
 __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepPre &pre, bool valid, const BlockLDS &L,
-                                              const KTables &Tb) {
+                                              const KTables &Tb, bool known = false, uint64_t known_mask = 0ull) {
     StepOut o{0u, 0.0f, false, 0ull};
     bool want_mask = false;
     if (valid) {
@@ -1172,8 +1174,14 @@ __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepP
             int bank[6];
             get_bank(T.sw, bank);
             // :55 mask = legal_moves(state): only "any legal?" and mask[action] are needed here
-            const bool anyl = abl(ABL_LEGAL_PRE) || any_legal(T.sw, cur, bank, L);
-            const bool ok = abl(ABL_LEGAL_PRE) || (in_range && action_legal(T.sw, cur, bank, action, L));
+            bool anyl, ok;
+            if (known) {
+                anyl = known_mask != 0ull;
+                ok = in_range && ((known_mask >> (action & 63)) & 1ull);
+            } else {
+                anyl = abl(ABL_LEGAL_PRE) || any_legal(T.sw, cur, bank, L);
+                ok = abl(ABL_LEGAL_PRE) || (in_range && action_legal(T.sw, cur, bank, action, L));
+            }
             if (!anyl) {                                          // :56-61 no legal move: draw
                 T.sw[SW_MISC] = (T.sw[SW_MISC] | ST_GAME_OVER) & 0x00FFFFFFu;
                 T.sw[SW_BANK1] &= 0xFF00FFFFu;                    // to_play = 0
@@ -1383,6 +1391,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
     // step's other outputs, the rest after the NEXT step's rules (from the same LDS rows, before
     // anything overwrites them), and the wave computes while each part drains.
     int32_t *obs_tail = nullptr;  // second part of the previous step's obs block, not yet issued
+    uint64_t cur_mask = 0ull;     // legal_moves of the current state, once a step has computed it
 #ifdef SPL_STAMPS
     int rst_lo[kRStamps] = {0}, rst_hi[kRStamps] = {0};
 #endif
@@ -1390,7 +1399,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
         wave_lds_sync();  // previous step's LDS reads done (rows, mask, frows)
         RSTAMP(0, k);
-        StepOut o = step_rules(T, action, pre, valid, L, Tb);
+        StepOut o = step_rules(T, action, pre, valid, L, Tb, k > 0, cur_mask);
         RSTAMP(1, k);
         if (obs_tail) store_obs_range(L, obs_tail, kObsSplit, kObsBlockWords);
         obs_tail = nullptr;
@@ -1411,6 +1420,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         RSTAMP(3, k);
         // the policy's next action and its prefetches go out before this step's stores
         action = sample_uniform(o.mask, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
+        cur_mask = o.mask;
         if (k + 1 < K) pre = step_prefetch(T, action, valid, A, t, Tb);
         int32_t *obs = S.obs + blk * kObsDim;
         const bool patch = valid && get_moves(T.sw) > 255;
@@ -1440,9 +1450,9 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
     }
     if (obs_tail) store_obs_range(L, obs_tail, kObsSplit, kObsBlockWords);
 #ifdef SPL_STAMPS
-    {
+    if (g_rstamps) {
         RSTAMP(5, 0);  // kernel end for this wave (lane 0)
-        if (lane < K)
+        if (lane < K && lane < 16)
             for (int i = 0; i < kRStamps; ++i)
                 g_rstamps[((size_t)blockIdx.x * 16 + lane) * kRStamps + i] =
                     ((uint64_t)(uint32_t)rst_hi[i] << 32) | (uint32_t)rst_lo[i];

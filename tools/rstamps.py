@@ -22,6 +22,9 @@ from splendor_gym.device import Engine
 T, K = 65536, 16
 e = Engine(T, 2, device="cuda:0", refill_period=0)
 e.lib.spl_debug_set_rollout_stamps.argtypes = [ctypes.c_void_p]
+e.lib.spl_debug_set_stamps.argtypes = [ctypes.c_void_p]
+step_st = torch.zeros((T // 64) * 16, dtype=torch.int64, device=e.device)  # k_step stamp points inside step_rules
+_native.check(e.lib, e.lib.spl_debug_set_stamps(step_st.data_ptr()))
 e.reset(seeds=range(T))
 buf = [torch.zeros(T, dtype=torch.int32, device=e.device) for _ in range(2)]
 e.sample_uniform(out=buf[0], seed=1, ply=0)
