@@ -1483,7 +1483,7 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
     const bool doit = valid && (mask_in == nullptr || mask_in[t] != 0);
     uint8_t *scr = &L.rows[lane * kScratchStride];
     if (doit) {
-        if (pcg_in) {  // reset(seed=...): restart this table's np_random stream, deal 2 episodes
+        if (pcg_in) {  // reset(seed=...): restart this table's np_random stream, deal every record
             Pcg64 g;
             g.s_hi = pcg_in[4 * (size_t)t];
             g.s_lo = pcg_in[4 * (size_t)t + 1];
@@ -1491,14 +1491,16 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
             g.inc_lo = pcg_in[4 * (size_t)t + 3];
             g.has32 = 0;
             g.u32 = 0;
-            Deal d0, d1;
-            const uint32_t seed0 = g.engine_seed();
-            deal_into(seed0, P, slot_rec(A, t, 0), scr, d0);
-            const uint32_t seed1 = g.engine_seed();
-            deal_into(seed1, P, slot_rec(A, t, 1), scr, d1);
+            // record 0 = this episode, records 1.. = the next episodes in stream order: the ring
+            // starts full, so refills (one deal per table per call) only have to keep pace
+            Deal d0, d;
+            deal_into(g.engine_seed(), P, slot_rec(A, t, 0), scr, d0);
+            for (int r = 1; r < kSlotRecords; ++r) {
+                deal_into(g.engine_seed(), P, slot_rec(A, t, r), scr, d);
+                if (r == 1) store_pool(A, t, d);
+            }
             store_pcg(A, t, g);
-            store_pool(A, t, d1);
-            fresh_state(T, ring_bits(0, kSlotRecords - 2), d0);  // record 0 live, 1 the next pool, the rest for refills
+            fresh_state(T, ring_bits(0, 0), d0);
         } else {       // reset() without a seed: continue the stream (pool deal)
             Deal d = pend_of(T.sw[SW_MISC]) < kSlotRecords - 1 ? load_pool(A, t) : empty_deal();
             uint32_t fl = 0;
