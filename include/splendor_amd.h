@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 1
+#define SPL_ABI_VERSION 2
 
 /* ---- per-table flag bits (uint8) --------------------------------------------------- */
 #define SPL_F_ILLEGAL 0x01        /* info["illegal_action"]      envs/splendor_env.py:64-66 */
@@ -53,6 +53,11 @@ extern "C" {
 #define SPL_F_RESET 0x20          /* autoreset: obs/mask describe the freshly dealt table   */
 #define SPL_F_RNG_LIMIT 0x40      /* a deal needed more MT outputs than the device streams; */
                                   /* never observed, reported instead of guessed */
+
+/* ---- device policies for next_actions (scripts/eval_suite.py opponents) --------------- */
+#define SPL_POLICY_UNIFORM 0         /* uniform over legal (wrappers/selfplay.py:66-73 random_opponent) */
+#define SPL_POLICY_GREEDY_V1 1       /* eval_suite.py:9-29 greedy_opponent_v1 (deterministic)        */
+#define SPL_POLICY_BASIC_PRIORITY 2  /* eval_suite.py:32-78 basic_priority_opponent                  */
 
 /* ---- error codes -------------------------------------------------------------------- */
 #define SPL_OK 0
@@ -83,8 +88,11 @@ typedef struct spl_step_args_s {
     uint8_t *flags;          /* [n]      SPL_F_* bits                                        */
     int8_t *winner;          /* [n] or NULL: winner of the state the step produced (−1 None) */
     int32_t *final_obs;      /* [n][297] or NULL: terminal obs, written on SPL_F_RESET rows  */
-    int32_t autoreset;       /* 1: terminated tables are re-dealt in the same step          */
-    int32_t *next_actions;   /* [n] or NULL: fused uniform-random policy over the new mask   */
+    int32_t autoreset;       /* 1: terminated tables are re-dealt in the same step; 2: also the
+                                tables already terminal when the step starts (no move applied:
+                                SPL_F_RESET, reward 0, final_obs row = that terminal obs)        */
+    int32_t policy;          /* next_actions policy: SPL_POLICY_* (0 = uniform random)       */
+    int32_t *next_actions;   /* [n] or NULL: fused policy's action over the new state / mask */
     const uint64_t *ply_base; /* device, nullable: added to `ply` (lets a captured graph replay) */
     uint64_t policy_seed;    /* Philox key for next_actions                                  */
     uint64_t ply;            /* Philox counter for next_actions                              */

@@ -61,6 +61,7 @@ struct KStep {
     uint64_t ply;
     int64_t table0;
     int autoreset;
+    int policy;
 };
 
 constexpr int kObsDim = 297;
@@ -1091,6 +1092,49 @@ __device__ __forceinline__ int sample_uniform(uint64_t m, uint64_t seed, uint64_
     return pos;
 }
 
+// scripts/eval_suite.py opponents over a 45-bit legal mask; their random choices are Philox
+// draws (sample_uniform over the preferred subset) where the reference calls np.random.choice.
+constexpr uint64_t kBuyBits = (((1ull << 12) - 1ull) << 15) | (7ull << 42);  // 15..26, 42..44
+constexpr uint64_t kTake2Bits = 0x1Full << 10, kTake3Bits = 0x3FFull, kReserveBits = ((1ull << 15) - 1ull) << 27;
+__device__ __forceinline__ int lowest_action(uint64_t m) { return m ? __ffsll((unsigned long long)m) - 1 : 0; }
+
+template <int P>
+__device__ __forceinline__ int policy_action(int policy, uint64_t m, const Tab<P> &T, const BlockLDS &L,
+                                             uint64_t seed, uint64_t table, uint64_t ply) {
+    if (policy == SPL_POLICY_GREEDY_V1) {  // eval_suite.py:9-29: first legal buy, take-2, take-3, reserve
+        const uint64_t pick = (m & kBuyBits) ? (m & kBuyBits)
+                              : (m & kTake2Bits) ? (m & kTake2Bits)
+                              : (m & kTake3Bits) ? (m & kTake3Bits)
+                              : (m & kReserveBits) ? (m & kReserveBits) : m;
+        return lowest_action(pick);
+    }
+    if (policy == SPL_POLICY_BASIC_PRIORITY) {  // eval_suite.py:32-78
+        const uint64_t vis = m & (((1ull << 12) - 1ull) << 15);
+        uint64_t pick;
+        if (vis) {  // visible buys with the most points (board points: obs[32 + 13k + 2])
+            int best = -1;
+            uint64_t best_set = 0;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+                const bool legal = (vis >> (15 + k)) & 1ull;
+                const int pts = (int)bget(card_rec(L, board_get(T.sw, k)).x, 2);
+                const bool better = legal && pts > best, tie = legal && pts == best;
+                best_set = better ? (1ull << (15 + k)) : (tie ? (best_set | (1ull << (15 + k))) : best_set);
+                best = better ? pts : best;
+            }
+            pick = best_set;
+        } else {
+            pick = (m & (7ull << 42)) ? (m & (7ull << 42))
+                   : (m & kTake3Bits) ? (m & kTake3Bits)
+                   : (m & kTake2Bits) ? (m & kTake2Bits)
+                   : (m & kReserveBits) ? (m & kReserveBits) : 0ull;
+            if (!pick) return lowest_action(m);
+        }
+        return sample_uniform(pick, seed, table, ply);
+    }
+    return sample_uniform(m, seed, table, ply);
+}
+
 // ------------------------------------------------------------------------------------------
 // kernels
 // ------------------------------------------------------------------------------------------
@@ -1295,19 +1339,23 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     STAMP(1);
 
     StepOut o = step_rules(T, action, pre, valid, L, Tb);
+    // autoreset 2: a table terminal on entry is re-dealt without a move (dual-step opponent phase)
+    const bool entry_reset = valid && S.autoreset == 2 && (o.flags & SPL_F_AFTER_TERMINAL);
+    if (entry_reset) o.flags = 0u;
+    const bool ended = valid && (o.term || entry_reset);
     const int8_t wnr = (int8_t)get_winner(T.sw);
     STAMP(4);
 
     // terminal observation for gymnasium's info["final_observation"], staged in LDS and stored
     // with everything else at the end
     const bool want_final = S.autoreset && S.final_obs != nullptr && !abl(ABL_FINAL);
-    const uint64_t fin = __ballot(valid && o.term && want_final);
-    if (valid && o.term && want_final) encode_row(T, &L.frows[lane * kObsDim], L);
+    const uint64_t fin = __ballot(ended && want_final);
+    if (ended && want_final) encode_row(T, &L.frows[lane * kObsDim], L);
     const int fin_moves = get_moves(T.sw);
     const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;
     STAMP(5);
     bool pool_dirty = false;
-    if (valid && o.term && S.autoreset && !abl(ABL_RESET))
+    if (ended && S.autoreset && !abl(ABL_RESET))
         autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], o, pool_dirty);
     STAMP(6);
     wave_lds_sync();  // deal scratch (rows) free again
@@ -1332,7 +1380,7 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     // move_count above 255 (crafted states only) does not fit the byte staging: patch it after
     // this wave's block stores of the same dwords have left
     const bool patch = valid && get_moves(T.sw) > 255;
-    const bool fpatch = valid && o.term && want_final && fin_moves > 255;
+    const bool fpatch = ended && want_final && fin_moves > 255;
     if (__any(patch || fpatch)) {
         __builtin_amdgcn_s_waitcnt(0);
         if (patch) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
@@ -1347,7 +1395,7 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
         }
         if (S.next_actions) {
             const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
-            S.next_actions[t] = sample_uniform(o.mask, S.policy_seed, (uint64_t)(S.table0 + t), ply);
+            S.next_actions[t] = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply);
         }
         if (!abl(ABL_TAB_STORE)) store_tab(T, A, t);
         if (pool_dirty) store_pool(A, t, pool);
@@ -1419,7 +1467,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         wave_lds_sync();
         RSTAMP(3, k);
         // the policy's next action and its prefetches go out before this step's stores
-        action = sample_uniform(o.mask, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
+        action = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
         cur_mask = o.mask;
         if (k + 1 < K) pre = step_prefetch(T, action, valid, A, t, Tb);
         int32_t *obs = S.obs + blk * kObsDim;
@@ -1912,6 +1960,8 @@ int spl_refill(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
 static int check_step_args(const spl_step_args_t *a) {
     if (!a || !a->actions || !a->obs || !a->mask || !a->reward || !a->terminated || !a->flags)
         return fail(SPL_E_ARG, "actions/obs/mask/reward/terminated/flags are required");
+    if (a->autoreset < 0 || a->autoreset > 2) return fail(SPL_E_ARG, "autoreset must be 0, 1 or 2");
+    if (a->policy < SPL_POLICY_UNIFORM || a->policy > SPL_POLICY_BASIC_PRIORITY) return fail(SPL_E_ARG, "unknown policy");
     if (((uintptr_t)a->obs & 15u) || (a->final_obs && ((uintptr_t)a->final_obs & 3u)))
         return fail(SPL_E_ARG, "obs must be 16-byte aligned");
     if ((uintptr_t)a->mask & 3u) return fail(SPL_E_ARG, "mask must be 4-byte aligned");
@@ -1936,6 +1986,7 @@ static KStep kstep(const spl_step_args_t *a) {
     S.ply = a->ply;
     S.table0 = a->table0;
     S.autoreset = a->autoreset;
+    S.policy = a->policy;
     return S;
 }
 

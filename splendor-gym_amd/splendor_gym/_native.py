@@ -10,9 +10,10 @@ import os
 import numpy as np
 
 LIB_NAME = "libsplendor_amd.so"
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # per-table flag bits (include/splendor_amd.h)
+POLICY_UNIFORM, POLICY_GREEDY_V1, POLICY_BASIC_PRIORITY = 0, 1, 2  # SPL_POLICY_* (device next_actions)
 F_ILLEGAL, F_DRAW, F_TURN_LIMIT = 0x01, 0x02, 0x04
 F_AFTER_TERMINAL, F_OOB, F_RESET, F_RNG_LIMIT = 0x08, 0x10, 0x20, 0x40
 
@@ -32,7 +33,7 @@ class StepArgs(ctypes.Structure):
     """spl_step_args_t"""
     _fields_ = [("actions", c_void_p), ("obs", c_void_p), ("mask", c_void_p), ("reward", c_void_p),
                 ("terminated", c_void_p), ("flags", c_void_p), ("winner", c_void_p),
-                ("final_obs", c_void_p), ("autoreset", c_int32), ("next_actions", c_void_p),
+                ("final_obs", c_void_p), ("autoreset", c_int32), ("policy", c_int32), ("next_actions", c_void_p),
                 ("ply_base", c_void_p), ("policy_seed", c_uint64), ("ply", c_uint64), ("table0", c_int64),
                 ("ep_return", c_void_p), ("ep_count", c_void_p)]
 

@@ -105,8 +105,11 @@ class Engine:
         return self.obs, self.mask
 
     def step(self, actions=None, autoreset=True, final_obs=True, next_actions=None, policy_seed=0, ply=0,
-             ep_return=None, ep_count=None, ply_base=None):
-        """One env step on every table (SplendorEnv.step semantics per table)."""
+             ep_return=None, ep_count=None, ply_base=None, policy=0):
+        """One env step on every table (SplendorEnv.step semantics per table).  autoreset: False,
+        True (same-step autoreset) or 2 (also re-deal tables terminal on entry, without a move).
+        next_actions (optional int32 tensor) receives `policy`'s action (_native.POLICY_*) over
+        the new state."""
         torch = self.torch
         if actions is None:
             actions = self.actions
@@ -119,7 +122,7 @@ class Engine:
                      reward=self.reward.data_ptr(), terminated=self.terminated.data_ptr(),
                      flags=self.flags.data_ptr(), winner=self.winner.data_ptr(),
                      final_obs=self.final_obs.data_ptr() if (final_obs and autoreset) else None,
-                     autoreset=1 if autoreset else 0,
+                     autoreset=(2 if autoreset == 2 else 1) if autoreset else 0, policy=int(policy),
                      next_actions=None if next_actions is None else next_actions.data_ptr(),
                      ply_base=None if ply_base is None else ply_base.data_ptr(),
                      policy_seed=int(policy_seed) & (2**64 - 1), ply=int(ply) & (2**64 - 1), table0=self.table0,
@@ -131,7 +134,7 @@ class Engine:
         return self.obs, self.mask, self.reward, self.terminated, self.flags
 
     def rollout(self, steps, actions=None, next_actions=None, policy_seed=0, ply=0, out=None, final_obs=True,
-                ep_return=None, ep_count=None, ply_base=None):
+                ep_return=None, ep_count=None, ply_base=None, policy=0):
         """`steps` env steps of every table under the device uniform-random policy in one launch
         (spl_rollout): the same trajectory as `steps` calls of step() with next_actions fed back
         and ply, ply+1, ...  out=None overwrites self.obs/mask/... each step; otherwise `out` is a
@@ -154,7 +157,7 @@ class Engine:
         a = StepArgs(actions=actions.data_ptr(), obs=bufs["obs"].data_ptr(), mask=bufs["mask"].data_ptr(),
                      reward=bufs["reward"].data_ptr(), terminated=bufs["terminated"].data_ptr(),
                      flags=bufs["flags"].data_ptr(), winner=ptr(bufs.get("winner")),
-                     final_obs=ptr(bufs.get("final_obs")) if final_obs else None, autoreset=1,
+                     final_obs=ptr(bufs.get("final_obs")) if final_obs else None, autoreset=1, policy=int(policy),
                      next_actions=None if next_actions is None else next_actions.data_ptr(),
                      ply_base=None if ply_base is None else ply_base.data_ptr(),
                      policy_seed=int(policy_seed) & (2**64 - 1), ply=int(ply) & (2**64 - 1), table0=self.table0,

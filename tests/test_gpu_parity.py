@@ -254,3 +254,41 @@ def test_rollout_equals_step_chain(P):
     for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
         assert torch.equal(getattr(chain, name), getattr(fused, name)), name
     assert torch.equal(a_c, na_f)
+
+
+def test_dual_step_vector_env_matches_per_env_wrappers():
+    """DualStepVectorEnv (fused device greedy_v1 opponent) == per-env DualStepNativeWrapper over
+    SplendorEnv with the host greedy_opponent_v1, including the PPO loop's reset after done."""
+    import torch
+    from splendor_gym.envs import SplendorEnv
+    from splendor_gym.opponents import greedy_opponent_v1
+    from splendor_gym.selfplay import DualStepVectorEnv
+    from splendor_gym.wrappers import DualStepNativeWrapper
+    n, steps, seed = 6, 150, 40
+    vec = DualStepVectorEnv(n, opponent="greedy_v1")
+    obs_v, info_v = vec.reset(seed=seed)
+    envs = [DualStepNativeWrapper(SplendorEnv(), opponent_policy=greedy_opponent_v1, random_starts=False)
+            for _ in range(n)]
+    per = [w.reset(seed=seed + i) for i, w in enumerate(envs)]
+    rs = np.random.default_rng(3)
+    ended = 0
+    for k in range(steps):
+        acts = []
+        for i in range(n):
+            legal = np.flatnonzero(per[i][1]["action_mask"])
+            acts.append(int(rs.choice(legal)) if len(legal) else 0)
+        assert np.array_equal(info_v["action_mask"].cpu().numpy(), np.stack([p[1]["action_mask"] for p in per]))
+        ao, ar, oo, orr, done, info_v = vec.dual_step(torch.tensor(acts, dtype=torch.int32, device=vec.device))
+        for i, w in enumerate(envs):
+            a_obs, a_rew, o_obs, o_rew, d, inf = w.dual_step(acts[i])
+            assert bool(done[i]) == bool(d), (k, i)
+            assert float(ar[i]) == pytest.approx(a_rew) and float(orr[i]) == pytest.approx(o_rew), (k, i)
+            assert np.array_equal(oo[i].cpu().numpy(), o_obs), (k, i)  # post-turn (final) observation
+            if d:
+                ended += 1
+                assert np.array_equal(info_v["final_observation"][i].cpu().numpy(), a_obs)
+                per[i] = w.reset()  # ppo_splendor.py:246-256
+            else:
+                per[i] = (a_obs, inf)
+            assert np.array_equal(ao[i].cpu().numpy(), per[i][0]), (k, i)
+    assert ended >= n  # every table finished at least one game and was re-dealt
