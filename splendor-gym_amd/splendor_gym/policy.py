@@ -13,10 +13,11 @@ from .engine.encode import OBSERVATION_DIM, TOTAL_ACTIONS
 
 def masked_categorical(logits: torch.Tensor, mask: torch.Tensor) -> Categorical:
     """Categorical over the legal actions; rows without a legal action keep their raw logits
-    (the env reports the no-legal-move draw itself) (ppo_splendor.py:27-37)."""
+    (the env reports the no-legal-move draw itself) (ppo_splendor.py:27-37).  Argument validation
+    is off: it reads values back to the host, which a captured HIP graph cannot do."""
     illegal = mask < 0.5
     any_legal = (~illegal).any(dim=1, keepdim=True)
-    return Categorical(logits=logits.masked_fill(illegal & any_legal, float("-inf")))
+    return Categorical(logits=logits.masked_fill(illegal & any_legal, float("-inf")), validate_args=False)
 
 
 class ActorCritic(nn.Module):

@@ -53,11 +53,12 @@ class DualStepVectorEnv:
         self._ply = 0
 
     # ------------------------------------------------------------------------------------
-    def reset(self, seed=None):
-        """Deal every table (env i seeded with seed + i; None continues each table's stream).
-        A fresh deal has player 0 to play, so the reference's opening loop never moves the
-        opponent here (dual_step_native.py:60-77)."""
-        seeds = None if seed is None else range(int(seed), int(seed) + self.num_envs)
+    def reset(self, seed=None, seeds=None):
+        """Deal every table (env i seeded with seed + i, or seeds[i]; neither: continue each
+        table's stream).  A fresh deal has player 0 to play, so the reference's opening loop never
+        moves the opponent here (dual_step_native.py:60-77)."""
+        if seeds is None and seed is not None:
+            seeds = range(int(seed), int(seed) + self.num_envs)
         obs, mask = self.eng.reset(seeds=seeds)
         return obs, {"action_mask": mask, "to_play": obs[:, 294]}
 

@@ -292,3 +292,20 @@ def test_dual_step_vector_env_matches_per_env_wrappers():
                 per[i] = (a_obs, inf)
             assert np.array_equal(ao[i].cpu().numpy(), per[i][0]), (k, i)
     assert ended >= n  # every table finished at least one game and was re-dealt
+
+
+def test_batched_eval_matches_reference_eval_suite():
+    """splendor_gym.evaluation.eval_vs_opponent == the reference eval_suite.eval_vs_opponent
+    (tests/golden/eval.json) for deterministic agents against greedy_opponent_v1."""
+    from splendor_gym.evaluation import eval_vs_opponent, first_legal_policy, last_legal_policy
+    with open(os.path.join(GOLD, "eval.json")) as f:
+        cases = json.load(f)
+    agents = {"first_legal": first_legal_policy, "last_legal": last_legal_policy}
+    for c in cases:
+        got = eval_vs_opponent(agents[c["agent"]], opponent=c["opponent"], n_games=c["n_games"], seed=c["seed"])
+        assert got.pop("unfinished") == 0
+        want = c["result"]
+        for k in ("n", "wins", "losses", "draws"):
+            assert got[k] == want[k], (c["agent"], c["seed"], k, got, want)
+        for k in ("win_rate", "win_rate_ci95", "avg_turns", "avg_prestige", "illegal_action_rate"):
+            assert got[k] == pytest.approx(want[k], abs=1e-12), (c["agent"], c["seed"], k, got, want)

@@ -1,0 +1,108 @@
+"""BASELINE config 5: 2-player self-play with the PPO actor on device (ppo_splendor.py:227-269).
+
+    python tools/bench_selfplay.py [--tables 65536] [--iters 64] [--warmup 16] [--bf16]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 tools/bench_selfplay.py ...
+
+One iteration = the PPO rollout step for every table: the agent's ActorCritic forward
+(get_action_and_value: actor + critic + masked categorical sample) on the current observations,
+then DualStepVectorEnv.dual_step (agent move, the opponent's greedy reply from a frozen
+ActorCritic — eval_suite.py:131-141 — and the reset of finished tables).  A dual step is 2
+env-steps.  Weights are random-initialised (no checkpoint travels); compute is
+fp32 like the reference unless --bf16.  Prints one JSON line on rank 0 (weak scaling: tables per
+GPU fixed, max-over-ranks time), plus the env-only share measured with the actor forward removed.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "splendor-gym_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tables", type=int, default=65536)
+    ap.add_argument("--iters", type=int, default=64)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--bf16", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    from splendor_gym.parallel import barrier, init_distributed, max_over_ranks
+    from splendor_gym.policy import ActorCritic, greedy_opponent_from
+    from splendor_gym.selfplay import DualStepVectorEnv
+
+    rank, world, local = init_distributed()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(1234 + rank)
+    N = args.tables
+    agent = ActorCritic().to(dev).eval()
+    opp_model = ActorCritic().to(dev).eval()
+    env = DualStepVectorEnv(N, device=dev, opponent=greedy_opponent_from(opp_model), table0=rank * N,
+                            opponent_obs=False)
+    obs, info = env.reset(seed=rank * N)
+    mask = info["action_mask"]
+    amp = torch.autocast("cuda", dtype=torch.bfloat16) if args.bf16 else torch.autocast("cuda", enabled=False)
+
+    def iteration(with_actor=True):
+        with torch.no_grad(), amp:
+            if with_actor:
+                action, logprob, _, value = agent.get_action_and_value(obs.float(), mask.float())
+                a = action.to(torch.int32)
+            else:
+                a = env.eng.sample_uniform(mask=mask, out=env.opp_actions.clone(), seed=7, ply=0)
+            return env.dual_step(a)
+
+    for _ in range(args.warmup):
+        iteration()
+    graph = None
+    if not args.no_graph:
+        try:
+            torch.cuda.synchronize(dev)
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    iteration()
+            torch.cuda.current_stream(dev).wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                iteration()
+        except Exception as exc:  # capture unsupported: eager
+            print(f"graph capture failed ({exc}); timing eager iterations", file=sys.stderr)
+            graph = None
+
+    def timed(fn, iters):
+        barrier(dev)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize(dev)
+        barrier(dev)
+        return max_over_ranks(time.perf_counter() - t0, device=dev)
+
+    full = timed(graph.replay if graph is not None else iteration, args.iters)
+    env_only = timed(lambda: iteration(with_actor=False), args.iters)
+    if rank == 0:
+        steps = 2 * N * world * args.iters
+        print(json.dumps({
+            "metric": f"env-steps/sec (whole node), 2p self-play with on-device ActorCritic actor, {N} tables/GPU",
+            "value": round(steps / full, 1), "unit": "env-steps/s", "n_gpus": world, "iters": args.iters,
+            "ms_per_dual_step": round(full / args.iters * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "dtype": "bf16" if args.bf16 else "fp32", "data": "synthetic: seeded deals, random-init ActorCritic",
+            "config": {"workload": "PPO rollout step: ActorCritic.get_action_and_value + DualStepVectorEnv.dual_step "
+                                   "(greedy frozen-ActorCritic opponent, reset after done)",
+                       "tables_per_gpu": N, "players": 2, "launch": "hipGraph replay" if graph is not None else "eager"},
+            "env_only": {"value": round(steps / env_only, 1), "ms_per_dual_step": round(env_only / args.iters * 1e3, 4),
+                         "note": "same loop with the agent's forward replaced by device uniform sampling (eager)"},
+        }))
+    env.close()
+
+
+if __name__ == "__main__":
+    main()
