@@ -122,12 +122,12 @@ def main():
     import torch
     from splendor_gym import _native
     from splendor_gym.device import Engine
-    from splendor_gym.parallel import barrier, gather_returns, init_distributed, max_over_ranks
+    from splendor_gym.parallel import barrier, gather_returns, init_distributed, local_device, max_over_ranks
 
     rank, world, local = init_distributed()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    dev = torch.device("cuda", local)
+    dev = local_device(local)
     torch.cuda.set_device(dev)
     T, P = args.tables, args.players
     table0 = rank * T

@@ -22,7 +22,9 @@ def shard_range(n_global, rank, world):
 
 def init_distributed(backend=None):
     """Initialise the default process group from torchrun's env (RANK, WORLD_SIZE, LOCAL_RANK,
-    MASTER_ADDR/PORT).  Returns (rank, world, local_rank); (0, 1, 0) without a launcher."""
+    MASTER_ADDR/PORT).  Returns (rank, world, local_rank); (0, 1, 0) without a launcher.
+    Backend: `backend`, else $SPLENDOR_DIST_BACKEND, else nccl (RCCL) with GPUs, gloo without.
+    gloo with GPUs rehearses several ranks on one card (local_device maps ranks onto the cards)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -30,13 +32,24 @@ def init_distributed(backend=None):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("SPLENDOR_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         kw = {}
         if backend == "nccl":
             torch.cuda.set_device(local)
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     return rank, world, local
+
+
+def local_device(local):
+    """The GPU of local rank `local`: one per rank on a full node; ranks share cards when there
+    are more ranks than cards (gloo rehearsal)."""
+    return torch.device("cuda", local % max(1, torch.cuda.device_count()))
+
+
+def _host_collectives():
+    """gloo collectives run on host tensors here (its CUDA support is partial)."""
+    return dist.get_backend() == "gloo"
 
 
 def gather_returns(ep_return, ep_count, n_global=None):
@@ -46,6 +59,9 @@ def gather_returns(ep_return, ep_count, n_global=None):
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return ep_return.clone(), ep_count.clone()
     world = dist.get_world_size()
+    if _host_collectives():
+        ret, cnt = gather_returns_host(ep_return.cpu(), ep_count.cpu(), n_global)
+        return ret.to(ep_return.device), cnt.to(ep_count.device)
     n_local = torch.tensor([ep_return.numel()], dtype=torch.int64, device=ep_return.device)
     sizes = [torch.zeros_like(n_local) for _ in range(world)]
     dist.all_gather(sizes, n_local)
@@ -64,18 +80,36 @@ def gather_returns(ep_return, ep_count, n_global=None):
     return ret.to(torch.float32), cnt.to(torch.int64)
 
 
+def gather_returns_host(ep_return, ep_count, n_global=None):
+    """gather_returns on host tensors (gloo): same padding and layout."""
+    world = dist.get_world_size()
+    sizes = [None] * world
+    dist.all_gather_object(sizes, int(ep_return.numel()))
+    width = max(sizes)
+    packed = torch.zeros((2, width), dtype=torch.float64)
+    packed[0, :ep_return.numel()] = ep_return.to(torch.float64)
+    packed[1, :ep_count.numel()] = ep_count.to(torch.float64)
+    parts = [torch.empty_like(packed) for _ in range(world)]
+    dist.all_gather(parts, packed)
+    ret = torch.cat([parts[r][0, :sizes[r]] for r in range(world)])
+    cnt = torch.cat([parts[r][1, :sizes[r]] for r in range(world)])
+    if n_global is not None and ret.numel() != n_global:
+        raise RuntimeError(f"gathered {ret.numel()} tables, expected {n_global}")
+    return ret.to(torch.float32), cnt.to(torch.int64)
+
+
 def max_over_ranks(value, device=None):
     """Max of a host float over all ranks (the bench's slowest-rank time)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=None if _host_collectives() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def barrier(device=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        if device is not None and device.type == "cuda":
+        if device is not None and device.type == "cuda" and not _host_collectives():
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()

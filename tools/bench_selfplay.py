@@ -31,12 +31,12 @@ def main():
     args = ap.parse_args()
 
     import torch
-    from splendor_gym.parallel import barrier, init_distributed, max_over_ranks
+    from splendor_gym.parallel import barrier, init_distributed, local_device, max_over_ranks
     from splendor_gym.policy import ActorCritic, greedy_opponent_from
     from splendor_gym.selfplay import DualStepVectorEnv
 
     rank, world, local = init_distributed()
-    dev = torch.device("cuda", local)
+    dev = local_device(local)
     torch.cuda.set_device(dev)
     torch.manual_seed(1234 + rank)
     N = args.tables
