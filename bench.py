@@ -12,7 +12,7 @@ write the same per-step outputs (tests/test_gpu_parity.py::test_rollout_equals_s
                   and each step's stores drain while the next step computes
   --mode step     one spl_step launch per env step (the drop-in SplendorEnv.step path);
                   the mode not selected is measured too and reported as "other_mode"
-plus a pool refill every 64 steps.  Inputs are resident in HBM before the timed region; the
+plus a pool refill every 64 steps (2p; 32 at 3p, 16 at 4p).  Inputs are resident in HBM before the timed region; the
 timed region replays captured HIP graphs of 64 steps.
 
 Weak scaling: each rank owns `--tables` tables (global ids rank*T ...), no collective in the
@@ -38,7 +38,9 @@ for _p in (REPO, os.path.join(REPO, "splendor-gym_amd")):
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 ALGO_BYTES = {2: 1370, 3: 1408, 4: 1446}  # 2*S_P + 297*4 + 45 + 4 + 4 + 1 (3p interpolated)
-REFILL_EVERY = 64  # pool refill period: three pool records per table cover three resets in between
+# pool refill period per player count: three pool deals per table must cover the resets between
+# refills (random games last ~77 plies at 2p, ~29 at 4p)
+REFILL_EVERY = {2: 64, 3: 32, 4: 16}
 ROLLOUT_K = 16     # env steps per spl_rollout launch
 
 
@@ -152,7 +154,7 @@ def main():
     step_args = [mkargs(buf[0], buf[1]), mkargs(buf[1], buf[0])]
     ctx, desc = eng.ctx, ctypes.byref(eng.desc)
     stream = eng.stream()
-    R = REFILL_EVERY
+    R = REFILL_EVERY[P]
 
     def run(mode, k0, k1, strm, ev=None):
         """Steps k0..k1-1 (ply k+1 relative to ply_base), refill every R steps.  mode "step":

@@ -21,7 +21,11 @@ class Engine:
     so results do not depend on how tables are split across GPUs.
     """
 
-    def __init__(self, num_tables, num_players=2, device=None, refill_period=64, table0=0):
+    # pool refill period by player count (three pool deals per table cover the resets in between;
+    # random games last ~77 plies at 2p, ~29 at 4p)
+    DEFAULT_REFILL = {2: 64, 3: 32, 4: 16}
+
+    def __init__(self, num_tables, num_players=2, device=None, refill_period=None, table0=0):
         torch = _native.require_gpu()
         self.torch = torch
         self.lib = _native.load_library()
@@ -39,6 +43,8 @@ class Engine:
             check(self.lib, self.lib.spl_ctx_create(self.device.index, cards.ctypes.data, nobles.ctypes.data,
                                                     ctypes.byref(ctx)))
         self.ctx = ctx
+        if refill_period is None:
+            refill_period = self.DEFAULT_REFILL.get(int(num_players), 16)
         check(self.lib, self.lib.spl_ctx_set_refill_period(self.ctx, int(refill_period)))
         nbytes = int(self.lib.spl_arena_bytes(self.n, self.P))
         dev = self.device

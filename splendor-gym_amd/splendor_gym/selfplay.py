@@ -36,7 +36,7 @@ _DEVICE_POLICIES = {"random": _native.POLICY_UNIFORM, "greedy_v1": _native.POLIC
 
 
 class DualStepVectorEnv:
-    def __init__(self, num_envs, device=None, opponent="random", policy_seed=0, refill_period=64, table0=0,
+    def __init__(self, num_envs, device=None, opponent="random", policy_seed=0, refill_period=None, table0=0,
                  opponent_obs=True):
         if isinstance(opponent, str) and opponent not in _DEVICE_POLICIES:
             raise ValueError(f"unknown device opponent {opponent!r}; choose {sorted(_DEVICE_POLICIES)} or a callable")

@@ -25,7 +25,7 @@ from .seeding import vector_seeds
 class SplendorVectorEnv:
     metadata = {"render_modes": [], "autoreset_mode": "same-step"}
 
-    def __init__(self, num_envs, num_players=2, device=None, autoreset=True, refill_period=64, table0=0,
+    def __init__(self, num_envs, num_players=2, device=None, autoreset=True, refill_period=None, table0=0,
                  to_numpy=False):
         self.num_envs = int(num_envs)
         self.num_players = int(num_players)

@@ -309,3 +309,39 @@ def test_batched_eval_matches_reference_eval_suite():
             assert got[k] == want[k], (c["agent"], c["seed"], k, got, want)
         for k in ("win_rate", "win_rate_ci95", "avg_turns", "avg_prestige", "illegal_action_rate"):
             assert got[k] == pytest.approx(want[k], abs=1e-12), (c["agent"], c["seed"], k, got, want)
+
+
+@pytest.mark.parametrize("policy", [1, 2])
+def test_device_scripted_policies(orc, policy):
+    """SPL_POLICY_GREEDY_V1 equals the host greedy_opponent_v1 on every table; every
+    SPL_POLICY_BASIC_PRIORITY choice lies in the reference's preferred set (its random tie-breaks
+    are Philox draws, eval_suite.py:32-78)."""
+    import torch
+    from splendor_gym.opponents import greedy_opponent_v1
+    n = 2048
+    e = engine(n, 2)
+    e.reset(seeds=range(100, 100 + n))
+    a = torch.zeros(n, dtype=torch.int32, device=e.device)
+    nxt = torch.zeros_like(a)
+    e.sample_uniform(out=a, seed=9, ply=0)
+    for k in range(60):
+        e.step(a, next_actions=nxt, policy=policy, policy_seed=9, ply=k + 1)
+        obs, mask, got = e.obs.cpu().numpy(), e.mask.cpu().numpy(), nxt.cpu().numpy()
+        for i in range(0, n, 7):
+            info = {"action_mask": mask[i]}
+            legal = np.flatnonzero(mask[i])
+            if policy == 1:
+                assert got[i] == greedy_opponent_v1(obs[i], info), (k, i)
+                continue
+            if len(legal) == 0:
+                assert got[i] == 0
+                continue
+            vis = legal[(legal >= 15) & (legal <= 26)]
+            if len(vis):
+                pts = np.array([obs[i][32 + (x - 15) * 13 + 2] for x in vis])
+                allowed = vis[pts == pts.max()]
+            else:
+                allowed = next(legal[(legal >= lo) & (legal <= hi)] for lo, hi in ((42, 44), (0, 9), (10, 14), (27, 41), (0, 44))
+                               if len(legal[(legal >= lo) & (legal <= hi)]))
+            assert got[i] in allowed, (k, i, got[i], allowed)
+        e.sample_uniform(out=a, seed=11, ply=k)  # keep the tables moving with uniform play
