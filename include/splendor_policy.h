@@ -1,0 +1,71 @@
+/*
+ * splendor_policy.h — C-ABI of the fused ActorCritic forward for batched self-play (gfx950).
+ *
+ * The reference runs its PPO actor as torch modules on one observation at a time
+ * (ppo_splendor.py:40-59 ActorCritic; :235-269 the rollout loop calls
+ * agent.get_action_and_value per step and the opponent's frozen actor per env), with
+ * masked_categorical (ppo_splendor.py:27-37) for sampling and the greedy masked argmax of
+ * training_utils.py:263-276 frozen_policy_from / scripts/eval_suite.py model_greedy_policy_from
+ * for opponents.  These entry points evaluate that network for a whole batch of tables in one
+ * launch: observations (int32 [n][297]) and masks (int8 [n][45]) straight from the engine, bf16
+ * MFMA (v_mfma_f32_32x32x16_bf16) with fp32 accumulation, tanh / softmax / sampling fused.
+ *
+ *   spl_policy_bytes   size of a packed weight image (actor only, or actor + critic)
+ *   spl_policy_pack    nn.Linear fp32 weights [out][in] + biases -> packed bf16 image (device)
+ *   spl_policy_act     ActorCritic.get_action_and_value (SAMPLE) or the greedy masked argmax
+ *                      (GREEDY) for n tables
+ *
+ * Conventions as in splendor_amd.h: caller-owned device buffers as raw pointers, `stream` a
+ * hipStream_t as void*, 0 / negative SPL_E_* returns, spl_last_error() for the message.
+ */
+#ifndef SPLENDOR_POLICY_H
+#define SPLENDOR_POLICY_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPL_POLICY_ABI 1
+
+/* one nn.Sequential(Linear(297,256), Tanh, Linear(256,256), Tanh, Linear(256,out)):
+ * weights row-major [out][in] (torch's nn.Linear.weight), biases [out], fp32, device memory */
+typedef struct {
+    const float *w1, *b1; /* [256][297], [256] */
+    const float *w2, *b2; /* [256][256], [256] */
+    const float *w3, *b3; /* [out][256], [out]: out = 45 (actor) or 1 (critic) */
+} spl_mlp_t;
+
+#define SPL_ACT_SAMPLE 0 /* masked categorical sample + log_prob + entropy (+ critic value)     */
+#define SPL_ACT_GREEDY 1 /* argmax of the actor logits with illegal actions at -inf (first max)  */
+
+typedef struct {
+    const int32_t *obs;  /* [n][297] int32, 16-byte aligned                                       */
+    const int8_t *mask;  /* [n][45] int8 (nonzero = legal), 4-byte aligned                        */
+    int32_t *action;     /* [n] out                                                               */
+    float *logprob;      /* [n] out (SAMPLE; may be NULL)                                         */
+    float *entropy;      /* [n] out, per table (SAMPLE; may be NULL; the reference reports mean)  */
+    float *value;        /* [n] out: critic(x) (SAMPLE; NULL skips the critic network)            */
+    float *logits;       /* [n][45] out: raw actor logits before masking (may be NULL)            */
+    uint64_t seed;       /* SAMPLE: Philox key; draw for table t at ply p = f(seed; table0+t, p)  */
+    uint64_t ply;
+    int64_t table0;
+    int32_t mode;        /* SPL_ACT_*                                                            */
+    int32_t reserved;
+} spl_act_args_t;
+
+/* bytes of a packed image: with_critic 0 = actor only (greedy opponents), 1 = actor + critic */
+int64_t spl_policy_bytes(int32_t with_critic);
+/* pack `actor` (and `critic` unless NULL) into `packed` (spl_policy_bytes(critic != NULL) bytes,
+ * 256-byte aligned device memory); asynchronous on `stream` */
+int spl_policy_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream);
+/* evaluate the packed network on n tables; SAMPLE with args->value != NULL needs a packed image
+ * that holds the critic */
+int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const spl_act_args_t *args,
+                   void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPLENDOR_POLICY_H */

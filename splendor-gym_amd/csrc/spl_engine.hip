@@ -1772,10 +1772,12 @@ struct spl_ctx_s {
 
 static thread_local std::string g_err;
 
-static int fail(int code, const std::string &msg) {
+// shared with spl_policy.hip
+int spl_fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
 }
+static inline int fail(int code, const std::string &msg) { return spl_fail(code, msg); }
 
 #define HIP_TRY(expr)                                                                   \
     do {                                                                                \

@@ -38,6 +38,22 @@ class StepArgs(ctypes.Structure):
                 ("ep_return", c_void_p), ("ep_count", c_void_p)]
 
 
+class MlpDesc(ctypes.Structure):
+    """spl_mlp_t (include/splendor_policy.h)"""
+    _fields_ = [("w1", c_void_p), ("b1", c_void_p), ("w2", c_void_p), ("b2", c_void_p), ("w3", c_void_p),
+                ("b3", c_void_p)]
+
+
+class ActArgs(ctypes.Structure):
+    """spl_act_args_t (include/splendor_policy.h)"""
+    _fields_ = [("obs", c_void_p), ("mask", c_void_p), ("action", c_void_p), ("logprob", c_void_p),
+                ("entropy", c_void_p), ("value", c_void_p), ("logits", c_void_p), ("seed", c_uint64),
+                ("ply", c_uint64), ("table0", c_int64), ("mode", c_int32), ("reserved", c_int32)]
+
+
+ACT_SAMPLE, ACT_GREEDY = 0, 1  # SPL_ACT_*
+
+
 # spl_table_t (include/splendor_table.h) as a numpy structured dtype
 PLAYER_DTYPE = np.dtype([("tokens", "<i4", 6), ("bonuses", "<i4", 5), ("prestige", "<i4"),
                          ("n_reserved", "<i4"), ("reserved", "<i4", 3), ("revealed", "<i4", 3),
@@ -72,6 +88,10 @@ SIGNATURES = {
                            c_int32),
     "spl_table_upload": ([c_void_p, ctypes.POINTER(ArenaDesc), c_int32, c_int32, c_void_p, c_void_p],
                          c_int32),
+    # include/splendor_policy.h
+    "spl_policy_bytes": ([c_int32], c_int64),
+    "spl_policy_pack": ([ctypes.POINTER(MlpDesc), ctypes.POINTER(MlpDesc), c_void_p, c_void_p], c_int32),
+    "spl_policy_act": ([c_void_p, c_int64, c_int32, ctypes.POINTER(ActArgs), c_void_p], c_int32),
 }
 
 

@@ -1,0 +1,152 @@
+"""Fused ActorCritic forward (include/splendor_policy.h) against the torch fp32 module it replaces
+(ppo_splendor.py:27-59 ActorCritic / masked_categorical; training_utils.py:263-276 greedy).
+
+Tolerances (bf16 MFMA, fp32 accumulation):
+  * against a torch model of the SAME bf16 roundings (inputs, weights and hidden activations
+    rounded to bf16, fp32 sums): |logit - ref| <= 2e-2, |value - ref| <= 2e-2 — what is left is
+    summation order, the tanh formulation and the odd one-ulp bf16 flip of a hidden unit;
+  * against the plain fp32 module: |logit - ref| <= 0.15 (bf16 weights and activations);
+  * greedy actions equal torch's argmax wherever the top two legal logits of the bf16-rounded
+    reference are more than 0.05 apart.
+Sampling is checked for legality, determinism and, on one state replicated over 65 536 tables,
+frequencies against the softmax to 4 standard errors."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def states(n, seed=5, plies=12):
+    """Engine observations/masks after a few random plies (varied, realistic inputs)."""
+    import torch
+    from splendor_gym.device import Engine
+    e = Engine(n, 2)
+    e.reset(seeds=range(seed, seed + n))
+    a = torch.zeros(n, dtype=torch.int32, device=e.device)
+    e.sample_uniform(out=a, seed=seed, ply=0)
+    for k in range(plies):
+        e.step(a, next_actions=a, policy_seed=seed, ply=k + 1)
+    return e, e.obs.clone(), e.mask.clone()
+
+
+def model(seed=0, device="cuda"):
+    import torch
+    from splendor_gym.policy import ActorCritic
+    torch.manual_seed(seed)
+    return ActorCritic().to(device).eval()
+
+
+def bf16_ref(seq, x):
+    """The fp32 module with bf16-rounded inputs, weights and hidden activations."""
+    import torch
+    r = lambda t: t.to(torch.bfloat16).float()
+    lin = [m for m in seq if isinstance(m, torch.nn.Linear)]
+    h = r(x.float())
+    for i, m in enumerate(lin):
+        h = h @ r(m.weight).T + m.bias
+        if i < 2:
+            h = r(torch.tanh(h))
+    return h
+
+
+@pytest.mark.parametrize("n", [1, 33, 1000, 8192])
+def test_greedy_logits_match_torch(n):
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic
+    _, obs, mask = states(max(n, 64))
+    obs, mask = obs[:n].contiguous(), mask[:n].contiguous()
+    m = model(1)
+    f = FusedActorCritic(m, with_critic=False)
+    act, logits = f.greedy(obs, mask, want_logits=True)
+    with torch.no_grad():
+        ref16 = bf16_ref(m.actor, obs)
+        ref32 = m.actor(obs.float())
+    assert (logits - ref16).abs().max().item() <= 2e-2
+    assert (logits - ref32).abs().max().item() <= 0.15
+    masked = ref16.masked_fill(mask < 1, float("-inf"))
+    want = torch.argmax(masked, dim=-1).to(torch.int32)
+    top2 = torch.topk(masked, 2, dim=-1).values
+    clear = (top2[:, 0] - top2[:, 1] > 0.05) | ~torch.isfinite(top2[:, 1])
+    assert torch.equal(act[clear], want[clear])
+    none = mask.sum(dim=1) == 0
+    assert (act[none] == 0).all()
+
+
+def test_full_image_serves_greedy_and_sample():
+    """An actor+critic image answers GREEDY (actor part) and SAMPLE (both nets)."""
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic
+    _, obs, mask = states(4096, seed=11)
+    m = model(2)
+    full = FusedActorCritic(m, with_critic=True)
+    actor_only = FusedActorCritic(m, with_critic=False)
+    g1, l1 = full.greedy(obs, mask, want_logits=True)
+    g2, l2 = actor_only.greedy(obs, mask, want_logits=True)
+    assert torch.equal(g1, g2) and torch.equal(l1, l2)
+    action, logprob, entropy, value, logits = full.act(obs, mask, seed=3, ply=1, want_logits=True)
+    assert torch.equal(logits, l1)
+    with torch.no_grad():
+        vref = bf16_ref(m.critic, obs)
+        vref32 = m.critic(obs.float())
+    assert value.shape == (4096, 1)
+    assert (value - vref).abs().max().item() <= 2e-2
+    assert (value - vref32).abs().max().item() <= 0.15
+    # log_prob / entropy of torch's Categorical over the kernel's own logits
+    from splendor_gym.policy import masked_categorical
+    dist = masked_categorical(logits, mask.float())
+    assert torch.allclose(logprob, dist.log_prob(action.long()), atol=1e-4, rtol=1e-4)
+    assert torch.allclose(entropy, dist.entropy(), atol=1e-4, rtol=1e-4)
+    legal_any = mask.sum(dim=1) > 0
+    assert (mask[legal_any].gather(1, action[legal_any].long()[:, None]) != 0).all()
+
+
+def test_sample_determinism_and_no_legal_rows():
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic
+    _, obs, mask = states(2048, seed=21)
+    mask = mask.clone()
+    mask[::17] = 0  # rows without a legal action sample from the raw logits
+    f = FusedActorCritic(model(3))
+    a1 = f.act(obs, mask, seed=5, ply=7)[0]
+    a2 = f.act(obs, mask, seed=5, ply=7)[0]
+    a3 = f.act(obs, mask, seed=5, ply=8)[0]
+    assert torch.equal(a1, a2) and not torch.equal(a1, a3)
+    assert ((a1 >= 0) & (a1 < 45)).all()
+    assert (f.greedy(obs, mask)[::17] == 0).all()
+
+
+def test_sample_frequencies_match_softmax():
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic
+    n = 65536
+    _, obs, mask = states(64, seed=31)
+    m = model(4)
+    with torch.no_grad():  # a flatter actor so that many actions have visible probability
+        for p in m.actor[-1].parameters():
+            p.mul_(0.05)
+    row = int(torch.argmax(mask.sum(dim=1)).item())
+    o = obs[row:row + 1].repeat(n, 1).contiguous()
+    k = mask[row:row + 1].repeat(n, 1).contiguous()
+    f = FusedActorCritic(m, with_critic=False)
+    _, logits = f.greedy(o[:1], k[:1], want_logits=True)
+    p = torch.softmax(logits[0].masked_fill(k[0] < 1, float("-inf")), dim=0).double().cpu().numpy()
+    f2 = FusedActorCritic(m, with_critic=True)
+    act = f2.act(o, k, seed=99, ply=0)[0].cpu().numpy()
+    freq = np.bincount(act, minlength=45) / n
+    se = np.sqrt(p * (1 - p) / n) + 1e-9
+    assert np.all(np.abs(freq - p) <= 4 * se + 1e-6), (freq, p)
+    assert freq[k[0].cpu().numpy() == 0].sum() == 0
+
+
+def test_refresh_tracks_weight_updates():
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic
+    _, obs, mask = states(512, seed=41)
+    m = model(5)
+    f = FusedActorCritic(m)
+    v1 = f.act(obs, mask)[3].clone()
+    with torch.no_grad():
+        m.critic[-1].bias.add_(1.0)
+    f.refresh()
+    v2 = f.act(obs, mask)[3]
+    assert torch.allclose(v2 - v1, torch.ones_like(v1), atol=1e-3)

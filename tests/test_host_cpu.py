@@ -44,6 +44,25 @@ def test_abi_host_side_errors():
     assert lib.spl_step(None, ctypes.byref(arena), None, None) == -1
 
 
+def test_policy_abi_host_side_errors():
+    """spl_policy_* argument checks (include/splendor_policy.h) run before any device work."""
+    from splendor_gym import _native
+    lib = _native.load_library()
+    assert lib.spl_policy_bytes(0) == 18 * 20480 and lib.spl_policy_bytes(1) == 35 * 20480
+    assert lib.spl_policy_pack(None, None, None, None) == -1
+    assert b"actor" in lib.spl_last_error()
+    assert lib.spl_policy_act(None, 0, 1, None, None) == -1
+    args = _native.ActArgs(obs=256, mask=256, action=256, mode=0)
+    args.obs = 258  # misaligned observations
+    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0), 1, ctypes.byref(args), None) == -1
+    assert b"obs" in lib.spl_last_error()
+    args.obs, args.value = 256, 256  # critic requested from an actor-only image
+    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0), 1, ctypes.byref(args), None) == -1
+    assert b"critic" in lib.spl_last_error() or b"value" in lib.spl_last_error()
+    args.value, args.mode = None, 7
+    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0), 1, ctypes.byref(args), None) == -1
+
+
 def test_arena_layout_sizes():
     from splendor_gym import _native
     lib = _native.load_library()

@@ -1,0 +1,77 @@
+"""Time the fused ActorCritic kernel (spl_policy_act) against the torch module on engine
+observations:  python tools/bench_policy.py [--tables 65536] [--iters 50]
+
+Prints one JSON line: per-call microseconds and achieved TFLOP/s (algorithmic: 2 x MACs of the
+unpadded 297-256-256-45 actor (+ 297-256-256-1 critic) per table) for SAMPLE (actor + critic) and
+GREEDY (actor), next to torch fp32 and bf16-autocast get_action_and_value / greedy."""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "splendor-gym_amd")]
+
+MACS_ACTOR = 297 * 256 + 256 * 256 + 256 * 45
+MACS_CRITIC = 297 * 256 + 256 * 256 + 256
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tables", type=int, default=65536)
+    ap.add_argument("--iters", type=int, default=50)
+    args = ap.parse_args()
+    import torch
+    from splendor_gym.device import Engine
+    from splendor_gym.fused_policy import FusedActorCritic
+    from splendor_gym.policy import ActorCritic, greedy_actions
+
+    n = args.tables
+    e = Engine(n, 2)
+    e.reset(seeds=range(n))
+    a = torch.zeros(n, dtype=torch.int32, device=e.device)
+    e.sample_uniform(out=a, seed=1, ply=0)
+    for k in range(8):
+        e.step(a, next_actions=a, policy_seed=1, ply=k + 1)
+    obs, mask = e.obs, e.mask
+    torch.manual_seed(0)
+    m = ActorCritic().to(e.device).eval()
+    f = FusedActorCritic(m)
+
+    def timeit(fn):
+        for _ in range(5):
+            fn()
+        s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(args.iters):
+            fn()
+        t.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(t) * 1e3 / args.iters
+
+    res = {}
+    res["fused_sample_us"] = timeit(lambda: f.act(obs, mask, seed=1, ply=2))
+    res["fused_greedy_us"] = timeit(lambda: f.greedy(obs, mask))
+
+    def torch_sample():
+        with torch.no_grad():
+            return m.get_action_and_value(obs.float(), mask.float())
+
+    def torch_sample_bf16():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            return m.get_action_and_value(obs.float(), mask.float())
+
+    res["torch_fp32_sample_us"] = timeit(torch_sample)
+    res["torch_bf16_sample_us"] = timeit(torch_sample_bf16)
+    res["torch_fp32_greedy_us"] = timeit(lambda: greedy_actions(m, obs, mask))
+    fl_s = 2.0 * n * (MACS_ACTOR + MACS_CRITIC)
+    fl_g = 2.0 * n * MACS_ACTOR
+    res["fused_sample_tflops"] = fl_s / res["fused_sample_us"] / 1e6
+    res["fused_greedy_tflops"] = fl_g / res["fused_greedy_us"] / 1e6
+    res["tables"] = n
+    print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main()
