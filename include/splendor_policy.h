@@ -50,6 +50,7 @@ typedef struct {
     float *logits;       /* [n][45] out: raw actor logits before masking (may be NULL)            */
     uint64_t seed;       /* SAMPLE: Philox key; draw for table t at ply p = f(seed; table0+t, p)  */
     uint64_t ply;
+    const uint64_t *ply_base; /* device, nullable: added to `ply` (lets a captured graph replay)  */
     int64_t table0;
     int32_t mode;        /* SPL_ACT_*                                                            */
     int32_t reserved;

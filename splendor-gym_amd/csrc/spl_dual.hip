@@ -1,0 +1,120 @@
+// spl_dual.hip — glue of the batched dual step (include/splendor_dual.h): the per-table branches
+// of wrappers/dual_step_native.py:90-193 as two elementwise kernels, so a dual step is four or
+// five launches instead of a chain of ~30 tensor ops.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/splendor_amd.h"
+#include "../../include/splendor_dual.h"
+
+int spl_fail(int code, const std::string &msg);  // spl_engine.hip
+
+namespace spld {
+
+__global__ __launch_bounds__(256) void k_dual_gate(int n, const uint8_t *__restrict__ ta, const uint8_t *__restrict__ fa,
+                                                   int32_t *__restrict__ opp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool passed = ta[i] == 0 && (fa[i] & (SPL_F_ILLEGAL | SPL_F_OOB)) == 0;
+    if (!passed) opp[i] = -1;
+}
+
+// final_rewards[player] of a finished game (envs/splendor_env.py:92-115): +-1 for the winner /
+// loser; without a winner -0.1 after the turn limit, else 0 (the no-legal-move draw reports none)
+__device__ __forceinline__ float final_reward(int player, int winner, uint8_t flags) {
+    if (winner < 0) return (flags & SPL_F_TURN_LIMIT) ? -0.1f : 0.f;
+    return winner == player ? 1.f : -1.f;
+}
+
+struct Io {
+    const float *ra, *rb;
+    const uint8_t *ta, *tb, *fa, *fb;
+    const int8_t *wa, *wb;
+    float *agent_reward, *opp_reward;
+    uint8_t *done;
+    int8_t *ended_on;
+    uint8_t *info;
+};
+
+__global__ __launch_bounds__(256) void k_dual_finish(int n, Io io) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t ta = io.ta[i], fa = io.fa[i], fb = io.fb[i];
+    const bool ended_a = ta != 0, ended_b = !ended_a && io.tb[i] != 0;
+    const bool passed = !ended_a && (fa & (SPL_F_ILLEGAL | SPL_F_OOB)) == 0;
+    io.agent_reward[i] = ended_a ? io.ra[i] : ended_b ? final_reward(0, io.wb[i], fb) : 0.f;
+    io.opp_reward[i] = ended_a ? final_reward(1, io.wa[i], fa) : passed ? io.rb[i] : 0.f;
+    io.done[i] = ended_a || ended_b;
+    io.ended_on[i] = ended_a ? 1 : ended_b ? 2 : 0;
+    io.info[i] = ((fa & SPL_F_ILLEGAL) ? SPL_DUAL_ILLEGAL : 0) | (((fa | fb) & SPL_F_DRAW) ? SPL_DUAL_DRAW : 0) |
+                 (((fa | fb) & SPL_F_TURN_LIMIT) ? SPL_DUAL_TURN_LIMIT : 0);
+}
+
+// opponent_obs = done ? final_obs : obs, 16 bytes per thread (rows are 297 int32: a 16-byte
+// piece may straddle two tables, so each int picks by its own table)
+__global__ __launch_bounds__(256) void k_dual_opp_obs(int n, const uint8_t *__restrict__ ta, const uint8_t *__restrict__ tb,
+                                                      const int4 *__restrict__ obs, const int4 *__restrict__ fin,
+                                                      int4 *__restrict__ out) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, total = (int64_t)n * 297;
+    if (4 * q >= total) return;
+    if (4 * q + 3 < total) {
+        const int4 o = obs[q], f = fin[q];
+        int v[4] = {o.x, o.y, o.z, o.w};
+        const int w[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t t = (4 * q + k) / 297;
+            if (ta[t] != 0 || tb[t] != 0) v[k] = w[k];
+        }
+        out[q] = make_int4(v[0], v[1], v[2], v[3]);
+    } else {
+        const int32_t *o = reinterpret_cast<const int32_t *>(obs), *f = reinterpret_cast<const int32_t *>(fin);
+        int32_t *d = reinterpret_cast<int32_t *>(out);
+        for (int64_t e = 4 * q; e < total; ++e) {
+            const int64_t t = e / 297;
+            d[e] = (ta[t] != 0 || tb[t] != 0) ? f[e] : o[e];
+        }
+    }
+}
+
+}  // namespace spld
+
+using namespace spld;
+
+extern "C" {
+
+int spl_dual_gate(int32_t n, const uint8_t *terminated_a, const uint8_t *flags_a, int32_t *opp_action, void *stream) {
+    if (n <= 0) return spl_fail(SPL_E_ARG, "n must be positive");
+    if (!terminated_a || !flags_a || !opp_action) return spl_fail(SPL_E_ARG, "null buffer");
+    hipLaunchKernelGGL(k_dual_gate, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, terminated_a, flags_a,
+                       opp_action);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SPL_OK : spl_fail(SPL_E_HIP, std::string("k_dual_gate: ") + hipGetErrorString(e));
+}
+
+int spl_dual_finish(int32_t n, const spl_dual_io_t *io, void *stream) {
+    if (n <= 0) return spl_fail(SPL_E_ARG, "n must be positive");
+    if (!io || !io->reward_a || !io->reward_b || !io->terminated_a || !io->terminated_b || !io->flags_a ||
+        !io->flags_b || !io->winner_a || !io->winner_b || !io->agent_reward || !io->opp_reward || !io->done ||
+        !io->game_ended_on || !io->info_flags)
+        return spl_fail(SPL_E_ARG, "null buffer");
+    if (io->opp_obs && (!io->obs || !io->final_obs)) return spl_fail(SPL_E_ARG, "opp_obs needs obs and final_obs");
+    if (io->opp_obs && (((uintptr_t)io->obs | (uintptr_t)io->final_obs | (uintptr_t)io->opp_obs) & 15u))
+        return spl_fail(SPL_E_ARG, "observation buffers must be 16-byte aligned");
+    const hipStream_t s = (hipStream_t)stream;
+    const Io k{io->reward_a, io->reward_b, io->terminated_a, io->terminated_b, io->flags_a, io->flags_b, io->winner_a,
+               io->winner_b, io->agent_reward, io->opp_reward, io->done, io->game_ended_on, io->info_flags};
+    hipLaunchKernelGGL(k_dual_finish, dim3((n + 255) / 256), dim3(256), 0, s, n, k);
+    if (io->opp_obs) {
+        const int64_t quads = ((int64_t)n * 297 + 3) / 4;
+        hipLaunchKernelGGL(k_dual_opp_obs, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, n, io->terminated_a,
+                           io->terminated_b, reinterpret_cast<const int4 *>(io->obs),
+                           reinterpret_cast<const int4 *>(io->final_obs), reinterpret_cast<int4 *>(io->opp_obs));
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SPL_OK : spl_fail(SPL_E_HIP, std::string("k_dual_finish: ") + hipGetErrorString(e));
+}
+
+}  // extern "C"

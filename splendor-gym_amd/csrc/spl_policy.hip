@@ -119,6 +119,7 @@ struct ActArgs {
     int32_t *action;
     float *logprob, *entropy, *value, *logits;
     uint64_t seed, ply;
+    const uint64_t *ply_base;
     int64_t table0;
     int n;
 };
@@ -338,8 +339,9 @@ __global__ __launch_bounds__(256, 1) void k_act(const uint8_t *__restrict__ W, A
                     T += p * d;
                 }
             const float logS = __logf(S);
+            const uint64_t ply = a.ply + (a.ply_base ? *a.ply_base : 0ull);
             const uint4 rnd = philox4x32(make_uint4((uint32_t)(a.table0 + t), (uint32_t)((uint64_t)(a.table0 + t) >> 32),
-                                                    (uint32_t)a.ply, (uint32_t)(a.ply >> 32)),
+                                                    (uint32_t)ply, (uint32_t)(ply >> 32)),
                                          make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32) ^ 0xA5C3E1F7u));
             const float target = (float)(rnd.x >> 8) * (1.f / 16777216.f) * S;
             float cum = 0.f;
@@ -398,7 +400,7 @@ int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const sp
     const bool critic = sample && args->value;
     if (critic && !has_critic) return spl_fail(SPL_E_ARG, "value requested from an actor-only image");
     const ActArgs a{args->obs, args->mask, args->action, args->logprob, args->entropy, args->value, args->logits,
-                    args->seed, args->ply, args->table0, n};
+                    args->seed, args->ply, args->ply_base, args->table0, n};
     const dim3 grid((unsigned)((n + kRowsPerBlock - 1) / kRowsPerBlock)), block(kWaves * 64);
     const hipStream_t s = (hipStream_t)stream;
     const uint8_t *W = static_cast<const uint8_t *>(packed);

@@ -48,10 +48,20 @@ class ActArgs(ctypes.Structure):
     """spl_act_args_t (include/splendor_policy.h)"""
     _fields_ = [("obs", c_void_p), ("mask", c_void_p), ("action", c_void_p), ("logprob", c_void_p),
                 ("entropy", c_void_p), ("value", c_void_p), ("logits", c_void_p), ("seed", c_uint64),
-                ("ply", c_uint64), ("table0", c_int64), ("mode", c_int32), ("reserved", c_int32)]
+                ("ply", c_uint64), ("ply_base", c_void_p), ("table0", c_int64), ("mode", c_int32), ("reserved", c_int32)]
 
 
 ACT_SAMPLE, ACT_GREEDY = 0, 1  # SPL_ACT_*
+
+
+class DualIo(ctypes.Structure):
+    """spl_dual_io_t (include/splendor_dual.h)"""
+    _fields_ = [(k, c_void_p) for k in ("reward_a", "reward_b", "terminated_a", "terminated_b", "flags_a", "flags_b",
+                                        "winner_a", "winner_b", "agent_reward", "opp_reward", "done",
+                                        "game_ended_on", "info_flags", "obs", "final_obs", "opp_obs")]
+
+
+DUAL_ILLEGAL, DUAL_DRAW, DUAL_TURN_LIMIT = 0x01, 0x02, 0x04  # SPL_DUAL_*
 
 
 # spl_table_t (include/splendor_table.h) as a numpy structured dtype
@@ -92,6 +102,9 @@ SIGNATURES = {
     "spl_policy_bytes": ([c_int32], c_int64),
     "spl_policy_pack": ([ctypes.POINTER(MlpDesc), ctypes.POINTER(MlpDesc), c_void_p, c_void_p], c_int32),
     "spl_policy_act": ([c_void_p, c_int64, c_int32, ctypes.POINTER(ActArgs), c_void_p], c_int32),
+    # include/splendor_dual.h
+    "spl_dual_gate": ([c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
+    "spl_dual_finish": ([c_int32, ctypes.POINTER(DualIo), c_void_p], c_int32),
 }
 
 

@@ -111,11 +111,12 @@ class Engine:
         return self.obs, self.mask
 
     def step(self, actions=None, autoreset=True, final_obs=True, next_actions=None, policy_seed=0, ply=0,
-             ep_return=None, ep_count=None, ply_base=None, policy=0):
+             ep_return=None, ep_count=None, ply_base=None, policy=0, small=None):
         """One env step on every table (SplendorEnv.step semantics per table).  autoreset: False,
         True (same-step autoreset) or 2 (also re-deal tables terminal on entry, without a move).
         next_actions (optional int32 tensor) receives `policy`'s action (_native.POLICY_*) over
-        the new state."""
+        the new state.  small: optional (reward, terminated, flags, winner) tensors that receive
+        those outputs instead of self.reward/terminated/flags/winner."""
         torch = self.torch
         if actions is None:
             actions = self.actions
@@ -124,9 +125,9 @@ class Engine:
             actions = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
         if actions.numel() != self.n:
             raise ValueError(f"expected {self.n} actions")
+        rw, tm, fl, wn = small if small is not None else (self.reward, self.terminated, self.flags, self.winner)
         a = StepArgs(actions=actions.data_ptr(), obs=self.obs.data_ptr(), mask=self.mask.data_ptr(),
-                     reward=self.reward.data_ptr(), terminated=self.terminated.data_ptr(),
-                     flags=self.flags.data_ptr(), winner=self.winner.data_ptr(),
+                     reward=rw.data_ptr(), terminated=tm.data_ptr(), flags=fl.data_ptr(), winner=wn.data_ptr(),
                      final_obs=self.final_obs.data_ptr() if (final_obs and autoreset) else None,
                      autoreset=(2 if autoreset == 2 else 1) if autoreset else 0, policy=int(policy),
                      next_actions=None if next_actions is None else next_actions.data_ptr(),
@@ -137,7 +138,7 @@ class Engine:
         with torch.cuda.device(self.device):
             check(self.lib, self.lib.spl_step(self.ctx, ctypes.byref(self.desc), ctypes.byref(a), self.stream()))
         self._keep_actions = actions
-        return self.obs, self.mask, self.reward, self.terminated, self.flags
+        return self.obs, self.mask, rw, tm, fl
 
     def rollout(self, steps, actions=None, next_actions=None, policy_seed=0, ply=0, out=None, final_obs=True,
                 ep_return=None, ep_count=None, ply_base=None, policy=0):

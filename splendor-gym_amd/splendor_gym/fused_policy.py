@@ -83,17 +83,19 @@ class FusedActorCritic:
         return obs.shape[0]
 
     def _run(self, obs, mask, mode, action, logprob=None, entropy=None, value=None, logits=None, seed=0, ply=0,
-             table0=0):
+             table0=0, ply_base=None):
         n = self._check_inputs(obs, mask)
         a = ActArgs(obs=obs.data_ptr(), mask=mask.data_ptr(), action=action.data_ptr(), logprob=ptr(logprob),
                     entropy=ptr(entropy), value=ptr(value), logits=ptr(logits), seed=int(seed) & (2**64 - 1),
-                    ply=int(ply) & (2**64 - 1), table0=int(table0), mode=mode, reserved=0)
+                    ply=int(ply) & (2**64 - 1), ply_base=ptr(ply_base), table0=int(table0), mode=mode, reserved=0)
         with self.torch.cuda.device(self.device):
             check(self.lib, self.lib.spl_policy_act(self.image.data_ptr(), self.image.numel(), n, ctypes.byref(a),
                                                     self._stream()))
 
-    def act(self, obs, mask, seed=0, ply=0, table0=0, out=None, want_logits=False):
-        """(action int32 [n], logprob f32 [n], entropy f32 [n], value f32 [n, 1] or None[, logits])."""
+    def act(self, obs, mask, seed=0, ply=0, table0=0, out=None, want_logits=False, ply_base=None):
+        """(action int32 [n], logprob f32 [n], entropy f32 [n], value f32 [n, 1] or None[, logits]).
+        The draw of table i is keyed by (seed; table0 + i, ply + *ply_base); ply_base is an
+        optional int64 device scalar that a captured graph can advance between replays."""
         t = self.torch
         n = obs.shape[0]
         o = out or {}
@@ -102,7 +104,7 @@ class FusedActorCritic:
         entropy = o.get("entropy", t.empty(n, dtype=t.float32, device=self.device))
         value = o.get("value", t.empty(n, 1, dtype=t.float32, device=self.device)) if self.with_critic else None
         logits = t.empty(n, NUM_ACTIONS, dtype=t.float32, device=self.device) if want_logits else None
-        self._run(obs, mask, ACT_SAMPLE, action, logprob, entropy, value, logits, seed, ply, table0)
+        self._run(obs, mask, ACT_SAMPLE, action, logprob, entropy, value, logits, seed, ply, table0, ply_base)
         return (action, logprob, entropy, value, logits) if want_logits else (action, logprob, entropy, value)
 
     def greedy(self, obs, mask, out=None, want_logits=False):

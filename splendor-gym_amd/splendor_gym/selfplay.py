@@ -26,6 +26,9 @@ stream); `agent_obs` / info["action_mask"] are then the new episode's, info["fin
 holds the observation that ended the game, and `opp_obs` is the reference's opponent_obs (the
 post-turn observation, i.e. the final one on finished tables) when requested.
 """
+import ctypes
+from collections.abc import Mapping
+
 import torch
 
 from . import _native
@@ -33,6 +36,27 @@ from .device import Engine
 
 _DEVICE_POLICIES = {"random": _native.POLICY_UNIFORM, "greedy_v1": _native.POLICY_GREEDY_V1,
                     "basic_priority": _native.POLICY_BASIC_PRIORITY}
+
+
+class DualInfo(Mapping):
+    """info of a batched dual step.  The boolean views illegal_action / draw / turn_limit are
+    derived from the packed info_flags on first access (each is one extra tensor op)."""
+    _LAZY = {"illegal_action": _native.DUAL_ILLEGAL, "draw": _native.DUAL_DRAW, "turn_limit": _native.DUAL_TURN_LIMIT}
+
+    def __init__(self, base, info_flags):
+        self._d = dict(base)
+        self._flags = info_flags
+
+    def __getitem__(self, k):
+        if k not in self._d and k in self._LAZY:
+            self._d[k] = (self._flags & self._LAZY[k]) != 0
+        return self._d[k]
+
+    def __iter__(self):
+        return iter(list(self._d) + [k for k in self._LAZY if k not in self._d])
+
+    def __len__(self):
+        return len(set(self._d) | set(self._LAZY))
 
 
 class DualStepVectorEnv:
@@ -47,9 +71,22 @@ class DualStepVectorEnv:
         self.want_opp_obs = opponent_obs
         t = torch
         n, dev = num_envs, self.device
-        self.opp_actions = t.zeros(n, dtype=t.int32, device=dev)
-        self.agent_reward = t.zeros(n, dtype=t.float32, device=dev)
-        self.opp_reward = t.zeros(n, dtype=t.float32, device=dev)
+        z = lambda dt: t.zeros(n, dtype=dt, device=dev)
+        self.opp_actions = z(t.int32)
+        # phase A (agent move) small outputs, kept apart from the engine's (phase B) buffers
+        self.small_a = (z(t.float32), z(t.uint8), z(t.uint8), z(t.int8))
+        self.agent_reward, self.opp_reward = z(t.float32), z(t.float32)
+        self.done, self.game_ended_on, self.info_flags = z(t.bool), z(t.int8), z(t.uint8)  # done: 0/1 bytes
+        self.opp_obs = t.zeros(n, _native.OBS_DIM, dtype=t.int32, device=dev) if opponent_obs else None
+        e = self.eng
+        ra, ta, fa, wa = self.small_a
+        p = lambda x: None if x is None else x.data_ptr()
+        self._io = _native.DualIo(reward_a=p(ra), reward_b=p(e.reward), terminated_a=p(ta),
+                                  terminated_b=p(e.terminated), flags_a=p(fa), flags_b=p(e.flags), winner_a=p(wa),
+                                  winner_b=p(e.winner), agent_reward=p(self.agent_reward),
+                                  opp_reward=p(self.opp_reward), done=p(self.done),
+                                  game_ended_on=p(self.game_ended_on), info_flags=p(self.info_flags),
+                                  obs=p(e.obs), final_obs=p(e.final_obs), opp_obs=p(self.opp_obs))
         self._ply = 0
 
     # ------------------------------------------------------------------------------------
@@ -62,50 +99,39 @@ class DualStepVectorEnv:
         obs, mask = self.eng.reset(seeds=seeds)
         return obs, {"action_mask": mask, "to_play": obs[:, 294]}
 
-    @staticmethod
-    def _final_reward(player, winner, flags):
-        """final_rewards[player] (envs/splendor_env.py:92-115): ±1, or 0 / -0.1 (turn limit) when
-        there is no winner; 0 for the no-legal-move draw, which reports none."""
-        tl = (flags & _native.F_TURN_LIMIT) != 0
-        no_winner = torch.where(tl, torch.full_like(winner, -0.1, dtype=torch.float32),
-                                torch.zeros_like(winner, dtype=torch.float32))
-        return torch.where(winner < 0, no_winner,
-                           torch.where(winner == player, 1.0, -1.0).to(torch.float32))
-
     def dual_step(self, actions):
-        e = self.eng
+        """wrappers/dual_step_native.py:90-193 on every table: spl_step (agent) -> opponent
+        actions -> spl_dual_gate -> spl_step (opponent, autoreset 2) -> spl_dual_finish."""
+        e, lib = self.eng, self.eng.lib
         device_opp = isinstance(self.opponent, str)
         self._ply += 1
+        ra, ta, fa, wa = self.small_a
         # phase A: the agent's move (no reset); a device opponent's reply is drawn in the same kernel
-        e.step(actions, autoreset=False, final_obs=False,
+        e.step(actions, autoreset=False, final_obs=False, small=self.small_a,
                next_actions=self.opp_actions if device_opp else None,
                policy=_DEVICE_POLICIES[self.opponent] if device_opp else 0,
                policy_seed=self.policy_seed, ply=self._ply)
-        # keep phase A's small outputs: the opponent move overwrites the engine's buffers
-        ra, ta, fa, wa = e.reward.clone(), e.terminated.clone(), e.flags.clone(), e.winner.clone()
-        passed = (ta == 0) & ((fa & (_native.F_ILLEGAL | _native.F_OOB)) == 0)  # player 1 is to play
         if device_opp:
             opp = self.opp_actions
         else:
-            opp = torch.as_tensor(self.opponent(e.obs, e.mask), device=self.device).to(torch.int32)
-        opp = torch.where(passed, opp, torch.full_like(opp, -1))  # -1: out of range, no move
-        # phase B: the opponent's move; autoreset 2 also re-deals tables that ended on the agent's move
-        e.step(opp, autoreset=2, final_obs=True)
-        tb, fb, wb, rb = e.terminated, e.flags, e.winner, e.reward
-        ended_a, ended_b = ta != 0, tb != 0
-        done = ended_a | ended_b
-        torch.where(ended_a, ra, torch.where(ended_b, self._final_reward(0, wb, fb), torch.zeros_like(rb)),
-                    out=self.agent_reward)
-        torch.where(ended_a, self._final_reward(1, wa, fa), torch.where(passed, rb, torch.zeros_like(rb)),
-                    out=self.opp_reward)
-        agent_obs = e.obs
-        opp_obs = torch.where(done[:, None], e.final_obs, e.obs) if self.want_opp_obs else None
-        info = {"action_mask": e.mask, "to_play": e.obs[:, 294], "final_observation": e.final_obs,
-                "opponent_action": torch.where(passed, opp, torch.full_like(opp, -1)),
-                "game_ended_on": torch.where(ended_a, 1, torch.where(ended_b, 2, 0)).to(torch.int8),
-                "illegal_action": (fa & _native.F_ILLEGAL) != 0, "agent_step_reward": ra,
-                "draw": ((fa | fb) & _native.F_DRAW) != 0, "turn_limit": ((fa | fb) & _native.F_TURN_LIMIT) != 0}
-        return agent_obs, self.agent_reward, opp_obs, self.opp_reward, done, info
+            opp = self.opponent(e.obs, e.mask)
+            if not (isinstance(opp, torch.Tensor) and opp.dtype == torch.int32 and opp.is_contiguous()
+                    and opp.device == self.device):
+                opp = torch.as_tensor(opp, device=self.device).to(torch.int32).contiguous()
+            self._opp_keep = opp
+        stream = e.stream()
+        with torch.cuda.device(self.device):
+            # -1 (out of range: no move) where the agent's move was not applied or ended the game
+            _native.check(lib, lib.spl_dual_gate(self.num_envs, ta.data_ptr(), fa.data_ptr(), opp.data_ptr(), stream))
+            # phase B: the opponent's move; autoreset 2 also re-deals tables that ended on the agent's move
+            e.step(opp, autoreset=2, final_obs=True)
+            io = self._io
+            io.opp_obs = self.opp_obs.data_ptr() if self.want_opp_obs else None
+            _native.check(lib, lib.spl_dual_finish(self.num_envs, ctypes.byref(io), stream))
+        info = DualInfo({"action_mask": e.mask, "to_play": e.obs[:, 294], "final_observation": e.final_obs,
+                         "opponent_action": opp, "game_ended_on": self.game_ended_on, "agent_step_reward": ra},
+                        self.info_flags)
+        return e.obs, self.agent_reward, self.opp_obs, self.opp_reward, self.done, info
 
     def close(self):
         self.eng.close()

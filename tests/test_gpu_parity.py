@@ -294,6 +294,63 @@ def test_dual_step_vector_env_matches_per_env_wrappers():
     assert ended >= n  # every table finished at least one game and was re-dealt
 
 
+def test_dual_step_callable_opponent_and_illegal_actions():
+    """The callable-opponent path (spl_dual_gate / spl_dual_finish around two spl_step launches)
+    equals the fused device-opponent path table for table, including illegal and out-of-range
+    agent actions: those leave the table unchanged, the opponent does not move, and info reports
+    illegal_action with the -0.01 step reward (envs/splendor_env.py:62-66)."""
+    import torch
+    from splendor_gym.opponents import greedy_opponent_v1
+    from splendor_gym.selfplay import DualStepVectorEnv
+
+    def host_greedy(obs, mask):
+        o, m = obs.cpu().numpy(), mask.cpu().numpy()
+        return torch.tensor([greedy_opponent_v1(o[i], {"action_mask": m[i]}) for i in range(len(o))],
+                            dtype=torch.int32, device=obs.device)
+
+    n, seed = 96, 70
+    dev = DualStepVectorEnv(n, opponent="greedy_v1")
+    cal = DualStepVectorEnv(n, opponent=host_greedy)
+    _, info_d = dev.reset(seed=seed)
+    _, info_c = cal.reset(seed=seed)
+    rs = np.random.default_rng(9)
+    seen_illegal = seen_done = 0
+    for k in range(120):
+        mask = info_d["action_mask"].cpu().numpy()
+        acts = []
+        for i in range(n):
+            legal = np.flatnonzero(mask[i])
+            u = rs.random()
+            if u < 0.05:
+                acts.append(int(rs.choice([-1, 45, 99])))
+            elif u < 0.12 and len(legal) < 45:
+                acts.append(int(rs.choice(np.setdiff1d(np.arange(45), legal))))
+            else:
+                acts.append(int(rs.choice(legal)) if len(legal) else 0)
+        before = dev.eng.obs.clone()
+        a = torch.tensor(acts, dtype=torch.int32, device=dev.device)
+        od, ard, ood, ord_, dd, info_d = dev.dual_step(a)
+        oc, arc, ooc, orc_, dc, info_c = cal.dual_step(a.clone())
+        for x, y in ((od, oc), (ard, arc), (ood, ooc), (ord_, orc_), (dd, dc)):
+            assert torch.equal(x, y), k
+        for key in ("action_mask", "final_observation", "opponent_action", "game_ended_on", "agent_step_reward",
+                    "illegal_action", "draw", "turn_limit"):
+            assert torch.equal(info_d[key], info_c[key]), (k, key)
+        bad = np.array([not (0 <= x < 45) or mask[i][x] == 0 for i, x in enumerate(acts)])
+        ill = info_d["illegal_action"].cpu().numpy()
+        oob = np.array([not (0 <= x < 45) for x in acts])
+        assert np.array_equal(ill, bad & ~oob & (mask.sum(axis=1) > 0)), k
+        unchanged = bad & (mask.sum(axis=1) > 0)
+        assert (info_d["opponent_action"].cpu().numpy()[unchanged] == -1).all()
+        assert torch.equal(od[torch.from_numpy(unchanged).to(od.device)],
+                           before[torch.from_numpy(unchanged).to(od.device)])
+        r = info_d["agent_step_reward"].cpu().numpy()
+        assert np.allclose(r[ill], -0.01)
+        seen_illegal += int(ill.sum())
+        seen_done += int(dd.sum())
+    assert seen_illegal > 50 and seen_done > n
+
+
 def test_batched_eval_matches_reference_eval_suite():
     """splendor_gym.evaluation.eval_vs_opponent == the reference eval_suite.eval_vs_opponent
     (tests/golden/eval.json) for deterministic agents against greedy_opponent_v1."""

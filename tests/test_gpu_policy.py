@@ -111,6 +111,8 @@ def test_sample_determinism_and_no_legal_rows():
     a2 = f.act(obs, mask, seed=5, ply=7)[0]
     a3 = f.act(obs, mask, seed=5, ply=8)[0]
     assert torch.equal(a1, a2) and not torch.equal(a1, a3)
+    base = torch.tensor([5], dtype=torch.int64, device=obs.device)  # device ply counter (graph replays)
+    assert torch.equal(f.act(obs, mask, seed=5, ply=2, ply_base=base)[0], a1)
     assert ((a1 >= 0) & (a1 < 45)).all()
     assert (f.greedy(obs, mask)[::17] == 0).all()
 
