@@ -95,6 +95,7 @@ def load_pmc_traffic(players, tables, mode, steps_per_launch):
 
 
 def main():
+    global ROLLOUT_K
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1024)
@@ -112,7 +113,13 @@ def main():
                          f"{ROLLOUT_K} env steps; step: one spl_step launch per env step (same trajectories "
                          "and per-step outputs, tests/test_gpu_parity.py::test_rollout_equals_step_chain)")
     ap.add_argument("--only", action="store_true", help="skip measuring the other mode (reported as other_mode)")
+    ap.add_argument("--rollout-k", type=int, default=ROLLOUT_K, help="env steps per spl_rollout launch")
+    ap.add_argument("--refill-every", type=int, default=0, help="0 = per player count (64/32/16)")
+    ap.add_argument("--refill", choices=("fused", "separate"), default="fused",
+                    help="rollout mode: due pool refills run inside the spl_rollout launch (fused) or as a "
+                         "spl_refill launch after it (step mode always launches spl_refill)")
     args = ap.parse_args()
+    ROLLOUT_K = args.rollout_k
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank_env = int(os.environ.get("RANK", "0"))
@@ -132,8 +139,11 @@ def main():
     dev = local_device(local)
     torch.cuda.set_device(dev)
     T, P = args.tables, args.players
+    R = args.refill_every or REFILL_EVERY[P]
     table0 = rank * T
-    eng = Engine(T, P, device=dev, refill_period=0, table0=table0)
+    # the library schedules the pool refills: every R steps (spl_step: a spl_refill launch; spl_rollout:
+    # inside the rollout launch unless --refill separate)
+    eng = Engine(T, P, device=dev, refill_period=R, table0=table0, refill_fused=args.refill == "fused")
     eng.reset(seeds=range(table0, table0 + T))
     lib = eng.lib
     buf = [torch.zeros(T, dtype=torch.int32, device=dev) for _ in range(2)]
@@ -154,11 +164,11 @@ def main():
     step_args = [mkargs(buf[0], buf[1]), mkargs(buf[1], buf[0])]
     ctx, desc = eng.ctx, ctypes.byref(eng.desc)
     stream = eng.stream()
-    R = REFILL_EVERY[P]
 
     def run(mode, k0, k1, strm, ev=None):
-        """Steps k0..k1-1 (ply k+1 relative to ply_base), refill every R steps.  mode "step":
-        one spl_step launch per step; "rollout": one spl_rollout launch per ROLLOUT_K steps."""
+        """Steps k0..k1-1 (ply k+1 relative to ply_base).  mode "step": one spl_step launch per
+        step; "rollout": one spl_rollout launch per ROLLOUT_K steps.  Refills every R steps are
+        issued by the library (the arena's step counter)."""
         per = 1 if mode == "step" else ROLLOUT_K
         for i, k in enumerate(range(k0, k1, per)):
             sa = step_args[(k // per) & 1]
@@ -171,8 +181,6 @@ def main():
                 _native.check(lib, lib.spl_rollout(ctx, desc, ctypes.byref(sa), ROLLOUT_K, 0, strm))
             if ev is not None:
                 ev[1][i].record()
-            if (k + per) % R == 0:
-                _native.check(lib, lib.spl_refill(ctx, desc, strm))
 
     def measure(mode, k_base):
         """Warm up, capture, time K steps; returns the timing record.  Steps are numbered from
@@ -273,7 +281,8 @@ def main():
             "config": {"workload": f"{P}-player SplendorEnv.step x {T} tables per GPU, legal mask + uniform-random "
                                    "policy, same-step autoreset, obs int32[297] + mask int8[45] per table-step",
                        "tables_per_gpu": T, "players": P, "parallelism": f"table-sharded x{world}",
-                       "refill_every": R, "rollout_steps_per_launch": ROLLOUT_K, "mode": main["mode"],
+                       "refill_every": R, "refill": args.refill if main_rec["mode"] == "rollout" else "separate",
+                       "rollout_steps_per_launch": ROLLOUT_K, "mode": main["mode"],
                        "launch": main["launch"]},
             "roofline": roof,
             "cpu_baseline": cpu,

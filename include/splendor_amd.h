@@ -111,6 +111,10 @@ int spl_ctx_destroy(spl_ctx_t *ctx);
 /* Pool refill period in steps (default 64; three pool deals per table cover three resets in between);
  * 0 disables automatic refills (inline deals). */
 int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period);
+/* spl_rollout only: 1 (default) = a due refill runs inside the rollout launch, each wave at a step
+ * of its own while other waves' stores keep HBM busy; 0 = a separate spl_refill launch after it.
+ * Results are identical either way. */
+int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused);
 
 int64_t spl_arena_bytes(int32_t n, int32_t players);
 /* Zero the arena and mark every table's pool as not dealt (must precede the first spl_reset
@@ -136,7 +140,8 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *args, vo
  * the last step.  With per_step_outputs != 0, step k writes block k of every output array (obs
  * [steps][n][297], mask [steps][n][45], reward/terminated/flags/winner [steps][n], final_obs
  * [steps][n][297]; n divisible by 4); otherwise every step overwrites block 0.  A pool refill
- * follows when the step counter crosses a multiple of the refill period (keep steps <= period). */
+ * is due when the step counter crosses a multiple of the refill period (keep steps <= period);
+ * it runs inside the launch (spl_ctx_set_refill_fused) or as a spl_refill launch after it. */
 int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *args, int32_t steps,
                 int32_t per_step_outputs, void *stream);
 

@@ -114,9 +114,13 @@ constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 
 constexpr int kMaskStreamWords = 64 * 45 / 32;  // 90
 
-struct __align__(16) BlockLDS {
+// constant tables staged per workgroup: 16-B obs-ready card records and 8-B noble records
+struct __align__(16) Consts {
     uint4 cards[90];
     uint2 nobles[10];
+};
+
+struct __align__(16) BlockLDS : Consts {
     uint64_t mask[64];
     uint32_t mbits[96];  // the wave's 64 x 45 mask bits as one stream (store_mask_block)
     uint8_t rows[64 * kObsDim];   // observation staging; also the deal scratch (64 x 112 B)
@@ -130,7 +134,7 @@ __device__ __forceinline__ uint32_t bget(uint32_t w, int k) { return (w >> (8 * 
 __device__ __forceinline__ uint32_t bset(uint32_t w, int k, uint32_t v) {
     return (w & ~(0xFFu << (8 * k))) | ((v & 0xFFu) << (8 * k));
 }
-__device__ __forceinline__ int lane_id() { return threadIdx.x; }
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63u); }
 
 // Cross-lane LDS hand-off inside ONE wave (every workgroup here is a single wave).
 // __syncthreads() would also emit s_waitcnt vmcnt(0): the wave would stall until its pending
@@ -232,7 +236,7 @@ __device__ __forceinline__ void board_set(uint32_t *sw, int k, uint32_t v) {  //
     for (int t = 0; t < 3; ++t) sw[SW_BOARD + t] = (k >> 2) == t ? bset(sw[SW_BOARD + t], k & 3, v) : sw[SW_BOARD + t];
 }
 
-__device__ __forceinline__ uint4 card_rec(const BlockLDS &L, int id) { return L.cards[id < 90 ? id : 0]; }
+__device__ __forceinline__ uint4 card_rec(const Consts &L, int id) { return L.cards[id < 90 ? id : 0]; }
 
 __device__ __forceinline__ int card_cost(uint4 rec, int c) { return c < 4 ? (int)bget(rec.z, c) : (int)bget(rec.w, 0); }
 
@@ -277,7 +281,7 @@ constexpr uint64_t kTake3Masks = (0x07ull) | (0x0Bull << 5) | (0x13ull << 10) | 
 __device__ __forceinline__ uint32_t take3_mask(int i) { return (uint32_t)(kTake3Masks >> (5 * i)) & 31u; }
 
 // engine/rules.py:40-93 legal_moves -> 45-bit mask
-__device__ __forceinline__ uint64_t legal_mask(const uint32_t *sw, const Pl &p, const int bank[6], const BlockLDS &L) {
+__device__ __forceinline__ uint64_t legal_mask(const uint32_t *sw, const Pl &p, const int bank[6], const Consts &L) {
     uint32_t avail = 0;
 #pragma unroll
     for (int c = 0; c < 5; ++c) avail |= (bank[c] >= 1 ? 1u : 0u) << c;
@@ -310,7 +314,7 @@ __device__ __forceinline__ uint64_t legal_mask(const uint32_t *sw, const Pl &p, 
 
 // engine/rules.py:40-93 restricted to one action (the env only needs mask[a]) ...
 __device__ __forceinline__ bool action_legal(const uint32_t *sw, const Pl &p, const int bank[6], int a,
-                                             const BlockLDS &L) {
+                                             const Consts &L) {
     if (a < 10) {
         uint32_t avail = 0;
 #pragma unroll
@@ -337,7 +341,7 @@ __device__ __forceinline__ bool action_legal(const uint32_t *sw, const Pl &p, co
 
 // ... and whether ANY move is legal: with a non-gold colour in the bank some take-3 always is
 // (rules.py:45-58), otherwise fall back to the full mask (rare).
-__device__ __forceinline__ bool any_legal(const uint32_t *sw, const Pl &p, const int bank[6], const BlockLDS &L) {
+__device__ __forceinline__ bool any_legal(const uint32_t *sw, const Pl &p, const int bank[6], const Consts &L) {
     const bool some_colour = bank[0] > 0 || bank[1] > 0 || bank[2] > 0 || bank[3] > 0 || bank[4] > 0;
     return some_colour || legal_mask(sw, p, bank, L) != 0ull;
 }
@@ -566,7 +570,7 @@ __device__ __forceinline__ void enforce_token_limit(Pl &p, int bank[6], int turn
 }
 
 // engine/rules.py:132-147 _grant_noble_if_applicable (first visible noble in slot order)
-__device__ __forceinline__ void grant_noble(uint32_t *sw, Pl &p, int to_play, const BlockLDS &L) {
+__device__ __forceinline__ void grant_noble(uint32_t *sw, Pl &p, int to_play, const Consts &L) {
     const int nn = (int)bget(sw[SW_DECK], 3);
     uint32_t owners = (sw[SW_NOB1] >> 8) & 0x7FFFu;
     bool granted = false;
@@ -626,7 +630,7 @@ __device__ __forceinline__ bool is_terminal(const uint32_t *sw) {
 
 // engine/rules.py:196-287 apply_action on the current player (action known legal)
 template <int P>
-__device__ __forceinline__ void apply_action(Tab<P> &T, int a, uint32_t top, const BlockLDS &L, const uint4 *lut,
+__device__ __forceinline__ void apply_action(Tab<P> &T, int a, uint32_t top, const Consts &L, const uint4 *lut,
                                              int pre_key, uint4 pre_e, uint32_t &flags) {
     uint32_t *sw = T.sw;
     const int tp = get_to_play(sw);
@@ -708,57 +712,71 @@ __device__ __forceinline__ void apply_action(Tab<P> &T, int a, uint32_t top, con
 }
 
 // ------------------------------------------------------------------------------------------
-// observation (engine/encode.py:124-187) into this lane's LDS row, as bytes
+// observation (engine/encode.py:124-187) into the wave's LDS row block, as bytes
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void put4(uint8_t *row, int o, uint32_t w) {
-    row[o] = (uint8_t)w;
-    row[o + 1] = (uint8_t)(w >> 8);
-    row[o + 2] = (uint8_t)(w >> 16);
-    row[o + 3] = (uint8_t)(w >> 24);
+// The wave's rows are packed back to back (row r at byte 297r), so most fields of a lane's row
+// sit at unaligned LDS addresses: written field by field they compile to unaligned ds_write_b96
+// / b32 accesses that stall the LDS pipe (SQ_LDS_UNALIGNED_STALL) and to ~35 byte writes per row.
+// Instead each lane assembles its 297 bytes as 75 dwords in registers (R[j] = bytes 4j..4j+3;
+// every offset is a compile-time constant, so R stays in VGPRs) and writes the ALIGNED dwords
+// that start inside its row, shifted into place with v_alignbyte_b32; the dword that straddles
+// rows L and L+1 is completed with row L+1's first bytes (its bank counts) taken from lane L+1.
+
+// n bytes of v at byte offset o of the row (o, n compile-time after unrolling)
+__device__ __forceinline__ void rput(uint32_t (&R)[76], int o, int n, uint32_t v) {
+    if (n < 4) v &= (1u << (8 * n)) - 1u;
+    const int j = o >> 2, sh = (o & 3) * 8;
+    R[j] |= v << sh;
+    if (sh != 0 && (o & 3) + n > 4) R[j + 1] |= v >> (32 - sh);
 }
 
-__device__ __forceinline__ void put_card13(uint8_t *row, int o, uint4 rec, bool present) {
-    put4(row, o, present ? rec.x : 0u);
-    put4(row, o + 4, present ? rec.y : 0u);
-    put4(row, o + 8, present ? rec.z : 0u);
-    row[o + 12] = present ? (uint8_t)rec.w : (uint8_t)0;
+__device__ __forceinline__ void rput_card13(uint32_t (&R)[76], int o, uint4 rec, bool present) {
+    rput(R, o, 4, present ? rec.x : 0u);
+    rput(R, o + 4, 4, present ? rec.y : 0u);
+    rput(R, o + 8, 4, present ? rec.z : 0u);
+    rput(R, o + 12, 1, present ? rec.w : 0u);
 }
 
+// Row of table T into rows_base[297*lane ...].  Every lane of the wave must call it (the row
+// boundaries are shared with the neighbouring lanes); rows of lanes whose table is not needed
+// are written too and simply not stored.
 template <int P>
-__device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *row, const BlockLDS &L) {
+__device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *rows_base, const Consts &L) {
     const uint32_t *sw = T.sw;
     const int tp = get_to_play(sw);
-    put4(row, 0, sw[SW_BANK0]);                 // bank :128
-    row[4] = (uint8_t)sw[SW_BANK1];
-    row[5] = (uint8_t)(sw[SW_BANK1] >> 8);
+    uint32_t R[76];
+#pragma unroll
+    for (int j = 0; j < 76; ++j) R[j] = 0u;
+    rput(R, 0, 4, sw[SW_BANK0]);                // bank :128
+    rput(R, 4, 2, sw[SW_BANK1]);
     uint32_t me[4], op[4];
     get_player(T, tp, me);                      // current :131-135
     get_player(T, (tp + 1) % P, op);            // opponent = next player :138-142
-    put4(row, 6, me[0]);
-    put4(row, 10, me[1]);
-    put4(row, 14, me[2]);
-    row[18] = (uint8_t)(me[3] & 3u);
-    put4(row, 19, op[0]);
-    put4(row, 23, op[1]);
-    put4(row, 27, op[2]);
-    row[31] = (uint8_t)(op[3] & 3u);
+    rput(R, 6, 4, me[0]);
+    rput(R, 10, 4, me[1]);
+    rput(R, 14, 4, me[2]);
+    rput(R, 18, 1, me[3] & 3u);
+    rput(R, 19, 4, op[0]);
+    rput(R, 23, 4, op[1]);
+    rput(R, 27, 4, op[2]);
+    rput(R, 31, 1, op[3] & 3u);
 #pragma unroll
     for (int k = 0; k < 12; ++k) {              // board :144-147
         const int id = (int)bget(sw[SW_BOARD + k / 4], k % 4);
-        put_card13(row, 32 + 13 * k, card_rec(L, id), id != 0xFF);
+        rput_card13(R, 32 + 13 * k, card_rec(L, id), id != 0xFF);
     }
     const int mn = (int)(me[3] & 3u), on = (int)(op[3] & 3u), orev = (int)((op[3] >> 2) & 7u);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {               // own reserved, always revealed :151-155
         const bool pr = i < mn;
-        put_card13(row, 188 + 14 * i, card_rec(L, (int)bget(me[3], i + 1)), pr);
-        row[188 + 14 * i + 13] = pr ? 1 : 0;
+        rput_card13(R, 188 + 14 * i, card_rec(L, (int)bget(me[3], i + 1)), pr);
+        rput(R, 188 + 14 * i + 13, 1, pr ? 1u : 0u);
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {               // opponent reserved, hidden -> zeros :158-168
         const bool pr = i < on && ((orev >> i) & 1);
-        put_card13(row, 230 + 14 * i, card_rec(L, (int)bget(op[3], i + 1)), pr);
-        row[230 + 14 * i + 13] = pr ? 1 : 0;
+        rput_card13(R, 230 + 14 * i, card_rec(L, (int)bget(op[3], i + 1)), pr);
+        rput(R, 230 + 14 * i + 13, 1, pr ? 1u : 0u);
     }
     const int nn = (int)bget(sw[SW_DECK], 3);
     const uint32_t owners = (sw[SW_NOB1] >> 8) & 0x7FFFu;
@@ -767,17 +785,22 @@ __device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *row, const 
         const int idx = (int)bget(sw[SW_NOB0], i);
         const bool pr = i < nn && ((owners >> (3 * i)) & 7u) == 0 && idx < 10;
         const uint2 rec = L.nobles[idx < 10 ? idx : 0];
-        put4(row, 272 + 6 * i, pr ? rec.x : 0u);
-        row[272 + 6 * i + 4] = pr ? (uint8_t)rec.y : (uint8_t)0;
-        row[272 + 6 * i + 5] = pr ? (uint8_t)(rec.y >> 8) : (uint8_t)0;
+        rput(R, 272 + 6 * i, 4, pr ? rec.x : 0u);
+        rput(R, 276 + 6 * i, 2, pr ? rec.y : 0u);
     }
-    row[290] = (uint8_t)sw[SW_DECK];            // deck sizes :180-181
-    row[291] = (uint8_t)(sw[SW_DECK] >> 8);
-    row[292] = (uint8_t)(sw[SW_DECK] >> 16);
-    row[293] = (uint8_t)get_turn(sw);           // misc :183-186
-    row[294] = (uint8_t)tp;
-    row[295] = (uint8_t)get_moves(sw);          // > 255 patched after the block store
-    row[296] = is_terminal(sw) ? 1 : 0;
+    rput(R, 290, 3, sw[SW_DECK]);               // deck sizes :180-181
+    rput(R, 293, 1, (uint32_t)get_turn(sw));    // misc :183-186
+    rput(R, 294, 1, (uint32_t)tp);
+    rput(R, 295, 1, (uint32_t)get_moves(sw));   // > 255 patched after the block store
+    rput(R, 296, 1, is_terminal(sw) ? 1u : 0u);
+    // bytes 297..299: the next lane's row bytes 0..2 (its bank counts)
+    R[74] |= (uint32_t)__shfl_down((int)R[0], 1) << 8;
+    const int lane = lane_id();
+    const uint32_t o0 = (4u - ((uint32_t)lane & 3u)) & 3u;  // row 297*lane starts at lane mod 4
+    uint32_t *dst = reinterpret_cast<uint32_t *>(rows_base + kObsDim * lane + o0);
+#pragma unroll
+    for (int j = 0; j < 74; ++j) dst[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], o0);
+    if (o0 == 0u) dst[74] = R[74];
 }
 
 // Block store of this wave's staged rows: obs[t0 .. t0+rows) as int32, 16 B per lane-store.
@@ -794,8 +817,8 @@ __device__ __forceinline__ v4i expand4(uint32_t w) {
 }
 
 // Part [d0, d1) (LDS words, multiples of 64*5 except the end) of a FULL wave's observation block.
-__device__ __forceinline__ void store_obs_range(const BlockLDS &L, int32_t *dst, int d0, int d1) {
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(L.rows);
+__device__ __forceinline__ void store_obs_range(const uint8_t *rows_lds, int32_t *dst, int d0, int d1) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
     v4i *out = reinterpret_cast<v4i *>(dst);
     constexpr int U = 5;
     int d = d0 + lane_id();
@@ -819,10 +842,10 @@ constexpr int kObsSplit = 64 * 5 * 7;             // 2240: 35 stores per lane in
 
 // Block store of this wave's observation rows: LDS bytes [rows][297] -> int32 [rows][297] at
 // dst (16-byte aligned: 64-row blocks are 76032 B).  Dword d of the block is LDS word d.
-__device__ __forceinline__ void store_obs_block(const BlockLDS &L, int rows, int32_t *dst) {
+__device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int rows, int32_t *dst) {
     const int nbytes = rows * kObsDim;
     const int full = nbytes >> 2;
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(L.rows);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
     v4i *out = reinterpret_cast<v4i *>(dst);
     constexpr int U = 5;
     int d = lane_id();
@@ -845,30 +868,30 @@ __device__ __forceinline__ void store_obs_block(const BlockLDS &L, int rows, int
         return;
     }
     for (; d < full; d += 64) out[d] = expand4(src[d]);
-    for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) dst[b] = (int32_t)L.rows[b];
+    for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) dst[b] = (int32_t)rows_lds[b];
 }
 
 // Block store of this wave's masks: mask[t0 .. t0+rows) as int8 [rows][45].  The 64 x 45 mask
 // bits are first laid out as ONE bit stream in LDS (row r at bits 45r..45r+44; each stream
 // dword is cut from at most two rows), so every output dword is one nibble of the stream,
 // spread to 4 bytes by a multiply: bit i of n moves to bit 8i in n * 0x204081.
-__device__ __forceinline__ void store_mask_block(BlockLDS &L, int rows, int8_t *dst) {
+__device__ __forceinline__ void store_mask_block(const uint64_t *mask, uint32_t *mbits, int rows, int8_t *dst) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int w = lane_id() + 64 * k;  // stream dword w: bits 32w .. 32w+31
         if (w < kMaskStreamWords) {
             const int r0 = (32 * w) / 45, c0 = 32 * w - 45 * r0;  // first bit: row r0, column c0
-            const uint64_t m0 = L.mask[r0], m1 = r0 + 1 < 64 ? L.mask[r0 + 1] : 0ull;
+            const uint64_t m0 = mask[r0], m1 = r0 + 1 < 64 ? mask[r0 + 1] : 0ull;
             // columns c0..44 of row r0, then row r0+1 from column 0
             const uint64_t lo = m0 >> c0, hi = (c0 > 13) ? (m1 << (45 - c0)) : 0ull;
-            L.mbits[w] = (uint32_t)(lo | hi);
+            mbits[w] = (uint32_t)(lo | hi);
         }
     }
     wave_lds_sync();
     if (rows == 64 && ((uintptr_t)dst & 15u) == 0) {  // 180 x 16 B: 3 stores per lane
         v4i *out4 = reinterpret_cast<v4i *>(dst);
         for (int c = lane_id(); c < 180; c += 64) {
-            const uint32_t half = (L.mbits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;  // stream bits 16c..16c+15
+            const uint32_t half = (mbits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;  // stream bits 16c..16c+15
             v4i v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = (int)((((half >> (4 * q)) & 0xFu) * 0x00204081u) & 0x01010101u);
@@ -880,11 +903,11 @@ __device__ __forceinline__ void store_mask_block(BlockLDS &L, int rows, int8_t *
     const int full = nbytes >> 2;
     uint32_t *out = reinterpret_cast<uint32_t *>(dst);
     for (int d = lane_id(); d < full; d += 64) {
-        const uint32_t nib = (L.mbits[d >> 3] >> (4 * (d & 7))) & 0xFu;
+        const uint32_t nib = (mbits[d >> 3] >> (4 * (d & 7))) & 0xFu;
         out[d] = (nib * 0x00204081u) & 0x01010101u;
     }
     for (int b = (full << 2) + lane_id(); b < nbytes; b += 64)
-        dst[b] = (int8_t)((L.mbits[b >> 5] >> (b & 31)) & 1u);
+        dst[b] = (int8_t)((mbits[b >> 5] >> (b & 31)) & 1u);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1055,13 +1078,13 @@ __device__ __forceinline__ void store_tab(const Tab<P> &T, const KArena &A, int 
         for (int k = 0; k < 4; ++k) A.planes[(size_t)pw_index(q, k) * A.n + t] = T.pw[q][k];
 }
 
-__device__ __forceinline__ void load_tables_lds(BlockLDS &L, const KTables &Tb) {
+__device__ __forceinline__ void load_tables_lds(Consts &L, const KTables &Tb) {
     for (int i = lane_id(); i < 90; i += 64) L.cards[i] = Tb.cards[i];
     if (lane_id() < 10) L.nobles[lane_id()] = Tb.nobles[lane_id()];
 }
 
 template <int P>
-__device__ __forceinline__ uint64_t legal_of(const Tab<P> &T, const BlockLDS &L) {
+__device__ __forceinline__ uint64_t legal_of(const Tab<P> &T, const Consts &L) {
     uint32_t w[4];
     get_player(T, get_to_play(T.sw), w);
     const Pl p = unpack_pl(w);
@@ -1099,7 +1122,7 @@ constexpr uint64_t kTake2Bits = 0x1Full << 10, kTake3Bits = 0x3FFull, kReserveBi
 __device__ __forceinline__ int lowest_action(uint64_t m) { return m ? __ffsll((unsigned long long)m) - 1 : 0; }
 
 template <int P>
-__device__ __forceinline__ int policy_action(int policy, uint64_t m, const Tab<P> &T, const BlockLDS &L,
+__device__ __forceinline__ int policy_action(int policy, uint64_t m, const Tab<P> &T, const Consts &L,
                                              uint64_t seed, uint64_t table, uint64_t ply) {
     if (policy == SPL_POLICY_GREEDY_V1) {  // eval_suite.py:9-29: first legal buy, take-2, take-3, reserve
         const uint64_t pick = (m & kBuyBits) ? (m & kBuyBits)
@@ -1203,7 +1226,7 @@ struct StepOut {
 // step): `known_mask` is legal_moves of the table's current state, computed by the previous step,
 // so "any legal move?" and mask[action] need no re-evaluation.
 template <int P>
-__device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepPre &pre, bool valid, const BlockLDS &L,
+__device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepPre &pre, bool valid, const Consts &L,
                                               const KTables &Tb, bool known = false, uint64_t known_mask = 0ull) {
     StepOut o{0u, 0.0f, false, 0ull};
     bool want_mask = false;
@@ -1287,6 +1310,24 @@ __device__ __forceinline__ bool flip_to_pool(Tab<P> &T, const KArena &A, int t, 
     return pend2 < kPools;
 }
 
+// One pool refill of table t (spl_refill's unit of work; status `misc` has pend > 0): re-deal the
+// earliest consumed record in ring order (the next episode's deal comes first in the engine-seed
+// stream).  When that record is the next pool, its words go to `pool` (`pool_dirty`).  Returns
+// the new status word.
+template <int P>
+__device__ __forceinline__ uint32_t refill_table(const KArena &A, int t, uint32_t misc, uint8_t *scr, Deal &pool,
+                                                 bool &pool_dirty) {
+    const int pend = pend_of(misc);
+    const int slot = (active_of(misc) + kSlotRecords - pend) % kSlotRecords;
+    Deal d;
+    deal_next<P>(A, t, slot, scr, d);
+    if (pend == kSlotRecords - 1) {
+        pool = d;
+        pool_dirty = true;
+    }
+    return (misc & ~ST_PEND) | ((uint32_t)(pend - 1) << ST_PEND_SHIFT);
+}
+
 // same-step autoreset of a terminal table; `pool_dirty` is set when the pool planes changed
 template <int P>
 __device__ __forceinline__ void autoreset_table(Tab<P> &T, const KArena &A, int t, Deal &pool, uint8_t *scr,
@@ -1297,12 +1338,12 @@ __device__ __forceinline__ void autoreset_table(Tab<P> &T, const KArena &A, int 
 }
 
 // Terminal rows staged in L.frows (bits of `fin`) -> final_obs rows of this wave.
-__device__ __forceinline__ void store_final_rows(const BlockLDS &L, uint64_t fin, int32_t *final_obs, int t0) {
+__device__ __forceinline__ void store_final_rows(const uint8_t *rows_lds, uint64_t fin, int32_t *final_obs, int t0) {
     while (fin) {
         const int r = __ffsll((unsigned long long)fin) - 1;
         fin &= fin - 1;
         int32_t *dst = final_obs + (size_t)(t0 + r) * kObsDim;
-        for (int e = lane_id(); e < kObsDim; e += 64) dst[e] = (int32_t)L.frows[r * kObsDim + e];
+        for (int e = lane_id(); e < kObsDim; e += 64) dst[e] = (int32_t)rows_lds[r * kObsDim + e];
     }
 }
 
@@ -1350,7 +1391,7 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     // with everything else at the end
     const bool want_final = S.autoreset && S.final_obs != nullptr && !abl(ABL_FINAL);
     const uint64_t fin = __ballot(ended && want_final);
-    if (ended && want_final) encode_row(T, &L.frows[lane * kObsDim], L);
+    if (__any(ended && want_final)) encode_row(T, L.frows, L);  // rows of other lanes are not stored
     const int fin_moves = get_moves(T.sw);
     const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;
     STAMP(5);
@@ -1361,17 +1402,17 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     wave_lds_sync();  // deal scratch (rows) free again
 
     // observation + mask of the current state, block stores
-    if (!abl(ABL_ENCODE)) encode_row(T, &L.rows[lane * kObsDim], L);
+    if (!abl(ABL_ENCODE)) encode_row(T, L.rows, L);
     L.mask[lane] = o.mask;
     STAMP(7);
     wave_lds_sync();
     STAMP(8);
     if (!abl(ABL_STORE)) {
-        if (!abl(ABL_OBS_STORE)) store_obs_block(L, rows, S.obs + (size_t)t0 * kObsDim);
+        if (!abl(ABL_OBS_STORE)) store_obs_block(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
         STAMP(9);
-        if (!abl(ABL_MASK_STORE)) store_mask_block(L, rows, S.mask + (size_t)t0 * 45);
+        if (!abl(ABL_MASK_STORE)) store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
     }
-    store_final_rows(L, fin, S.final_obs, t0);
+    store_final_rows(L.frows, fin, S.final_obs, t0);
     STAMP(10);
     if (valid && o.term) {  // no-return atomics: nothing to wait for
         if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_add);
@@ -1410,9 +1451,17 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
 // next step's deck-card / token-table gathers are issued a whole step ahead.  Step k's outputs
 // go to block k of each output array when `per_step` (rollout storage [K][n][...]), else every
 // step overwrites block 0.
+//
+// refill != 0 (a pool refill is due in this launch): the refill is fused — each wave re-deals its
+// tables' earliest consumed pool record (k_refill's work) at a step of its own, spread over the
+// K steps.  The deal is a long serial integer chain per lane; inside the rollout it runs while
+// this wave's stores drain and the other waves keep HBM busy, where a separate k_refill launch
+// leaves HBM idle for its whole duration.  Trajectories do not depend on when a refill happens
+// (deals are taken from each table's engine-seed stream in episode order either way).
 template <int P>
-__global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, int K, int per_step) {
+__global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, int K, int per_step, int refill) {
     __shared__ BlockLDS L;
+    const int refill_k = (refill && S.autoreset) ? (int)(((blockIdx.x * 0x9E3779B1u) >> 16) % (uint32_t)K) : -1;
     const int lane = lane_id();
     const int t0 = blockIdx.x * 64;
     const int t = t0 + lane;
@@ -1449,12 +1498,17 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         RSTAMP(0, k);
         StepOut o = step_rules(T, action, pre, valid, L, Tb, k > 0, cur_mask);
         RSTAMP(1, k);
-        if (obs_tail) store_obs_range(L, obs_tail, kObsSplit, kObsBlockWords);
+        if (obs_tail) store_obs_range(L.rows, obs_tail, kObsSplit, kObsBlockWords);
         obs_tail = nullptr;
+        if (k == refill_k) {  // fused pool refill (wave-uniform)
+            wave_lds_sync();  // the tail's LDS reads are done: the rows serve as deal scratch
+            if (valid && pend_of(T.sw[SW_MISC]) > 0)
+                T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], &L.rows[lane * kScratchStride], pool, pool_dirty);
+        }
         RSTAMP(2, k);
         const int8_t wnr = (int8_t)get_winner(T.sw);
         const uint64_t fin = __ballot(valid && o.term && want_final);
-        if (valid && o.term && want_final) encode_row(T, &L.frows[lane * kObsDim], L);
+        if (__any(valid && o.term && want_final)) encode_row(T, L.frows, L);  // rows of other lanes are not stored
         const int fin_moves = get_moves(T.sw);
         if (valid && o.term) {  // per termination, as k_step (same float rounding)
             if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], final_reward_p0(T));
@@ -1462,7 +1516,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         }
         if (valid && o.term && S.autoreset) autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], o, pool_dirty);
         wave_lds_sync();
-        encode_row(T, &L.rows[lane * kObsDim], L);
+        if (!abl(ABL_ENCODE)) encode_row(T, L.rows, L);
         L.mask[lane] = o.mask;
         wave_lds_sync();
         RSTAMP(3, k);
@@ -1474,15 +1528,16 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         const bool patch = valid && get_moves(T.sw) > 255;
         const bool fpatch = valid && o.term && want_final && fin_moves > 255;
         const bool split = rows == 64 && !__any(patch || fpatch);  // crafted states store at once
-        if (split) {
-            store_obs_range(L, obs + (size_t)t0 * kObsDim, 0, kObsSplit);
+        if (abl(ABL_OBS_STORE)) {
+        } else if (split) {
+            store_obs_range(L.rows, obs + (size_t)t0 * kObsDim, 0, kObsSplit);
             obs_tail = obs + (size_t)t0 * kObsDim;
         } else {
-            store_obs_block(L, rows, obs + (size_t)t0 * kObsDim);
+            store_obs_block(L.rows, rows, obs + (size_t)t0 * kObsDim);
         }
-        store_mask_block(L, rows, S.mask + blk * 45 + (size_t)t0 * 45);
+        store_mask_block(L.mask, L.mbits, rows, S.mask + blk * 45 + (size_t)t0 * 45);
         int32_t *fobs = want_final ? S.final_obs + blk * kObsDim : nullptr;
-        if (want_final) store_final_rows(L, fin, fobs, t0);
+        if (want_final) store_final_rows(L.frows, fin, fobs, t0);
         if (!split && __any(patch || fpatch)) {  // move_count > 255: crafted states only (see k_step)
             __builtin_amdgcn_s_waitcnt(0);
             if (patch) obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
@@ -1496,7 +1551,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         }
         RSTAMP(4, k);
     }
-    if (obs_tail) store_obs_range(L, obs_tail, kObsSplit, kObsBlockWords);
+    if (obs_tail) store_obs_range(L.rows, obs_tail, kObsSplit, kObsBlockWords);
 #ifdef SPL_STAMPS
     if (g_rstamps) {
         RSTAMP(5, 0);  // kernel end for this wave (lane 0)
@@ -1557,11 +1612,11 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
     }
     wave_lds_sync();
     if (obs || mask_out) {
-        encode_row(T, &L.rows[lane * kObsDim], L);
+        encode_row(T, L.rows, L);
         L.mask[lane] = (valid && !is_terminal(T.sw)) ? legal_of(T, L) : 0ull;  // env info mask
         wave_lds_sync();
-        if (obs) store_obs_block(L, rows, obs + (size_t)t0 * kObsDim);
-        if (mask_out) store_mask_block(L, rows, mask_out + (size_t)t0 * 45);
+        if (obs) store_obs_block(L.rows, rows, obs + (size_t)t0 * kObsDim);
+        if (mask_out) store_mask_block(L.mask, L.mbits, rows, mask_out + (size_t)t0 * 45);
     }
     if (valid) store_tab(T, A, t);
 }
@@ -1580,14 +1635,11 @@ __global__ __launch_bounds__(64) void k_refill(KArena A) {
     if (t >= A.n) return;
     const size_t mi = (size_t)SW_MISC * A.n + t;
     const uint32_t misc = A.planes[mi];
-    const int pend = pend_of(misc);
-    if (pend == 0) return;
-    const int a = active_of(misc);
-    const int slot = (a + kSlotRecords - pend) % kSlotRecords;  // earliest free record in ring order
-    Deal d;
-    deal_next<P>(A, t, slot, &scr_all[lane_id() * kScratchStride], d);
-    if (pend == kSlotRecords - 1) store_pool(A, t, d);  // it is the next pool: words to the pool planes
-    A.planes[mi] = (misc & ~ST_PEND) | ((uint32_t)(pend - 1) << ST_PEND_SHIFT);
+    if (pend_of(misc) == 0) return;
+    Deal pool;
+    bool pool_dirty = false;
+    A.planes[mi] = refill_table<P>(A, t, misc, &scr_all[lane_id() * kScratchStride], pool, pool_dirty);
+    if (pool_dirty) store_pool(A, t, pool);  // it was the next pool: words to the pool planes
 }
 
 // Observation and/or mask of the current state (spl_encode / spl_legal).
@@ -1604,17 +1656,17 @@ __global__ __launch_bounds__(64) void k_observe(KArena A, KTables Tb, int32_t *o
     if (valid) load_tab(T, A, t);
     else fresh_state(T, 0u, empty_deal());
     wave_lds_sync();
-    if (obs) encode_row(T, &L.rows[lane * kObsDim], L);
+    if (obs) encode_row(T, L.rows, L);
     L.mask[lane] = valid ? legal_of(T, L) : 0ull;  // engine legal_moves (no terminal check)
     wave_lds_sync();
     if (obs) {
-        store_obs_block(L, rows, obs + (size_t)t0 * kObsDim);
+        store_obs_block(L.rows, rows, obs + (size_t)t0 * kObsDim);
         if (__any(valid && get_moves(T.sw) > 255)) {
             __builtin_amdgcn_s_waitcnt(0);
             if (valid && get_moves(T.sw) > 255) obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
         }
     }
-    if (mask_out) store_mask_block(L, rows, mask_out + (size_t)t0 * 45);
+    if (mask_out) store_mask_block(L.mask, L.mbits, rows, mask_out + (size_t)t0 * 45);
 }
 
 __global__ __launch_bounds__(64) void k_sample(int n, const int8_t *mask, int32_t *actions, uint64_t seed, uint64_t ply,
@@ -1766,6 +1818,7 @@ struct spl_ctx_s {
     uint2 *nobles;
     uint4 *lut;
     int refill_period;
+    int refill_fused;  // spl_rollout: refill inside the rollout launch (default) or as a k_refill launch after it
     void *stage;
     size_t stage_bytes;
 };
@@ -1871,6 +1924,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     spl_ctx_t *c = new spl_ctx_t();
     c->device = device;
     c->refill_period = 64;
+    c->refill_fused = 1;
     if (hipMalloc(&c->cards, sizeof(uint4) * 90) != hipSuccess || hipMalloc(&c->nobles, sizeof(uint2) * 10) != hipSuccess ||
         hipMalloc(&c->lut, sizeof(uint4) * kLutEntries) != hipSuccess) {
         spl_ctx_destroy(c);
@@ -1901,6 +1955,12 @@ int spl_ctx_destroy(spl_ctx_t *ctx) {
 int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period) {
     if (!ctx || period < 0) return fail(SPL_E_ARG, "bad refill period");
     ctx->refill_period = period;
+    return SPL_OK;
+}
+
+int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused) {
+    if (!ctx) return fail(SPL_E_ARG, "null ctx");
+    ctx->refill_fused = fused != 0;
     return SPL_OK;
 }
 
@@ -2017,13 +2077,16 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     const KStep S = kstep(a);
     const KArena A = karena(arena);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_rollout<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
-                                                  ktables(ctx), S, (int)steps, (int)(per_step_outputs != 0)));
-    if (int r = launch_check()) return r;
     const int64_t before = arena->steps;
+    const bool due = a->autoreset && ctx->refill_period > 0 &&
+                     (before + steps) / ctx->refill_period != before / ctx->refill_period;
+    const int fused = due && ctx->refill_fused;
+    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_rollout<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
+                                                  ktables(ctx), S, (int)steps, (int)(per_step_outputs != 0), fused));
+    if (int r = launch_check()) return r;
     arena->steps += steps;
-    if (a->autoreset && ctx->refill_period > 0 && arena->steps / ctx->refill_period != before / ctx->refill_period)
-        return spl_refill(ctx, arena, stream);
+    if (fused) arena->epoch += 1;
+    else if (due) return spl_refill(ctx, arena, stream);
     return SPL_OK;
 }
 

@@ -198,14 +198,16 @@ def test_unseeded_tables_deal_engine_seed_zero(orc):
     assert canon(table_to_view(recs[5])) == want
 
 
-@pytest.mark.parametrize("P", [2, 4])
-def test_rollout_equals_step_chain(P):
+@pytest.mark.parametrize("P,K,refill_fused", [(2, 16, True), (4, 16, True), (2, 16, False), (2, 64, True)])
+def test_rollout_equals_step_chain(P, K, refill_fused):
     """spl_rollout(K) is K chained spl_step calls (next_actions fed back, plies ply..ply+K-1):
     every per-step output, the terminal rows of final_obs, episode statistics, the next action
-    and the table state match bit for bit, across launches with refills in between."""
+    and the table state match bit for bit, across launches with refills in between — refills
+    fused into the rollout launch (each wave at its own step) or launched after it."""
     import torch
-    n, K, launches, seed = 1024, 16, 5, 11
-    chain, fused = engine(n, P, refill_period=K), engine(n, P, refill_period=K)
+    n, launches, seed = 1024, 5 if K <= 16 else 3, 11
+    chain = engine(n, P, refill_period=K)
+    fused = engine(n, P, refill_period=K, refill_fused=refill_fused)
     chain.reset(seeds=range(n))
     fused.reset(seeds=range(n))
     dev = chain.device
