@@ -41,7 +41,7 @@ ALGO_BYTES = {2: 1370, 3: 1408, 4: 1446}  # 2*S_P + 297*4 + 45 +
 # pool refill period per player count: three pool deals per table must cover the resets between
 # refills (random games last ~77 plies at 2p, ~29 at 4p)
 REFILL_EVERY = {2: 64, 3: 32, 4: 16}
-ROLLOUT_K = 16     # env steps per spl_rollout launch
+ROLLOUT_K = 64     # env steps per spl_rollout launch (one fused pool refill per launch at 2p)
 
 
 def cpu_baseline(players, procs, steps_per_proc):

@@ -115,6 +115,10 @@ int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period);
  * of its own while other waves' stores keep HBM busy; 0 = a separate spl_refill launch after it.
  * Results are identical either way. */
 int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused);
+/* spl_rollout only: 1 (default) = the two-wave pipelined kernel for 2-player arenas (one wave
+ * steps the tables, the other encodes and stores the step's outputs); 0 = one wave per 64 tables.
+ * Results are identical either way. */
+int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
 
 int64_t spl_arena_bytes(int32_t n, int32_t players);
 /* Zero the arena and mark every table's pool as not dealt (must precede the first spl_reset

@@ -737,14 +737,11 @@ __device__ __forceinline__ void rput_card13(uint32_t (&R)[76], int o, uint4 rec,
     rput(R, o + 12, 1, present ? rec.w : 0u);
 }
 
-// Row of table T into rows_base[297*lane ...].  Every lane of the wave must call it (the row
-// boundaries are shared with the neighbouring lanes); rows of lanes whose table is not needed
-// are written too and simply not stored.
+// The 297 observation bytes of table T as dwords R[0..74] (R[75] = 0).
 template <int P>
-__device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *rows_base, const Consts &L) {
+__device__ __forceinline__ void build_row(const Tab<P> &T, const Consts &L, uint32_t (&R)[76]) {
     const uint32_t *sw = T.sw;
     const int tp = get_to_play(sw);
-    uint32_t R[76];
 #pragma unroll
     for (int j = 0; j < 76; ++j) R[j] = 0u;
     rput(R, 0, 4, sw[SW_BANK0]);                // bank :128
@@ -793,6 +790,15 @@ __device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *rows_base, 
     rput(R, 294, 1, (uint32_t)tp);
     rput(R, 295, 1, (uint32_t)get_moves(sw));   // > 255 patched after the block store
     rput(R, 296, 1, is_terminal(sw) ? 1u : 0u);
+}
+
+// Row of table T into rows_base[297*lane ...].  Every lane of the wave must call it (the row
+// boundaries are shared with the neighbouring lanes); rows of lanes whose table is not needed
+// are written too and simply not stored.
+template <int P>
+__device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *rows_base, const Consts &L) {
+    uint32_t R[76];
+    build_row(T, L, R);
     // bytes 297..299: the next lane's row bytes 0..2 (its bank counts)
     R[74] |= (uint32_t)__shfl_down((int)R[0], 1) << 8;
     const int lane = lane_id();
@@ -801,6 +807,16 @@ __device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *rows_base, 
 #pragma unroll
     for (int j = 0; j < 74; ++j) dst[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], o0);
     if (o0 == 0u) dst[74] = R[74];
+}
+
+// Observation of table T written by its own lane straight to dst[0..296] (int32; 297 dword
+// stores): the rare path for terminal rows that do not fit the pipelined kernel's hand-off.
+template <int P>
+__device__ __forceinline__ void store_row_direct(const Tab<P> &T, const Consts &L, int32_t *dst) {
+    uint32_t R[76];
+    build_row(T, L, R);
+#pragma unroll
+    for (int e = 0; e < kObsDim; ++e) dst[e] = e == 295 ? get_moves(T.sw) : (int32_t)bget(R[e >> 2], e & 3);
 }
 
 // Block store of this wave's staged rows: obs[t0 .. t0+rows) as int32, 16 B per lane-store.
@@ -1568,6 +1584,170 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
     }
 }
 
+// ---- two-wave pipelined rollout -----------------------------------------------------------
+// k_rollout as a two-stage pipeline per 64 tables: workgroup = 2 waves, lane l of both = table
+// t0 + l.  The RULES wave runs the steps (SplendorEnv.step, autoreset, policy, small outputs,
+// fused refill) and hands each step's table state to the OUTPUT wave through LDS; the output
+// wave encodes the observation rows (and the terminal rows) and issues the step's block stores
+// while the rules wave already computes the next step.  With one wave per table block, a step
+// was the rules' dependency chains PLUS the store issue stalls of one instruction stream
+// (k_rollout: 12.4 us of the 15 us step with the observation stores compiled out); split over
+// two waves on two SIMDs, the step costs the longer of the two stages.
+//
+// Hand-off per step k (buffers k & 1, so the rules wave refills buffer b only after the output
+// wave has passed the next barrier, i.e. finished with it): the state words after the step
+// (post-autoreset), the info mask, and the terminal (pre-autoreset) states of the first kWsTerm
+// terminal lanes; the rules wave writes any further terminal rows itself (store_row_direct).
+// One s_barrier per step; LDS ordering by lgkmcnt(0) only — a workgroup fence would add
+// vmcnt(0) and make each wave wait for its own global stores.
+constexpr int kWsTerm = 16;
+
+template <int P>
+struct __align__(16) WsLDS : Consts {
+    static constexpr int kW = SW_COUNT + 4 * P;  // state words per table
+    uint32_t st[2][kW][64];
+    uint32_t tst[2][kWsTerm][kW];
+    uint64_t mask[2][64];
+    uint64_t fin[2];
+    uint32_t mbits[96];
+    uint8_t rows[64 * kObsDim];
+    uint8_t scr[64 * kScratchStride];  // the rules wave's deal scratch
+};
+
+template <int P>
+__device__ __forceinline__ uint32_t tab_word(const Tab<P> &T, int w) {
+    return w < SW_COUNT ? T.sw[w] : T.pw[(w - SW_COUNT) >> 2][(w - SW_COUNT) & 3];
+}
+template <int P>
+__device__ __forceinline__ void set_tab_word(Tab<P> &T, int w, uint32_t v) {
+    if (w < SW_COUNT) T.sw[w] = v;
+    else T.pw[(w - SW_COUNT) >> 2][(w - SW_COUNT) & 3] = v;
+}
+
+__device__ __forceinline__ void ws_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes have landed
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+
+template <int P>
+__global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep S, int K, int per_step, int refill) {
+    __shared__ WsLDS<P> L;
+    constexpr int kW = WsLDS<P>::kW;
+    const int lane = lane_id();
+    const bool rules_wave = threadIdx.x < 64;
+    const int t0 = blockIdx.x * 64;
+    const int t = t0 + lane;
+    const bool valid = t < A.n;
+    const int rows = min(64, A.n - t0);
+    const bool want_final = S.autoreset && S.final_obs != nullptr;
+    load_tables_lds(L, Tb);
+    ws_sync();
+
+    if (rules_wave) {
+        const int refill_k = (refill && S.autoreset) ? (int)(((blockIdx.x * 0x9E3779B1u) >> 16) % (uint32_t)K) : -1;
+        uint8_t *scr = &L.scr[lane * kScratchStride];
+        Tab<P> T;
+        int action = 0;
+        Deal pool = empty_deal();
+        if (valid) {
+            load_tab(T, A, t);
+            action = S.actions[t];
+            if (S.autoreset) pool = load_pool(A, t);
+        } else {
+            fresh_state(T, 0u, empty_deal());
+        }
+        StepPre pre = step_prefetch(T, action, valid, A, t, Tb);
+        bool pool_dirty = false;
+        const uint64_t ply0 = S.ply + (S.ply_base ? *S.ply_base : 0ull);
+        uint64_t cur_mask = 0ull;
+        const uint64_t below = (1ull << lane) - 1ull;
+        for (int k = 0; k < K; ++k) {
+            const int b = k & 1;
+            const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
+            StepOut o = step_rules(T, action, pre, valid, L, Tb, k > 0, cur_mask);
+            if (k == refill_k && valid && pend_of(T.sw[SW_MISC]) > 0)  // fused pool refill
+                T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], scr, pool, pool_dirty);
+            const int8_t wnr = (int8_t)get_winner(T.sw);
+            const bool fin_me = valid && o.term && want_final;
+            const uint64_t fin_all = __ballot(fin_me);
+            const int idx = __popcll(fin_all & below);
+            if (fin_me) {  // the terminal state, before the autoreset replaces it
+                if (idx < kWsTerm) {
+#pragma unroll
+                    for (int w = 0; w < kW; ++w) L.tst[b][idx][w] = tab_word(T, w);
+                } else {
+                    store_row_direct(T, L, S.final_obs + (blk + (size_t)t) * kObsDim);
+                }
+            }
+            if (valid && o.term) {  // per termination, as k_step (same float rounding)
+                if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], final_reward_p0(T));
+                if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
+            }
+            if (valid && o.term && S.autoreset) autoreset_table(T, A, t, pool, scr, o, pool_dirty);
+            if (valid) {
+                S.reward[blk + t] = o.reward;
+                S.terminated[blk + t] = o.term ? 1 : 0;
+                S.flags[blk + t] = (uint8_t)o.flags;
+                if (S.winner) S.winner[blk + t] = wnr;
+            }
+            action = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
+            cur_mask = o.mask;
+            if (k + 1 < K) pre = step_prefetch(T, action, valid, A, t, Tb);
+#pragma unroll
+            for (int w = 0; w < kW; ++w) L.st[b][w][lane] = tab_word(T, w);
+            L.mask[b][lane] = o.mask;
+            const uint64_t fin_listed = __ballot(fin_me && idx < kWsTerm);  // outside the lane-0 branch
+            if (lane == 0) L.fin[b] = fin_listed;
+            ws_sync();  // hand-off of step k
+        }
+        if (valid) {
+            if (S.next_actions) S.next_actions[t] = action;
+            store_tab(T, A, t);
+            if (pool_dirty) store_pool(A, t, pool);
+        }
+    } else {
+        const uint64_t below = (1ull << lane) - 1ull;
+        for (int k = 0; k < K; ++k) {
+            ws_sync();  // hand-off of step k
+            const int b = k & 1;
+            const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
+            Tab<P> T;
+#pragma unroll
+            for (int w = 0; w < kW; ++w) set_tab_word(T, w, L.st[b][w][lane]);
+            const uint64_t fin = L.fin[b];
+            if (fin) {  // terminal rows (info["final_observation"]) first, through the same rows
+                int32_t *fobs = S.final_obs + blk * kObsDim;
+                const bool mine = (fin >> lane) & 1ull;
+                const int idx = __popcll(fin & below);
+                Tab<P> F = T;
+                if (mine) {
+#pragma unroll
+                    for (int w = 0; w < kW; ++w) set_tab_word(F, w, L.tst[b][idx][w]);
+                }
+                encode_row(F, L.rows, L);
+                wave_lds_sync();
+                store_final_rows(L.rows, fin, fobs, t0);
+                if (__any(mine && get_moves(F.sw) > 255)) {  // move_count > 255: crafted states only
+                    __builtin_amdgcn_s_waitcnt(0);
+                    if (mine && get_moves(F.sw) > 255) fobs[(size_t)t * kObsDim + 295] = get_moves(F.sw);
+                }
+                wave_lds_sync();  // the final rows' LDS reads are done
+            }
+            encode_row(T, L.rows, L);
+            wave_lds_sync();
+            int32_t *obs = S.obs + blk * kObsDim;
+            store_obs_block(L.rows, rows, obs + (size_t)t0 * kObsDim);
+            store_mask_block(L.mask[b], L.mbits, rows, S.mask + blk * 45 + (size_t)t0 * 45);
+            if (__any(valid && get_moves(T.sw) > 255)) {
+                __builtin_amdgcn_s_waitcnt(0);
+                if (valid && get_moves(T.sw) > 255) obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
+            }
+        }
+    }
+}
+
 // Explicit reset (SplendorEnv.reset / VectorEnv.reset), then observation + mask of all tables.
 template <int P>
 __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64_t *pcg_in, const uint8_t *mask_in,
@@ -1819,6 +1999,7 @@ struct spl_ctx_s {
     uint4 *lut;
     int refill_period;
     int refill_fused;  // spl_rollout: refill inside the rollout launch (default) or as a k_refill launch after it
+    int pipeline;      // spl_rollout: two-wave pipelined kernel where its LDS fits (2 players)
     void *stage;
     size_t stage_bytes;
 };
@@ -1925,6 +2106,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     c->device = device;
     c->refill_period = 64;
     c->refill_fused = 1;
+    c->pipeline = 1;
     if (hipMalloc(&c->cards, sizeof(uint4) * 90) != hipSuccess || hipMalloc(&c->nobles, sizeof(uint2) * 10) != hipSuccess ||
         hipMalloc(&c->lut, sizeof(uint4) * kLutEntries) != hipSuccess) {
         spl_ctx_destroy(c);
@@ -1955,6 +2137,12 @@ int spl_ctx_destroy(spl_ctx_t *ctx) {
 int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period) {
     if (!ctx || period < 0) return fail(SPL_E_ARG, "bad refill period");
     ctx->refill_period = period;
+    return SPL_OK;
+}
+
+int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on) {
+    if (!ctx) return fail(SPL_E_ARG, "null ctx");
+    ctx->pipeline = on != 0;
     return SPL_OK;
 }
 
@@ -2081,8 +2269,12 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     const bool due = a->autoreset && ctx->refill_period > 0 &&
                      (before + steps) / ctx->refill_period != before / ctx->refill_period;
     const int fused = due && ctx->refill_fused;
-    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_rollout<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
-                                                  ktables(ctx), S, (int)steps, (int)(per_step_outputs != 0), fused));
+    if (ctx->pipeline && arena->players == 2)  // WsLDS<2> fits four workgroups per CU; 3-4 players do not
+        hipLaunchKernelGGL(k_rollout_ws<2>, dim3(blocks_for(arena->n)), dim3(128), 0, s, A, ktables(ctx), S, (int)steps,
+                           (int)(per_step_outputs != 0), fused);
+    else
+        DISPATCH_P(arena->players, hipLaunchKernelGGL(k_rollout<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
+                                                      ktables(ctx), S, (int)steps, (int)(per_step_outputs != 0), fused));
     if (int r = launch_check()) return r;
     arena->steps += steps;
     if (fused) arena->epoch += 1;

@@ -21,13 +21,15 @@ class Engine:
     so results do not depend on how tables are split across GPUs.
     refill_period / refill_fused: pool refill every `refill_period` steps; rollout() runs a due
     refill inside its launch unless refill_fused is False (results are the same either way).
+    pipeline: rollout() uses the two-wave pipelined kernel (2 players; same results).
     """
 
     # pool refill period by player count (three pool deals per table cover the resets in between;
     # random games last ~77 plies at 2p, ~29 at 4p)
     DEFAULT_REFILL = {2: 64, 3: 32, 4: 16}
 
-    def __init__(self, num_tables, num_players=2, device=None, refill_period=None, table0=0, refill_fused=True):
+    def __init__(self, num_tables, num_players=2, device=None, refill_period=None, table0=0, refill_fused=True,
+                 pipeline=True):
         torch = _native.require_gpu()
         self.torch = torch
         self.lib = _native.load_library()
@@ -50,6 +52,8 @@ class Engine:
         check(self.lib, self.lib.spl_ctx_set_refill_period(self.ctx, int(refill_period)))
         # rollout(): a due refill runs inside the rollout launch (True) or as a refill launch after it
         check(self.lib, self.lib.spl_ctx_set_refill_fused(self.ctx, 1 if refill_fused else 0))
+        # rollout(): two-wave pipelined kernel (2 players) or one wave per 64 tables; same results
+        check(self.lib, self.lib.spl_ctx_set_rollout_pipeline(self.ctx, 1 if pipeline else 0))
         nbytes = int(self.lib.spl_arena_bytes(self.n, self.P))
         dev = self.device
         self._arena_raw = torch.zeros(nbytes + 256, dtype=torch.uint8, device=dev)

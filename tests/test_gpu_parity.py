@@ -198,16 +198,18 @@ def test_unseeded_tables_deal_engine_seed_zero(orc):
     assert canon(table_to_view(recs[5])) == want
 
 
-@pytest.mark.parametrize("P,K,refill_fused", [(2, 16, True), (4, 16, True), (2, 16, False), (2, 64, True)])
-def test_rollout_equals_step_chain(P, K, refill_fused):
+@pytest.mark.parametrize("P,K,refill_fused,pipeline", [(2, 16, True, True), (2, 16, True, False), (4, 16, True, True),
+                                                        (2, 16, False, True), (2, 64, True, True), (3, 16, True, True)])
+def test_rollout_equals_step_chain(P, K, refill_fused, pipeline):
     """spl_rollout(K) is K chained spl_step calls (next_actions fed back, plies ply..ply+K-1):
     every per-step output, the terminal rows of final_obs, episode statistics, the next action
     and the table state match bit for bit, across launches with refills in between — refills
-    fused into the rollout launch (each wave at its own step) or launched after it."""
+    fused into the rollout launch (each wave at its own step) or launched after it; the two-wave
+    pipelined kernel (2 players) or one wave per 64 tables."""
     import torch
     n, launches, seed = 1024, 5 if K <= 16 else 3, 11
     chain = engine(n, P, refill_period=K)
-    fused = engine(n, P, refill_period=K, refill_fused=refill_fused)
+    fused = engine(n, P, refill_period=K, refill_fused=refill_fused, pipeline=pipeline)
     chain.reset(seeds=range(n))
     fused.reset(seeds=range(n))
     dev = chain.device
@@ -256,6 +258,64 @@ def test_rollout_equals_step_chain(P, K, refill_fused):
     for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
         assert torch.equal(getattr(chain, name), getattr(fused, name)), name
     assert torch.equal(a_c, na_f)
+
+
+@pytest.mark.parametrize("pipeline", [True, False])
+def test_rollout_mass_termination_and_long_games(pipeline):
+    """Every table of a wave ending in the same step (crafted: one move before the turn limit),
+    more than the pipelined kernel hands over per step, and final rows with move_count > 255:
+    spl_rollout equals chained spl_step, per-step outputs and final_obs rows."""
+    import torch
+    n, K, seed = 512, 8, 5
+    chain = engine(n, 2, refill_period=K)
+    roll = engine(n, 2, refill_period=K, pipeline=pipeline)
+    chain.reset(seeds=range(n))
+    roll.reset(seeds=range(n))
+    dev = chain.device
+    a = torch.zeros(n, dtype=torch.int32, device=dev)
+    chain.sample_uniform(out=a, seed=seed, ply=0)
+    for k in range(7):  # an odd number of plies in (player 1 to move), then craft
+        na = torch.empty_like(a)
+        chain.step(a, next_actions=na, policy_seed=seed, ply=100 + k)
+        a = na
+    recs = chain.download()
+    odd = (recs["move_count"] % 2) == 1
+    # tables with player 1 to move: one move before turn 100 (move_count 197) -> all end next step;
+    # every 7th of them far beyond it (crafted move_count > 255: the final row patch)
+    recs["move_count"] = np.where(odd, 197, recs["move_count"])
+    recs["turn_count"] = np.where(odd, 99, recs["turn_count"])
+    far = odd & (np.arange(n) % 7 == 0)
+    recs["move_count"] = np.where(far, 301, recs["move_count"])
+    recs["turn_count"] = np.where(far, 151, recs["turn_count"])
+    chain.upload(recs)
+    roll.upload(recs)
+    chain.sample_uniform(out=a, seed=seed, ply=0)
+    a_r = a.clone()
+    want = []
+    for k in range(K):
+        na = torch.empty_like(a)
+        chain.step(a, next_actions=na, policy_seed=seed, ply=1 + k)
+        want.append({name: getattr(chain, name).clone() for name in
+                     ("obs", "mask", "reward", "terminated", "flags", "winner", "final_obs")})
+        a = na
+    out = {"obs": torch.empty((K, n, 297), dtype=torch.int32, device=dev),
+           "mask": torch.empty((K, n, 45), dtype=torch.int8, device=dev),
+           "reward": torch.empty((K, n), dtype=torch.float32, device=dev),
+           "terminated": torch.empty((K, n), dtype=torch.uint8, device=dev),
+           "flags": torch.empty((K, n), dtype=torch.uint8, device=dev),
+           "winner": torch.empty((K, n), dtype=torch.int8, device=dev),
+           "final_obs": torch.zeros((K, n, 297), dtype=torch.int32, device=dev)}
+    na = torch.empty_like(a_r)
+    roll.rollout(K, actions=a_r, next_actions=na, policy_seed=seed, ply=1, out=out)
+    assert int(want[0]["terminated"].sum()) > 64  # whole waves ended at once
+    assert int(want[0]["final_obs"][:, 295].max()) > 255
+    for k in range(K):
+        for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
+            assert torch.equal(out[name][k], want[k][name]), (k, name)
+        term = want[k]["terminated"].bool()
+        assert torch.equal(out["final_obs"][k][term], want[k]["final_obs"][term]), k
+    assert torch.equal(na, a)
+    assert chain.download().tobytes() == roll.download().tobytes()
 
 
 def test_dual_step_vector_env_matches_per_env_wrappers():
