@@ -118,6 +118,9 @@ def main():
     ap.add_argument("--refill", choices=("fused", "separate"), default="fused",
                     help="rollout mode: due pool refills run inside the spl_rollout launch (fused) or as a "
                          "spl_refill launch after it (step mode always launches spl_refill)")
+    ap.add_argument("--pipeline", choices=("auto", "always", "off"), default="auto",
+                    help="rollout mode: two-wave pipelined kernel (auto: 2 players, or 3-4 players when the grid "
+                         "is resident at once) vs one wave per 64 tables")
     args = ap.parse_args()
     ROLLOUT_K = args.rollout_k
 
@@ -143,7 +146,9 @@ def main():
     table0 = rank * T
     # the library schedules the pool refills: every R steps (spl_step: a spl_refill launch; spl_rollout:
     # inside the rollout launch unless --refill separate)
-    eng = Engine(T, P, device=dev, refill_period=R, table0=table0, refill_fused=args.refill == "fused")
+    pipe = {"auto": True, "always": "always", "off": False}[args.pipeline]
+    eng = Engine(T, P, device=dev, refill_period=R, table0=table0, refill_fused=args.refill == "fused",
+                 pipeline=pipe)
     eng.reset(seeds=range(table0, table0 + T))
     lib = eng.lib
     buf = [torch.zeros(T, dtype=torch.int32, device=dev) for _ in range(2)]
@@ -281,7 +286,7 @@ def main():
             "config": {"workload": f"{P}-player SplendorEnv.step x {T} tables per GPU, legal mask + uniform-random "
                                    "policy, same-step autoreset, obs int32[297] + mask int8[45] per table-step",
                        "tables_per_gpu": T, "players": P, "parallelism": f"table-sharded x{world}",
-                       "refill_every": R, "refill": args.refill if main_rec["mode"] == "rollout" else "separate",
+                       "refill_every": R, "refill": args.refill if main_rec["mode"] == "rollout" else "separate", "pipeline": args.pipeline,
                        "rollout_steps_per_launch": ROLLOUT_K, "mode": main["mode"],
                        "launch": main["launch"]},
             "roofline": roof,

@@ -115,9 +115,10 @@ int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period);
  * of its own while other waves' stores keep HBM busy; 0 = a separate spl_refill launch after it.
  * Results are identical either way. */
 int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused);
-/* spl_rollout only: 1 (default) = the two-wave pipelined kernel for 2-player arenas (one wave
- * steps the tables, the other encodes and stores the step's outputs); 0 = one wave per 64 tables.
- * Results are identical either way. */
+/* spl_rollout only: the two-wave pipelined kernel (one wave steps the tables, the other encodes
+ * and stores the step's outputs) vs one wave per 64 tables.  1 (default) = two-wave for 2-player
+ * arenas, and for 3-4 players when the whole grid is resident at once (e.g. 32 768 tables);
+ * 2 = two-wave always; 0 = never.  Results are identical either way. */
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
 
 int64_t spl_arena_bytes(int32_t n, int32_t players);

@@ -17,6 +17,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1474,10 +1475,27 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
 // this wave's stores drain and the other waves keep HBM busy, where a separate k_refill launch
 // leaves HBM idle for its whole duration.  Trajectories do not depend on when a refill happens
 // (deals are taken from each table's engine-seed stream in episode order either way).
+// Fused pool refills of one rollout launch: `count` refills (one per refill period the launch
+// crosses), one per segment of K / count steps, each workgroup at its own offset within the segment
+// so that deals (VALU-bound) overlap other workgroups' stores.  Results do not depend on the slots.
+struct RefillSlots {
+    int seg, count, off;
+    __device__ __forceinline__ bool due(int k) const { return count > 0 && k < seg * count && k % seg == off; }
+};
+__device__ __forceinline__ RefillSlots refill_slots(int K, int count) {
+    RefillSlots r{1, 0, 0};
+    if (count > 0) {
+        r.count = min(count, K);
+        r.seg = K / r.count;
+        r.off = (int)(((blockIdx.x * 0x9E3779B1u) >> 16) % (uint32_t)r.seg);
+    }
+    return r;
+}
+
 template <int P>
 __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, int K, int per_step, int refill) {
     __shared__ BlockLDS L;
-    const int refill_k = (refill && S.autoreset) ? (int)(((blockIdx.x * 0x9E3779B1u) >> 16) % (uint32_t)K) : -1;
+    const RefillSlots rs = refill_slots(K, S.autoreset ? refill : 0);
     const int lane = lane_id();
     const int t0 = blockIdx.x * 64;
     const int t = t0 + lane;
@@ -1516,7 +1534,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         RSTAMP(1, k);
         if (obs_tail) store_obs_range(L.rows, obs_tail, kObsSplit, kObsBlockWords);
         obs_tail = nullptr;
-        if (k == refill_k) {  // fused pool refill (wave-uniform)
+        if (rs.due(k)) {  // fused pool refill (wave-uniform)
             wave_lds_sync();  // the tail's LDS reads are done: the rows serve as deal scratch
             if (valid && pend_of(T.sw[SW_MISC]) > 0)
                 T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], &L.rows[lane * kScratchStride], pool, pool_dirty);
@@ -1596,23 +1614,38 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
 //
 // Hand-off per step k (buffers k & 1, so the rules wave refills buffer b only after the output
 // wave has passed the next barrier, i.e. finished with it): the state words after the step
-// (post-autoreset), the info mask, and the terminal (pre-autoreset) states of the first kWsTerm
+// (post-autoreset), the info mask, and the terminal (pre-autoreset) states of the first kTerm
 // terminal lanes; the rules wave writes any further terminal rows itself (store_row_direct).
 // One s_barrier per step; LDS ordering by lgkmcnt(0) only — a workgroup fence would add
 // vmcnt(0) and make each wave wait for its own global stores.
-constexpr int kWsTerm = 16;
-
+//
+// LDS per workgroup must stay <= 40 KB so that four workgroups (a 65 536-table grid) are resident
+// per CU.  At 3-4 players the larger state and terminal hand-off would overflow that, so the deal
+// scratch shrinks to the 100 bytes a deal uses (stride 25 dwords: odd, conflict-free byte lanes),
+// 3 players list at most 8 terminal states per step, and at 4 players the scratch lives inside the
+// rules wave's own state slot st[k & 1]: a deal (fused refill or inline autoreset deal) runs
+// before that slot is written for step k, and the output wave finished reading it (step k - 2)
+// before the hand-off barrier of step k - 1.
 template <int P>
 struct __align__(16) WsLDS : Consts {
     static constexpr int kW = SW_COUNT + 4 * P;  // state words per table
+    static constexpr int kTerm = P == 3 ? 8 : 16;  // terminal states listed per step
+    static constexpr int kScrStride = P == 2 ? kScratchStride : 100;
+    static constexpr bool kScrInSlot = P == 4;
+    static_assert(!kScrInSlot || kW * 64 * 4 >= 64 * kScrStride, "scratch must fit the state slot");
     uint32_t st[2][kW][64];
-    uint32_t tst[2][kWsTerm][kW];
+    uint32_t tst[2][kTerm][kW];
     uint64_t mask[2][64];
     uint64_t fin[2];
     uint32_t mbits[96];
     uint8_t rows[64 * kObsDim];
-    uint8_t scr[64 * kScratchStride];  // the rules wave's deal scratch
+    uint8_t scr[kScrInSlot ? 16 : 64 * kScrStride];  // the rules wave's deal scratch (P < 4)
+    __device__ __forceinline__ uint8_t *scratch(int b, int lane) {
+        return kScrInSlot ? reinterpret_cast<uint8_t *>(&st[b][0][0]) + lane * kScrStride : &scr[lane * kScrStride];
+    }
 };
+static_assert(sizeof(WsLDS<2>) <= 40960 && sizeof(WsLDS<3>) <= 40960 && sizeof(WsLDS<4>) <= 40960,
+              "k_rollout_ws needs four workgroups per CU");
 
 template <int P>
 __device__ __forceinline__ uint32_t tab_word(const Tab<P> &T, int w) {
@@ -1646,8 +1679,7 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
     ws_sync();
 
     if (rules_wave) {
-        const int refill_k = (refill && S.autoreset) ? (int)(((blockIdx.x * 0x9E3779B1u) >> 16) % (uint32_t)K) : -1;
-        uint8_t *scr = &L.scr[lane * kScratchStride];
+        const RefillSlots rs = refill_slots(K, S.autoreset ? refill : 0);
         Tab<P> T;
         int action = 0;
         Deal pool = empty_deal();
@@ -1667,14 +1699,14 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
             const int b = k & 1;
             const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
             StepOut o = step_rules(T, action, pre, valid, L, Tb, k > 0, cur_mask);
-            if (k == refill_k && valid && pend_of(T.sw[SW_MISC]) > 0)  // fused pool refill
-                T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], scr, pool, pool_dirty);
+            if (rs.due(k) && valid && pend_of(T.sw[SW_MISC]) > 0)  // fused pool refill
+                T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], L.scratch(b, lane), pool, pool_dirty);
             const int8_t wnr = (int8_t)get_winner(T.sw);
             const bool fin_me = valid && o.term && want_final;
             const uint64_t fin_all = __ballot(fin_me);
             const int idx = __popcll(fin_all & below);
             if (fin_me) {  // the terminal state, before the autoreset replaces it
-                if (idx < kWsTerm) {
+                if (idx < WsLDS<P>::kTerm) {
 #pragma unroll
                     for (int w = 0; w < kW; ++w) L.tst[b][idx][w] = tab_word(T, w);
                 } else {
@@ -1685,7 +1717,7 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
                 if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], final_reward_p0(T));
                 if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
             }
-            if (valid && o.term && S.autoreset) autoreset_table(T, A, t, pool, scr, o, pool_dirty);
+            if (valid && o.term && S.autoreset) autoreset_table(T, A, t, pool, L.scratch(b, lane), o, pool_dirty);
             if (valid) {
                 S.reward[blk + t] = o.reward;
                 S.terminated[blk + t] = o.term ? 1 : 0;
@@ -1698,7 +1730,7 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
 #pragma unroll
             for (int w = 0; w < kW; ++w) L.st[b][w][lane] = tab_word(T, w);
             L.mask[b][lane] = o.mask;
-            const uint64_t fin_listed = __ballot(fin_me && idx < kWsTerm);  // outside the lane-0 branch
+            const uint64_t fin_listed = __ballot(fin_me && idx < WsLDS<P>::kTerm);  // outside the lane-0 branch
             if (lane == 0) L.fin[b] = fin_listed;
             ws_sync();  // hand-off of step k
         }
@@ -1999,7 +2031,8 @@ struct spl_ctx_s {
     uint4 *lut;
     int refill_period;
     int refill_fused;  // spl_rollout: refill inside the rollout launch (default) or as a k_refill launch after it
-    int pipeline;      // spl_rollout: two-wave pipelined kernel where its LDS fits (2 players)
+    int pipeline;      // spl_rollout: 0 one wave per 64 tables, 1 two-wave kernel where the grid is resident, 2 always
+    int ws_resident[5];  // k_rollout_ws<P>: workgroups resident per device (occupancy x CUs), index P
     void *stage;
     size_t stage_bytes;
 };
@@ -2102,11 +2135,22 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         memcpy(&nrec[i], b, 8);
     }
     HIP_TRY(hipSetDevice(device));
+    int ws_resident[5];
+    {
+        int cus = 0;
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        int occ[5] = {0, 0, 0, 0, 0};
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], k_rollout_ws<2>, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[3], k_rollout_ws<3>, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[4], k_rollout_ws<4>, 128, 0));
+        for (int q = 0; q < 5; ++q) ws_resident[q] = occ[q] * cus;
+    }
     spl_ctx_t *c = new spl_ctx_t();
     c->device = device;
     c->refill_period = 64;
     c->refill_fused = 1;
     c->pipeline = 1;
+    memcpy(c->ws_resident, ws_resident, sizeof(ws_resident));
     if (hipMalloc(&c->cards, sizeof(uint4) * 90) != hipSuccess || hipMalloc(&c->nobles, sizeof(uint2) * 10) != hipSuccess ||
         hipMalloc(&c->lut, sizeof(uint4) * kLutEntries) != hipSuccess) {
         spl_ctx_destroy(c);
@@ -2142,7 +2186,8 @@ int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period) {
 
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on) {
     if (!ctx) return fail(SPL_E_ARG, "null ctx");
-    ctx->pipeline = on != 0;
+    if (on < 0 || on > 2) return fail(SPL_E_ARG, "rollout pipeline must be 0, 1 or 2");
+    ctx->pipeline = on;
     return SPL_OK;
 }
 
@@ -2268,16 +2313,26 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     const int64_t before = arena->steps;
     const bool due = a->autoreset && ctx->refill_period > 0 &&
                      (before + steps) / ctx->refill_period != before / ctx->refill_period;
-    const int fused = due && ctx->refill_fused;
-    if (ctx->pipeline && arena->players == 2)  // WsLDS<2> fits four workgroups per CU; 3-4 players do not
-        hipLaunchKernelGGL(k_rollout_ws<2>, dim3(blocks_for(arena->n)), dim3(128), 0, s, A, ktables(ctx), S, (int)steps,
-                           (int)(per_step_outputs != 0), fused);
-    else
+    // fused: every refill the launch is due (one per refill period it crosses) runs inside it
+    const int fused = (due && ctx->refill_fused)
+                          ? (int)std::min<int64_t>(steps, (before + steps) / ctx->refill_period - before / ctx->refill_period)
+                          : 0;
+    // two-wave kernel: always at 2 players (WsLDS<2> fits four workgroups per CU, the whole 65 536-table
+    // grid); at 3-4 players (three per CU) only when the grid is resident in one pass, unless forced
+    const bool ws = ctx->pipeline == 2 ||
+                    (ctx->pipeline == 1 && (arena->players == 2 ||
+                                            (int64_t)blocks_for(arena->n) <= (int64_t)ctx->ws_resident[arena->players]));
+    if (ws) {
+        DISPATCH_P(arena->players,
+                   hipLaunchKernelGGL(k_rollout_ws<PP>, dim3(blocks_for(arena->n)), dim3(128), 0, s, A, ktables(ctx), S,
+                                      (int)steps, (int)(per_step_outputs != 0), fused));
+    } else {
         DISPATCH_P(arena->players, hipLaunchKernelGGL(k_rollout<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
                                                       ktables(ctx), S, (int)steps, (int)(per_step_outputs != 0), fused));
+    }
     if (int r = launch_check()) return r;
     arena->steps += steps;
-    if (fused) arena->epoch += 1;
+    if (fused) arena->epoch += fused;
     else if (due) return spl_refill(ctx, arena, stream);
     return SPL_OK;
 }

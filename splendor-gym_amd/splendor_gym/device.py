@@ -21,7 +21,8 @@ class Engine:
     so results do not depend on how tables are split across GPUs.
     refill_period / refill_fused: pool refill every `refill_period` steps; rollout() runs a due
     refill inside its launch unless refill_fused is False (results are the same either way).
-    pipeline: rollout() uses the two-wave pipelined kernel (2 players; same results).
+    pipeline: rollout() kernel choice, same results either way: True = two-wave pipelined kernel at
+              2 players and at 3-4 players when the grid is resident at once; "always"; False = never.
     """
 
     # pool refill period by player count (three pool deals per table cover the resets in between;
@@ -52,8 +53,9 @@ class Engine:
         check(self.lib, self.lib.spl_ctx_set_refill_period(self.ctx, int(refill_period)))
         # rollout(): a due refill runs inside the rollout launch (True) or as a refill launch after it
         check(self.lib, self.lib.spl_ctx_set_refill_fused(self.ctx, 1 if refill_fused else 0))
-        # rollout(): two-wave pipelined kernel (2 players) or one wave per 64 tables; same results
-        check(self.lib, self.lib.spl_ctx_set_rollout_pipeline(self.ctx, 1 if pipeline else 0))
+        # rollout(): two-wave pipelined kernel or one wave per 64 tables; same results
+        pipe = 2 if pipeline == "always" else (1 if pipeline else 0)
+        check(self.lib, self.lib.spl_ctx_set_rollout_pipeline(self.ctx, pipe))
         nbytes = int(self.lib.spl_arena_bytes(self.n, self.P))
         dev = self.device
         self._arena_raw = torch.zeros(nbytes + 256, dtype=torch.uint8, device=dev)

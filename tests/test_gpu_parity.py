@@ -198,18 +198,25 @@ def test_unseeded_tables_deal_engine_seed_zero(orc):
     assert canon(table_to_view(recs[5])) == want
 
 
-@pytest.mark.parametrize("P,K,refill_fused,pipeline", [(2, 16, True, True), (2, 16, True, False), (4, 16, True, True),
-                                                        (2, 16, False, True), (2, 64, True, True), (3, 16, True, True)])
-def test_rollout_equals_step_chain(P, K, refill_fused, pipeline):
+@pytest.mark.parametrize("P,K,refill_fused,pipeline,R", [(2, 16, True, True, 16), (2, 16, True, False, 16),
+                                                          (4, 16, True, True, 16), (4, 16, True, False, 16),
+                                                          (4, 16, False, "always", 16), (2, 16, False, True, 16),
+                                                          (2, 64, True, True, 64), (3, 16, True, True, 16),
+                                                          (3, 16, True, False, 16), (4, 64, True, True, 16),
+                                                          (4, 64, True, False, 16), (3, 64, True, "always", 32),
+                                                          (4, 16, True, True, 0), (3, 16, True, True, 0)])
+def test_rollout_equals_step_chain(P, K, refill_fused, pipeline, R):
     """spl_rollout(K) is K chained spl_step calls (next_actions fed back, plies ply..ply+K-1):
     every per-step output, the terminal rows of final_obs, episode statistics, the next action
     and the table state match bit for bit, across launches with refills in between — refills
-    fused into the rollout launch (each wave at its own step) or launched after it; the two-wave
-    pipelined kernel (2 players) or one wave per 64 tables."""
+    fused into the rollout launch (each wave at its own step; several per launch when it spans
+    several refill periods) or launched after it, or never (R = 0: inline deals once the pool ring is
+    spent, through the deal scratch that shares the state slot at 4 players); the two-wave
+    pipelined kernel (any player count; 1 024 tables are resident at once) or one wave per 64 tables."""
     import torch
     n, launches, seed = 1024, 5 if K <= 16 else 3, 11
-    chain = engine(n, P, refill_period=K)
-    fused = engine(n, P, refill_period=K, refill_fused=refill_fused, pipeline=pipeline)
+    chain = engine(n, P, refill_period=R)
+    fused = engine(n, P, refill_period=R, refill_fused=refill_fused, pipeline=pipeline)
     chain.reset(seeds=range(n))
     fused.reset(seeds=range(n))
     dev = chain.device
