@@ -118,9 +118,9 @@ def main():
     ap.add_argument("--refill", choices=("fused", "separate"), default="fused",
                     help="rollout mode: due pool refills run inside the spl_rollout launch (fused) or as a "
                          "spl_refill launch after it (step mode always launches spl_refill)")
-    ap.add_argument("--pipeline", choices=("auto", "always", "off"), default="auto",
-                    help="rollout mode: two-wave pipelined kernel (auto: 2 players, or 3-4 players when the grid "
-                         "is resident at once) vs one wave per 64 tables")
+    ap.add_argument("--pipeline", choices=("auto", "always", "half", "off"), default="auto",
+                    help="rollout mode: two-wave pipelined kernel (auto: 32 or 64 tables per workgroup by grid "
+                         "size; always: 64; half: 32) vs one wave per 64 tables (off)")
     args = ap.parse_args()
     ROLLOUT_K = args.rollout_k
 
@@ -146,7 +146,7 @@ def main():
     table0 = rank * T
     # the library schedules the pool refills: every R steps (spl_step: a spl_refill launch; spl_rollout:
     # inside the rollout launch unless --refill separate)
-    pipe = {"auto": True, "always": "always", "off": False}[args.pipeline]
+    pipe = {"auto": True, "always": "always", "half": "half", "off": False}[args.pipeline]
     eng = Engine(T, P, device=dev, refill_period=R, table0=table0, refill_fused=args.refill == "fused",
                  pipeline=pipe)
     eng.reset(seeds=range(table0, table0 + T))

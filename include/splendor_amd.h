@@ -116,9 +116,10 @@ int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period);
  * Results are identical either way. */
 int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused);
 /* spl_rollout only: the two-wave pipelined kernel (one wave steps the tables, the other encodes
- * and stores the step's outputs) vs one wave per 64 tables.  1 (default) = two-wave for 2-player
- * arenas, and for 3-4 players when the whole grid is resident at once (e.g. 32 768 tables);
- * 2 = two-wave always; 0 = never.  Results are identical either way. */
+ * and stores the step's outputs) vs one wave per 64 tables (0).  1 (default) = two-wave, with 32
+ * tables per workgroup when 64 would leave half of the resident workgroup slots empty (e.g. 32 768
+ * tables), else 64; 2 = two-wave at 64 tables per workgroup; 3 = two-wave at 32.  Results are
+ * identical in every mode. */
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
 
 int64_t spl_arena_bytes(int32_t n, int32_t players);

@@ -859,6 +859,8 @@ constexpr int kObsSplit = 64 * 5 * 7;             // 2240: 35 stores per lane in
 
 // Block store of this wave's observation rows: LDS bytes [rows][297] -> int32 [rows][297] at
 // dst (16-byte aligned: 64-row blocks are 76032 B).  Dword d of the block is LDS word d.
+// R = the workgroup's table count (64, or 32 in the half-populated two-wave rollout).
+template <int R = 64>
 __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int rows, int32_t *dst) {
     const int nbytes = rows * kObsDim;
     const int full = nbytes >> 2;
@@ -866,8 +868,8 @@ __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int row
     v4i *out = reinterpret_cast<v4i *>(dst);
     constexpr int U = 5;
     int d = lane_id();
-    if (rows == 64) {  // every wave but a ragged last one: compile-time trip count
-        constexpr int kFull = 64 * kObsDim / 4;  // 4752 = 14 x 320 + 272
+    if (rows == R) {  // every wave but a ragged last one: compile-time trip count
+        constexpr int kFull = R * kObsDim / 4;  // 64 rows: 4752 = 14 x 320 + 272
 #pragma unroll 1
         for (int it = 0; it < kFull / (64 * U); ++it, d += 64 * U) {
             uint32_t w[U];
@@ -905,9 +907,10 @@ __device__ __forceinline__ void store_mask_block(const uint64_t *mask, uint32_t 
         }
     }
     wave_lds_sync();
-    if (rows == 64 && ((uintptr_t)dst & 15u) == 0) {  // 180 x 16 B: 3 stores per lane
+    if ((rows == 64 || rows == 32) && ((uintptr_t)dst & 15u) == 0) {  // 180 (90) x 16 B
         v4i *out4 = reinterpret_cast<v4i *>(dst);
-        for (int c = lane_id(); c < 180; c += 64) {
+        const int nc = rows * 45 / 16;
+        for (int c = lane_id(); c < nc; c += 64) {
             const uint32_t half = (mbits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;  // stream bits 16c..16c+15
             v4i v;
 #pragma unroll
@@ -1664,16 +1667,21 @@ __device__ __forceinline__ void ws_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-template <int P>
+// TPW = tables per workgroup: 64, or 32 for grids too small to give every SIMD a wave (e.g. the
+// 32 768-table share of a 4-player 8-GPU run): twice the workgroups, lanes 32-63 idle.  The rules
+// work is latency-bound at one wave per SIMD, so half-populated waves on every SIMD finish a step
+// in about the time full ones take on half of them.
+template <int P, int TPW>
 __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep S, int K, int per_step, int refill) {
+    static_assert(TPW == 64 || TPW == 32, "64 or 32 tables per workgroup");
     __shared__ WsLDS<P> L;
     constexpr int kW = WsLDS<P>::kW;
     const int lane = lane_id();
     const bool rules_wave = threadIdx.x < 64;
-    const int t0 = blockIdx.x * 64;
+    const int t0 = blockIdx.x * TPW;
     const int t = t0 + lane;
-    const bool valid = t < A.n;
-    const int rows = min(64, A.n - t0);
+    const bool valid = lane < TPW && t < A.n;
+    const int rows = min(TPW, A.n - t0);
     const bool want_final = S.autoreset && S.final_obs != nullptr;
     load_tables_lds(L, Tb);
     ws_sync();
@@ -1770,7 +1778,7 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
             encode_row(T, L.rows, L);
             wave_lds_sync();
             int32_t *obs = S.obs + blk * kObsDim;
-            store_obs_block(L.rows, rows, obs + (size_t)t0 * kObsDim);
+            store_obs_block<TPW>(L.rows, rows, obs + (size_t)t0 * kObsDim);
             store_mask_block(L.mask[b], L.mbits, rows, S.mask + blk * 45 + (size_t)t0 * 45);
             if (__any(valid && get_moves(T.sw) > 255)) {
                 __builtin_amdgcn_s_waitcnt(0);
@@ -2031,7 +2039,7 @@ struct spl_ctx_s {
     uint4 *lut;
     int refill_period;
     int refill_fused;  // spl_rollout: refill inside the rollout launch (default) or as a k_refill launch after it
-    int pipeline;      // spl_rollout: 0 one wave per 64 tables, 1 two-wave kernel where the grid is resident, 2 always
+    int pipeline;      // spl_rollout: 0 one wave per 64 tables, 1 two-wave (auto tables per workgroup), 2 / 3 two-wave at 64 / 32
     int ws_resident[5];  // k_rollout_ws<P>: workgroups resident per device (occupancy x CUs), index P
     void *stage;
     size_t stage_bytes;
@@ -2140,9 +2148,9 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         int occ[5] = {0, 0, 0, 0, 0};
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], k_rollout_ws<2>, 128, 0));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[3], k_rollout_ws<3>, 128, 0));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[4], k_rollout_ws<4>, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], k_rollout_ws<2, 64>, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[3], k_rollout_ws<3, 64>, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[4], k_rollout_ws<4, 64>, 128, 0));
         for (int q = 0; q < 5; ++q) ws_resident[q] = occ[q] * cus;
     }
     spl_ctx_t *c = new spl_ctx_t();
@@ -2186,7 +2194,7 @@ int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period) {
 
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on) {
     if (!ctx) return fail(SPL_E_ARG, "null ctx");
-    if (on < 0 || on > 2) return fail(SPL_E_ARG, "rollout pipeline must be 0, 1 or 2");
+    if (on < 0 || on > 3) return fail(SPL_E_ARG, "rollout pipeline must be 0..3");
     ctx->pipeline = on;
     return SPL_OK;
 }
@@ -2317,15 +2325,23 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     const int fused = (due && ctx->refill_fused)
                           ? (int)std::min<int64_t>(steps, (before + steps) / ctx->refill_period - before / ctx->refill_period)
                           : 0;
-    // two-wave kernel: always at 2 players (WsLDS<2> fits four workgroups per CU, the whole 65 536-table
-    // grid); at 3-4 players (three per CU) only when the grid is resident in one pass, unless forced
-    const bool ws = ctx->pipeline == 2 ||
-                    (ctx->pipeline == 1 && (arena->players == 2 ||
-                                            (int64_t)blocks_for(arena->n) <= (int64_t)ctx->ws_resident[arena->players]));
-    if (ws) {
+    // two-wave kernel (WsLDS<P> fits four workgroups per CU at every player count)
+    // (pipeline 1 = auto, 2 = two-wave at 64 tables per workgroup, 3 = two-wave at 32).  Auto: two-wave
+    // with 32 tables per workgroup when 64 would leave half the resident slots empty
+    const int64_t resident = ctx->ws_resident[arena->players];
+    int tpw = 0;
+    if (ctx->pipeline == 2) tpw = 64;
+    else if (ctx->pipeline == 3) tpw = 32;
+    else if (ctx->pipeline == 1) tpw = 2 * (int64_t)blocks_for(arena->n) <= resident ? 32 : 64;
+    const int p_out = per_step_outputs != 0;
+    if (tpw == 64) {
         DISPATCH_P(arena->players,
-                   hipLaunchKernelGGL(k_rollout_ws<PP>, dim3(blocks_for(arena->n)), dim3(128), 0, s, A, ktables(ctx), S,
-                                      (int)steps, (int)(per_step_outputs != 0), fused));
+                   hipLaunchKernelGGL((k_rollout_ws<PP, 64>), dim3(blocks_for(arena->n)), dim3(128), 0, s, A,
+                                      ktables(ctx), S, (int)steps, p_out, fused));
+    } else if (tpw == 32) {
+        DISPATCH_P(arena->players,
+                   hipLaunchKernelGGL((k_rollout_ws<PP, 32>), dim3((unsigned)((arena->n + 31) / 32)), dim3(128), 0, s,
+                                      A, ktables(ctx), S, (int)steps, p_out, fused));
     } else {
         DISPATCH_P(arena->players, hipLaunchKernelGGL(k_rollout<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
                                                       ktables(ctx), S, (int)steps, (int)(per_step_outputs != 0), fused));

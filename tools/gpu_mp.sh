@@ -8,7 +8,8 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread -k "rollout" > $O/pt_$TAG.log 2>&1 || { echo "tests failed"; tail -30 $O/pt_$TAG.log; exit 1; }
 tail -1 $O/pt_$TAG.log
 : > $O/mp_$TAG.jsonl
-for cfg in ${CFGS:-"4 65536 auto" "4 65536 off" "3 65536 auto" "3 65536 off" "4 32768 auto" "3 32768 auto" "2 65536 auto"}; do
+IFS=',' read -ra CFG_LIST <<< "${CFGS:-4 65536 auto,4 65536 off,3 65536 auto,3 65536 off,4 32768 auto,3 32768 auto,2 65536 auto}"
+for cfg in "${CFG_LIST[@]}"; do
   set -- $cfg
   timeout -k 10 200 python bench.py --no-cpu-baseline --only --players $1 --tables $2 --pipeline $3 >> $O/mp_$TAG.jsonl 2>> $O/mp_$TAG.err || { echo "fail $cfg"; exit 1; }
 done
