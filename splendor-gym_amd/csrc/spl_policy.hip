@@ -45,16 +45,22 @@ constexpr int kK1 = 19;  // layer-1 k-steps of 16: 297 inputs padded to 304
 constexpr int kK2 = 16;  // layers 2 and 3: 256 inputs
 constexpr int kChunk = 20480, kBiasOff = 19 * 1024;
 constexpr int kActorChunks = 18, kCriticChunks = 17, kAllChunks = 35;
-constexpr int kWaves = 4, kRowsPerWave = 32, kRowsPerBlock = kWaves * kRowsPerWave;
-constexpr int kXRow = 312;                       // bf16 per staged observation row (bank-conflict pad)
-constexpr int kXWave = kRowsPerWave * kXRow * 2;  // 19 968 B
+// Ablation switches for profiling builds only (tools/ablate_policy.sh); the product build defines none.
+#ifndef SPL_ACT_ABL
+#define SPL_ACT_ABL 0
+#endif
+constexpr int ABL_MFMA = 1, ABL_EPI = 2, ABL_XLOAD = 4, ABL_RING = 8;
+
+constexpr int kWaves = 8, kRowsPerWave = 32, kRowsPerBlock = kWaves * kRowsPerWave;  // 256 tables
+constexpr int kSlots = 6;                         // weight ring: 5 chunks in flight
 constexpr int kMaskWave = kRowsPerWave * kAct;    // 1 440 B
 constexpr int kLogitRow = 65;                     // floats per staged logit row
-constexpr int kLdsX = 3 * kChunk;
-constexpr int kLdsMask = kLdsX + kWaves * kXWave;
-constexpr int kLds = kLdsMask + kWaves * kMaskWave;  // 147 072 B
-static_assert(kRowsPerWave * kLogitRow * 4 <= kXWave, "logits reuse the observation image");
+constexpr int kLdsMask = kSlots * kChunk;         // 122 880 B of ring
+constexpr int kLds = kLdsMask + kWaves * kMaskWave;  // 134 400 B
+static_assert(kWaves * kRowsPerWave * kLogitRow * 4 <= kLdsMask, "logits reuse the weight ring");
 static_assert(kLds <= 160 * 1024, "LDS");
+// fp32 critic output layer after the chunks of a full image: w3 [256], b3, zero padding
+constexpr int kCriticTail = 272 * 4;
 
 // chunk order of an image: with a critic [critic L1 x8][critic L2 x8][critic L3 x1], then
 // [actor L1 x8][actor L2 x8][actor L3 x2] — the order a forward pass consumes them; the actor part
@@ -103,6 +109,10 @@ __global__ __launch_bounds__(256) void k_pack(PackNet actor, PackNet critic, int
                    e[6] | (uint32_t)e[7] << 16};
         *reinterpret_cast<u32x4 *>(out + (size_t)v * 16) = w;
     }
+    if (net == 1 && layer == 3) {  // the critic's output layer also as fp32 (evaluated on VALU)
+        float *tail = reinterpret_cast<float *>(dst + (size_t)kAllChunks * kChunk);
+        for (int k = threadIdx.x; k < 272; k += blockDim.x) tail[k] = k < kHid ? W[k] : k == kHid ? B[0] : 0.f;
+    }
     if (threadIdx.x < 32) {  // bias in accumulator order: [lane half][reg] -> row (reg&3)+8(reg>>2)+4h
         const int h = threadIdx.x >> 4, reg = threadIdx.x & 15;
         const int row = 32 * tile + (reg & 3) + 8 * (reg >> 2) + 4 * h;
@@ -118,6 +128,7 @@ struct ActArgs {
     const int8_t *mask;
     int32_t *action;
     float *logprob, *entropy, *value, *logits;
+    const float *critic_out;  // fp32 critic output layer (kCriticTail) of a full image
     uint64_t seed, ply;
     const uint64_t *ply_base;
     int64_t table0;
@@ -131,19 +142,28 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-B load
 
-// this wave's fifth of one chunk, global -> LDS (lane-linear 16-byte pieces)
+// this wave's 1-KB blocks of one chunk, global -> LDS: wave w moves blocks w, w+8, w+16 (< 20), so
+// waves 0-3 issue 3 loads per chunk and waves 4-7 issue 2
+constexpr int kChunkBlocks = kChunk / 1024;  // 20
 __device__ __forceinline__ void issue_chunk(const uint8_t *W, int chunk, uint8_t *slot, int wave, int lane) {
-    const uint8_t *src = W + (size_t)chunk * kChunk + wave * 1024 + lane * 16;
-    uint8_t *dst = slot + wave * 1024;
+    if constexpr (SPL_ACT_ABL & ABL_RING) return;
+    const uint8_t *src = W + (size_t)chunk * kChunk + lane * 16;
 #pragma unroll
-    for (int i = 0; i < kChunk / 4096; ++i)
-        __builtin_amdgcn_global_load_lds(src + i * 4096, (lds_void *)(dst + i * 4096), 16, 0, 0);
+    for (int i = 0; i < 3; ++i) {
+        const int blk = wave + kWaves * i;
+        if (blk < kChunkBlocks)
+            __builtin_amdgcn_global_load_lds(src + blk * 1024, (lds_void *)(slot + blk * 1024), 16, 0, 0);
+    }
 }
 
+// tanh(x) = 1 - 2 / (e^2x + 1) as v_exp_f32 + v_rcp_f32 (about 1 ulp each; +-inf saturate to +-1):
+// __expf / __fdividef compiled to the full-precision division sequence (v_div_scale / fmas /
+// fixup, ~14 instructions per value), which made the tanh epilogues cost more than the MFMAs
 __device__ __forceinline__ float tanh_fast(float x) {
-    const float e = __expf(2.f * x);
-    return 1.f - __fdividef(2.f, e + 1.f);
+    const float e = __builtin_amdgcn_exp2f(x * 2.88539008177792681f);  // 2 / ln 2
+    return __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
 }
 
 __device__ __forceinline__ bf16x8 pack8(float a0, float a1, float a2, float a3, float a4, float a5, float a6,
@@ -164,44 +184,37 @@ __device__ __forceinline__ void tanh_pack(const f32x16 &a, bf16x8 &lo, bf16x8 &h
     hi = pack8(t[8], t[9], t[10], t[11], t[12], t[13], t[14], t[15]);
 }
 
-// one 32-row output tile: bias + sum over KS k-steps; B fragments from registers (layers 2-3) or
-// from the wave's staged observation row (layer 1, a 16-byte LDS read per k-step).  LDS fragment
-// reads run one group of 4 k-steps ahead of the MFMAs that use them; the scheduling barriers keep
-// the compiler from hoisting every read of the tile (and its registers) to the top.
-template <int KS, bool kBFromLds, typename BF>
-__device__ __forceinline__ f32x16 tile_mma(const uint8_t *slot, BF B, int lane) {
+// one 32-row output tile: bias + sum over KS k-steps, B fragments in registers (the observation
+// for layer 1, the previous layer's tanh for layers 2-3); weight fragments from the LDS ring slot,
+// read one group of 4 k-steps ahead of the MFMAs that use them (the scheduling barriers keep the
+// compiler from hoisting every read of the tile, and its registers, to the top)
+template <int KS, int NB>
+__device__ __forceinline__ f32x16 tile_mma(const uint8_t *slot, const bf16x8 (&B)[NB], int lane) {
+    static_assert(KS <= NB, "B fragments");
     constexpr int G = 4, NG = (KS + G - 1) / G;
     const float *bias = reinterpret_cast<const float *>(slot + kBiasOff) + (lane >> 5) * 16;
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = bias[r];
     const bf16x8 *A = reinterpret_cast<const bf16x8 *>(slot) + lane;
-    bf16x8 af[2][G], bf[2][G];
+    bf16x8 af[2][G];
 #pragma unroll
-    for (int i = 0; i < G; ++i) {
-        af[0][i] = A[i * 64];
-        if constexpr (kBFromLds) bf[0][i] = B[i];
-    }
+    for (int i = 0; i < G; ++i) af[0][i] = A[i * 64];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
         if (g + 1 < NG) {
 #pragma unroll
             for (int i = 0; i < G; ++i) {
                 const int s = (g + 1) * G + i;
-                if (s < KS) {
-                    af[(g + 1) & 1][i] = A[s * 64];
-                    if constexpr (kBFromLds) bf[(g + 1) & 1][i] = B[s];
-                }
+                if (s < KS) af[(g + 1) & 1][i] = A[s * 64];
             }
         }
 #pragma unroll
         for (int i = 0; i < G; ++i) {
             const int s = g * G + i;
             if (s < KS) {
-                if constexpr (kBFromLds)
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[g & 1][i], bf[g & 1][i], acc, 0, 0, 0);
-                else
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[g & 1][i], B[s], acc, 0, 0, 0);
+                if constexpr (SPL_ACT_ABL & ABL_MFMA) acc[i] += (float)af[g & 1][i][0] + (float)B[s][1];
+                else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[g & 1][i], B[s], acc, 0, 0, 0);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -209,100 +222,167 @@ __device__ __forceinline__ f32x16 tile_mma(const uint8_t *slot, BF B, int lane) 
     return acc;
 }
 
+// tile_mma that also evaluates tanh of the PREVIOUS tile's accumulator `pend` into tp[16],
+// four values per group of four MFMAs: the transcendental work (v_exp + v_rcp per value) issues in
+// the MFMA gaps instead of as a separate VALU phase after every tile
+template <int KS, int NB>
+__device__ __forceinline__ f32x16 tile_mma_tanh(const uint8_t *slot, const bf16x8 (&B)[NB], int lane,
+                                                const f32x16 &pend, float (&tp)[16]) {
+    static_assert(KS <= NB, "B fragments");
+    constexpr int G = 4, NG = (KS + G - 1) / G;
+    static_assert(NG >= 4, "16 tanh values over at least four groups");
+    const float *bias = reinterpret_cast<const float *>(slot + kBiasOff) + (lane >> 5) * 16;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = bias[r];
+    const bf16x8 *A = reinterpret_cast<const bf16x8 *>(slot) + lane;
+    bf16x8 af[2][G];
+#pragma unroll
+    for (int i = 0; i < G; ++i) af[0][i] = A[i * 64];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        if (g + 1 < NG) {
+#pragma unroll
+            for (int i = 0; i < G; ++i) {
+                const int s = (g + 1) * G + i;
+                if (s < KS) af[(g + 1) & 1][i] = A[s * 64];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+            const int s = g * G + i;
+            if (s < KS) {
+                if constexpr (SPL_ACT_ABL & ABL_MFMA) acc[i] += (float)af[g & 1][i][0] + (float)B[s][1];
+                else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[g & 1][i], B[s], acc, 0, 0, 0);
+            }
+            if (g < 4) tp[4 * g + i] = tanh_fast(pend[4 * g + i]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
+}
+
+// one layer of 8 tiles whose tanh feeds the next layer as bf16 B fragments H[16]; each tile's tanh
+// runs inside the next tile's MFMAs, the last one after the loop
+template <int KS, int NB, typename Enter>
+__device__ __forceinline__ void layer_tanh(Enter &enter, const bf16x8 (&B)[NB], bf16x8 (&H)[16], int lane) {
+    f32x16 pend = tile_mma<KS>(enter(), B, lane);
+#pragma unroll
+    for (int t = 1; t < 8; ++t) {
+        float tp[16];
+        const f32x16 acc = tile_mma_tanh<KS>(enter(), B, lane, pend, tp);
+        H[2 * t - 2] = pack8(tp[0], tp[1], tp[2], tp[3], tp[4], tp[5], tp[6], tp[7]);
+        H[2 * t - 1] = pack8(tp[8], tp[9], tp[10], tp[11], tp[12], tp[13], tp[14], tp[15]);
+        pend = acc;
+    }
+    tanh_pack(pend, H[14], H[15]);
+}
+
+// Workgroup = 8 waves = 256 tables (two waves per SIMD), one wave = 32 tables = the 32 columns of
+// every v_mfma_f32_32x32x16_bf16 tile.  Activations are TRANSPOSED (hidden unit on the
+// accumulator row, table on the lane), so each layer's accumulators are directly the next layer's
+// B operand, and the observation's B fragments are loaded straight from HBM into registers
+// (8 int32 of one row per lane and k-step -> bf16; every obs value is a small integer, exact in
+// bf16).  Weights stream once per workgroup through a 6-slot LDS ring (20-KB chunks = one 32-row
+// tile of a layer, global_load_lds, 5 in flight) shared by the 8 waves; a 65 536-table grid is
+// one workgroup per CU, so each CU streams the 0.7-MB image once per launch.  The critic's output
+// layer (one unit) runs on VALU in fp32 as its layer-2 tiles come out, so neither its layer-2
+// activations nor an output tile are ever materialised.
 template <bool kCritic, bool kSample>
-__global__ __launch_bounds__(256, 1) void k_act(const uint8_t *__restrict__ W, ActArgs a) {
+__global__ __launch_bounds__(512) void k_act(const uint8_t *__restrict__ W, ActArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
-    constexpr int kTotal = kCritic ? kAllChunks : kActorChunks;
+    constexpr int kTotal = kCritic ? kAllChunks - 1 : kActorChunks;  // the critic L3 chunk is skipped
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const int64_t tbase = (int64_t)blockIdx.x * kRowsPerBlock + wave * kRowsPerWave;
     const int valid = (int)max<int64_t>(0, min<int64_t>(kRowsPerWave, (int64_t)a.n - tbase));
     uint8_t *ring = lds;
-    __bf16 *xs = reinterpret_cast<__bf16 *>(lds + kLdsX + wave * kXWave);
     uint8_t *ms = lds + kLdsMask + wave * kMaskWave;
+    auto chunk_of = [](int c) { return kCritic && c >= 16 ? c + 1 : c; };
 
-    // weight ring prologue: chunks 0 and 1 in flight
-    issue_chunk(W, 0, ring, wave, lane);
-    issue_chunk(W, 1, ring + kChunk, wave, lane);
+    // weight ring prologue: chunks 0 .. kSlots-2 in flight
+#pragma unroll
+    for (int c = 0; c < kSlots - 1; ++c) issue_chunk(W, chunk_of(c), ring + c * kChunk, wave, lane);
 
-    // stage this wave's observations (contiguous rows) as bf16 and its masks as bytes
-    if (valid == kRowsPerWave) {  // full wave: branch-free 16-byte loads, all issued up front
-        constexpr int kQ = kRowsPerWave * kObs / 4, kIters = (kQ + 63) / 64;  // 2376 int4, 38 per lane
-        constexpr int kMQ = kMaskWave / 4, kMIters = (kMQ + 63) / 64;          // 360 dwords, 6 per lane
-        const int4 *src = reinterpret_cast<const int4 *>(a.obs + tbase * kObs);
+    // observation B fragments: lane (r, h), k-step s = obs[table r][16s + 8h .. +7] as bf16
+    const int32_t *xrow = a.obs + (size_t)min<int64_t>(tbase + r, (int64_t)a.n - 1) * kObs;
+    auto load_x = [&](bf16x8 (&X)[kK1]) {
+        if constexpr (SPL_ACT_ABL & ABL_XLOAD) {
+            for (int s = 0; s < kK1; ++s) X[s] = pack8(h, r, 0, 1, 2, 3, 4, 5);
+            return;
+        }
+#pragma unroll
+        for (int s = 0; s < kK1 - 1; ++s) {
+            const u32x4u v0 = *reinterpret_cast<const u32x4u *>(xrow + 16 * s + 8 * h);
+            const u32x4u v1 = *reinterpret_cast<const u32x4u *>(xrow + 16 * s + 8 * h + 4);
+            X[s] = pack8((float)(int)v0.x, (float)(int)v0.y, (float)(int)v0.z, (float)(int)v0.w, (float)(int)v1.x,
+                         (float)(int)v1.y, (float)(int)v1.z, (float)(int)v1.w);
+        }
+        // k-step 18: k = 288..295 (h = 0) or 296 and the zero padding (h = 1)
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 16 * (kK1 - 1) + 8 * h + j;
+            v[j] = k < kObs ? (float)xrow[min(k, kObs - 1)] : 0.f;
+        }
+        X[kK1 - 1] = pack8(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]);
+    };
+    bf16x8 X[kK1];
+    load_x(X);
+    // masks as bytes
+    if (valid == kRowsPerWave) {
+        constexpr int kMQ = kMaskWave / 4;  // 360 dwords
         const uint32_t *msrc = reinterpret_cast<const uint32_t *>(a.mask + tbase * kAct);
-        int4 v[kIters];
-        uint32_t mv[kMIters];
-#pragma unroll
-        for (int it = 0; it < kIters; ++it) v[it] = src[min(it * 64 + lane, kQ - 1)];
-#pragma unroll
-        for (int it = 0; it < kMIters; ++it) mv[it] = msrc[min(it * 64 + lane, kMQ - 1)];
-#pragma unroll
-        for (int it = 0; it < kIters; ++it) {
-            const int q = it * 64 + lane;
-            if (q < kQ) {
-                const int vals[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int e = 4 * q + i, row = e / kObs, k = e - row * kObs;
-                    xs[row * kXRow + k] = (__bf16)(float)vals[i];
-                }
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < kMIters; ++it) {
-            const int q = it * 64 + lane;
-            if (q < kMQ) reinterpret_cast<uint32_t *>(ms)[q] = mv[it];
-        }
-    } else {  // the grid's last, partial wave (or an idle one): element-wise, bounds-checked
-        const int32_t *src = a.obs + tbase * kObs;
-        for (int e = lane; e < valid * kObs; e += 64) {
-            const int row = e / kObs, k = e - row * kObs;
-            xs[row * kXRow + k] = (__bf16)(float)src[e];
-        }
+        for (int q = lane; q < kMQ; q += 64) reinterpret_cast<uint32_t *>(ms)[q] = msrc[q];
+    } else {
         const int8_t *msrc = a.mask + tbase * kAct;
         for (int e = lane; e < valid * kAct; e += 64) ms[e] = (uint8_t)msrc[e];
     }
-    for (int idx = lane; idx < kRowsPerWave * 7; idx += 64)  // k = 297..303 of every row
-        xs[(idx / 7) * kXRow + kObs + idx % 7] = (__bf16)0.f;
-    wave_lds_sync();
-    const bf16x8 *xrow = reinterpret_cast<const bf16x8 *>(reinterpret_cast<const uint8_t *>(xs) + r * kXRow * 2) + h;
-    struct XFrag {
-        const bf16x8 *p;
-        __device__ bf16x8 operator[](int s) const { return p[2 * s]; }
-    } X{xrow};
 
     int c = 0;
     auto enter = [&]() -> const uint8_t * {
-        asm volatile("s_waitcnt vmcnt(5)" ::: "memory");  // this wave's part of chunk c landed
-        __builtin_amdgcn_s_barrier();                      // everyone's part landed; slot c-1 free
+        // this wave's part of chunk c landed (later chunks' loads may stay outstanding)
+        if (wave < kChunkBlocks - 2 * kWaves) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // everyone's part landed; slot c-1 is free
         asm volatile("" ::: "memory");
-        const int nxt = c + 2 < kTotal ? c + 2 : kTotal - 1;  // past the end: harmless reload
-        issue_chunk(W, nxt, ring + ((c + 2) % 3) * kChunk, wave, lane);
-        const uint8_t *slot = ring + (c % 3) * kChunk;
+        const int nxt = c + kSlots - 1 < kTotal ? c + kSlots - 1 : kTotal - 1;  // past the end: harmless reload
+        issue_chunk(W, chunk_of(nxt), ring + ((c + kSlots - 1) % kSlots) * kChunk, wave, lane);
+        const uint8_t *slot = ring + (c % kSlots) * kChunk;
         ++c;
         return slot;
     };
+    static_assert((kSlots - 2) * 3 == 12 && (kSlots - 2) * 2 == 8, "vmcnt immediates");
 
     bf16x8 H1[16], H2[16];
     float value = 0.f;
-    if constexpr (kCritic) {  // critic first: only its scalar output stays live across the actor
+    if constexpr (kCritic) {
+        layer_tanh<kK1>(enter, X, H1, lane);
+        // layer 2 tile t -> tanh -> its 32 units' share of the fp32 output unit, on the spot
+#pragma unroll 1
+        for (int t = 0; t < 8; ++t) {
+            const f32x16 acc = tile_mma<kK2>(enter(), H1, lane);
+            const float *w3 = a.critic_out + 32 * t + 4 * h;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) tanh_pack(tile_mma<kK1, true>(enter(), X, lane), H1[2 * t], H1[2 * t + 1]);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) tanh_pack(tile_mma<kK2, false>(enter(), H1, lane), H2[2 * t], H2[2 * t + 1]);
-        value = tile_mma<kK2, false>(enter(), H2, lane)[0];  // row 0 = the critic output (lanes h == 0)
+            for (int q = 0; q < 4; ++q) {
+                const float4 w = *reinterpret_cast<const float4 *>(w3 + 8 * q);
+                value += w.x * tanh_fast(acc[4 * q]) + w.y * tanh_fast(acc[4 * q + 1]) +
+                         w.z * tanh_fast(acc[4 * q + 2]) + w.w * tanh_fast(acc[4 * q + 3]);
+            }
+        }
+        value += __shfl_xor(value, 32) + a.critic_out[kHid];  // the other lane half's rows, bias
+        // the observation again (L2 / Infinity Cache) instead of holding its 76 registers through
+        // the critic's layer 2 (the enter() barriers' memory clobbers keep this a real reload)
+        load_x(X);
     }
-#pragma unroll
-    for (int t = 0; t < 8; ++t) tanh_pack(tile_mma<kK1, true>(enter(), X, lane), H1[2 * t], H1[2 * t + 1]);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) tanh_pack(tile_mma<kK2, false>(enter(), H1, lane), H2[2 * t], H2[2 * t + 1]);
-    const f32x16 L0 = tile_mma<kK2, false>(enter(), H2, lane);
-    const f32x16 L1 = tile_mma<kK2, false>(enter(), H2, lane);
+    layer_tanh<kK1>(enter, X, H1, lane);
+    layer_tanh<kK2>(enter, H1, H2, lane);
+    const f32x16 L0 = tile_mma<kK2>(enter(), H2, lane);
+    const f32x16 L1 = tile_mma<kK2>(enter(), H2, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing reloads
+    __builtin_amdgcn_s_barrier();                      // every wave is done with the ring
 
-    // logits -> LDS [table][action] (reusing the observation image), then per-table epilogue
-    float *lg = reinterpret_cast<float *>(xs);
-    wave_lds_sync();
+    // logits -> LDS [table][action] (reusing the ring), then the per-table epilogue
+    float *lg = reinterpret_cast<float *>(ring) + wave * kRowsPerWave * kLogitRow;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         const int a0 = (reg & 3) + 8 * (reg >> 2) + 4 * h;
@@ -313,6 +393,10 @@ __global__ __launch_bounds__(256, 1) void k_act(const uint8_t *__restrict__ W, A
     if (a.logits) {
         float *dst = a.logits + tbase * kAct;
         for (int i = lane; i < valid * kAct; i += 64) dst[i] = lg[(i / kAct) * kLogitRow + i % kAct];
+    }
+    if ((SPL_ACT_ABL & ABL_EPI) && h == 0 && r < valid) {
+        a.action[tbase + r] = (int)lg[r * kLogitRow];
+        return;
     }
     if (h == 0 && r < valid) {
         const int64_t t = tbase + r;
@@ -368,7 +452,9 @@ using namespace splp;
 
 extern "C" {
 
-int64_t spl_policy_bytes(int32_t with_critic) { return (int64_t)(with_critic ? kAllChunks : kActorChunks) * kChunk; }
+int64_t spl_policy_bytes(int32_t with_critic) {
+    return with_critic ? (int64_t)kAllChunks * kChunk + kCriticTail : (int64_t)kActorChunks * kChunk;
+}
 
 int spl_policy_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream) {
     if (!actor || !actor->w1 || !actor->b1 || !actor->w2 || !actor->b2 || !actor->w3 || !actor->b3)
@@ -399,8 +485,11 @@ int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const sp
     const bool sample = args->mode == SPL_ACT_SAMPLE;
     const bool critic = sample && args->value;
     if (critic && !has_critic) return spl_fail(SPL_E_ARG, "value requested from an actor-only image");
-    const ActArgs a{args->obs, args->mask, args->action, args->logprob, args->entropy, args->value, args->logits,
-                    args->seed, args->ply, args->ply_base, args->table0, n};
+    const uint8_t *img = static_cast<const uint8_t *>(packed);
+    const float *critic_out = has_critic ? reinterpret_cast<const float *>(img + (size_t)kAllChunks * kChunk) : nullptr;
+    const ActArgs a{args->obs,   args->mask,       args->action,   args->logprob, args->entropy,
+                    args->value, args->logits,     critic_out,     args->seed,    args->ply,
+                    args->ply_base, args->table0, n};
     const dim3 grid((unsigned)((n + kRowsPerBlock - 1) / kRowsPerBlock)), block(kWaves * 64);
     const hipStream_t s = (hipStream_t)stream;
     const uint8_t *W = static_cast<const uint8_t *>(packed);

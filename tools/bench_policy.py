@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tables", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--fused-only", action="store_true", help="skip the torch timings")
     args = ap.parse_args()
     import torch
     from splendor_gym.device import Engine
@@ -62,9 +63,10 @@ def main():
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
             return m.get_action_and_value(obs.float(), mask.float())
 
-    res["torch_fp32_sample_us"] = timeit(torch_sample)
-    res["torch_bf16_sample_us"] = timeit(torch_sample_bf16)
-    res["torch_fp32_greedy_us"] = timeit(lambda: greedy_actions(m, obs, mask))
+    if not args.fused_only:
+        res["torch_fp32_sample_us"] = timeit(torch_sample)
+        res["torch_bf16_sample_us"] = timeit(torch_sample_bf16)
+        res["torch_fp32_greedy_us"] = timeit(lambda: greedy_actions(m, obs, mask))
     fl_s = 2.0 * n * (MACS_ACTOR + MACS_CRITIC)
     fl_g = 2.0 * n * MACS_ACTOR
     res["fused_sample_tflops"] = fl_s / res["fused_sample_us"] / 1e6
