@@ -399,29 +399,42 @@ __global__ __launch_bounds__(512) void k_act(const uint8_t *__restrict__ W, ActA
         return;
     }
     if (h == 0 && r < valid) {
+        // the table's 45 logits and legal bits into registers (fully unrolled: the LDS reads issue
+        // together instead of one latency per loop iteration), then max / softmax / sample in place
         const int64_t t = tbase + r;
         const float *row = lg + r * kLogitRow;
+        const uint8_t *mrow = ms + r * kAct;
+        float lv[kAct];
         uint64_t legal = 0;
-        for (int k = 0; k < kAct; ++k) legal |= (uint64_t)(ms[r * kAct + k] != 0) << k;
+#pragma unroll
+        for (int k = 0; k < kAct; ++k) {
+            lv[k] = row[k];
+            legal |= (uint64_t)(mrow[k] != 0) << k;
+        }
         int act = 0;
         if constexpr (!kSample) {
             // logits.masked_fill(mask < 0.5, -inf).argmax(): first maximum; all-illegal -> 0
             float best = -__builtin_inff();
-            for (int k = 0; k < kAct; ++k)
-                if (((legal >> k) & 1) && row[k] > best) best = row[k], act = k;
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) {
+                const bool better = ((legal >> k) & 1) && lv[k] > best;
+                best = better ? lv[k] : best;
+                act = better ? k : act;
+            }
         } else {
             // masked_categorical: illegal -> -inf unless the row has no legal action
             const uint64_t allow = legal ? legal : (1ull << kAct) - 1;
             float mx = -__builtin_inff();
-            for (int k = 0; k < kAct; ++k)
-                if ((allow >> k) & 1) mx = fmaxf(mx, row[k]);
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) mx = ((allow >> k) & 1) ? fmaxf(mx, lv[k]) : mx;
             float S = 0.f, T = 0.f;
-            for (int k = 0; k < kAct; ++k)
-                if ((allow >> k) & 1) {
-                    const float d = row[k] - mx, p = __expf(d);
-                    S += p;
-                    T += p * d;
-                }
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) {
+                const float d = lv[k] - mx, p = ((allow >> k) & 1) ? __expf(d) : 0.f;
+                lv[k] = p;  // the unnormalised probability, for the inverse-CDF scan
+                S += p;
+                T += p * d;
+            }
             const float logS = __logf(S);
             const uint64_t ply = a.ply + (a.ply_base ? *a.ply_base : 0ull);
             const uint4 rnd = philox4x32(make_uint4((uint32_t)(a.table0 + t), (uint32_t)((uint64_t)(a.table0 + t) >> 32),
@@ -431,12 +444,15 @@ __global__ __launch_bounds__(512) void k_act(const uint8_t *__restrict__ W, ActA
             float cum = 0.f;
             int last = 0;
             bool found = false;
-            for (int k = 0; k < kAct; ++k)
-                if ((allow >> k) & 1) {
-                    cum += __expf(row[k] - mx);
-                    last = k;
-                    if (!found && cum > target) act = k, found = true;
-                }
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) {
+                const bool al = (allow >> k) & 1;
+                cum += lv[k];
+                last = al ? k : last;
+                const bool hit = al && !found && cum > target;
+                act = hit ? k : act;
+                found = found || hit;
+            }
             if (!found) act = last;
             if (a.logprob) a.logprob[t] = row[act] - mx - logS;
             if (a.entropy) a.entropy[t] = logS - T / S;
