@@ -229,7 +229,7 @@ def main():
             # ROCm rejects timing events as graph nodes ("External events are disallowed"), so the
             # kernel duration comes from HIP events around each launch of an eager window of the
             # same loop, run right after the timed replays on the same stream and state.
-            nwin = 64
+            nwin = max(64, 4 * per)  # at least four launches
             ev = ([torch.cuda.Event(enable_timing=True) for _ in range(nwin // per)],
                   [torch.cuda.Event(enable_timing=True) for _ in range(nwin // per)])
             ply_base.fill_(k_base + W + K + 1)
@@ -238,7 +238,7 @@ def main():
         nev = len(ev[0])
         launch_s = sum(ev[0][i].elapsed_time(ev[1][i]) for i in range(nev)) / nev / 1e3
         return {"mode": mode, "elapsed": elapsed, "launch_s": launch_s, "steps_per_launch": per, "how": how,
-                "nev": nev, "k_next": k_base + W + K + 1 + 64 + 1}
+                "nev": nev, "k_next": k_base + W + K + 1 + max(64, 4 * per) + 1}
 
     main_rec = measure(args.mode, 0)
     alt_rec = None
@@ -253,7 +253,8 @@ def main():
     def summary(rec):
         total_steps = T * world * K
         algo = ALGO_BYTES[P] * T * rec["steps_per_launch"]
-        kname = f"spl::k_step<{P}>" if rec["mode"] == "step" else f"spl::k_rollout<{P}> ({ROLLOUT_K} steps per launch)"
+        rk = "k_rollout" if args.pipeline == "off" else "k_rollout_ws"  # two-wave pipelined kernel
+        kname = f"spl::k_step<{P}>" if rec["mode"] == "step" else f"spl::{rk}<{P}> ({ROLLOUT_K} steps per launch)"
         return {"mode": rec["mode"], "value": round(total_steps / rec["elapsed"], 1),
                 "ms_per_step": round(rec["elapsed"] / K * 1e3, 4),
                 "roofline": {"bound": "hbm", "achieved": round(algo / rec["launch_s"] / 1e9, 1),
