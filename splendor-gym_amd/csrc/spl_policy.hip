@@ -6,21 +6,22 @@
 // entropy and critic(x); opponents play the greedy masked argmax of a frozen actor
 // (training_utils.py:263-276).  Here one launch evaluates that for every table:
 //
-//   * a workgroup = 4 waves = 128 tables, one wave = 32 tables = the 32 columns of every
-//     v_mfma_f32_32x32x16_bf16 tile.  Activations are computed TRANSPOSED (hidden unit on the
-//     accumulator row, table on the lane), so each layer's accumulator registers are directly the
-//     next layer's B operand: no LDS round trip between layers (the k order inside a 16-step is
-//     permuted; the packed weights carry the matching column order).
+//   * a workgroup = 8 waves = 256 tables (two waves per SIMD), one wave = 32 tables = the 32
+//     columns of every v_mfma_f32_32x32x16_bf16 tile.  Activations are computed TRANSPOSED (hidden
+//     unit on the accumulator row, table on the lane), so each layer's accumulator registers are
+//     directly the next layer's B operand: no LDS round trip between layers (the k order inside a
+//     16-step is permuted; the packed weights carry the matching column order).
 //   * weights are packed once (k_pack) into 20 KB "chunks" — one 32-row output tile of one layer,
 //     [k-step][lane][8 bf16] in fragment order plus the tile's bias in accumulator order — and
-//     streamed through a 3-slot LDS ring with global_load_lds (2 chunks in flight), shared by the
-//     workgroup's 4 waves.  The whole image (0.7 MB) stays L2-resident across workgroups.
-//   * observations (int32) are staged per wave in LDS as bf16 (every obs value is a small
-//     integer, exact in bf16); layer 1 reads its B fragments from there (one ds_read_b128 per
-//     MFMA beside the weight fragment's), so only the hidden activations occupy registers.
-//   * tanh, bias, masking, log-softmax, entropy and the Philox-driven inverse-CDF sample are
-//     fused after the last tile; the sampled action differs from torch's multinomial stream by
-//     design (same distribution), logits match the fp32 module to bf16 accuracy.
+//     streamed through a 6-slot LDS ring with global_load_lds (5 chunks in flight), shared by the
+//     workgroup's 8 waves; a 65 536-table batch is one workgroup per CU.
+//   * observations (int32) load straight into registers as the layer-1 B fragments (bf16; every
+//     obs value is a small integer, exact in bf16) and stay there through both networks' layer 1.
+//   * the critic's one-unit output layer runs on VALU in fp32 as its layer-2 tiles come out;
+//     tanh (v_exp + v_rcp) runs inside the next tile's MFMA stream; masking, log-softmax, entropy
+//     and the Philox-driven inverse-CDF sample are fused after the last tile on register-resident
+//     logits; the sampled action differs from torch's multinomial stream by design (same
+//     distribution), logits match the fp32 module to bf16 accuracy.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -50,6 +51,9 @@ constexpr int kActorChunks = 18, kCriticChunks = 17, kAllChunks = 35;
 #define SPL_ACT_ABL 0
 #endif
 constexpr int ABL_MFMA = 1, ABL_EPI = 2, ABL_XLOAD = 4, ABL_RING = 8;
+#ifndef SPL_ACT_RELOAD_X
+#define SPL_ACT_RELOAD_X 0  // 1: reload the observation after the critic (fewer registers live)
+#endif
 
 constexpr int kWaves = 8, kRowsPerWave = 32, kRowsPerBlock = kWaves * kRowsPerWave;  // 256 tables
 constexpr int kSlots = 6;                         // weight ring: 5 chunks in flight
@@ -370,9 +374,11 @@ __global__ __launch_bounds__(512) void k_act(const uint8_t *__restrict__ W, ActA
             }
         }
         value += __shfl_xor(value, 32) + a.critic_out[kHid];  // the other lane half's rows, bias
+#if SPL_ACT_RELOAD_X
         // the observation again (L2 / Infinity Cache) instead of holding its 76 registers through
         // the critic's layer 2 (the enter() barriers' memory clobbers keep this a real reload)
         load_x(X);
+#endif
     }
     layer_tanh<kK1>(enter, X, H1, lane);
     layer_tanh<kK2>(enter, H1, H2, lane);
