@@ -48,7 +48,8 @@ def test_policy_abi_host_side_errors():
     """spl_policy_* argument checks (include/splendor_policy.h) run before any device work."""
     from splendor_gym import _native
     lib = _native.load_library()
-    assert lib.spl_policy_bytes(0) == 18 * 20480 and lib.spl_policy_bytes(1) == 35 * 20480
+    # actor: 18 bf16 chunks; full image: 35 chunks + the fp32 critic output layer (w3, b3, padding)
+    assert lib.spl_policy_bytes(0) == 18 * 20480 and lib.spl_policy_bytes(1) == 35 * 20480 + 272 * 4
     assert lib.spl_policy_pack(None, None, None, None) == -1
     assert b"actor" in lib.spl_last_error()
     assert lib.spl_policy_act(None, 0, 1, None, None) == -1
