@@ -5,28 +5,35 @@
 
 One "step" = one SplendorEnv.step on every table of the batch (BASELINE.json config 3: legal
 mask + uniform-random policy, same-step autoreset, obs int32[297] + mask int8[45] + reward +
-terminated + flags written per table-step, terminal rows to final_obs).  Actions come from the
-device policy (Philox over the new mask).  Two launch shapes compute the same trajectories and
-write the same per-step outputs (tests/test_gpu_parity.py::test_rollout_equals_step_chain):
-  --mode rollout  (headline) one spl_rollout launch per 16 env steps: state stays in registers
-                  and each step's stores drain while the next step computes
-  --mode step     one spl_step launch per env step (the drop-in SplendorEnv.step path);
-                  the mode not selected is measured too and reported as "other_mode"
-plus a pool refill every 64 steps (2p; 32 at 3p, 16 at 4p).  Inputs are resident in HBM before the timed region; the
-timed region replays captured HIP graphs of 64 steps.
+terminated + flags + winner written per table-step, terminal rows to final_obs).  Actions come
+from the device policy (Philox over the new mask).  Two launch shapes compute the same
+trajectories and write the same per-step outputs (tests/test_gpu_parity.py::test_rollout_equals_step_chain):
+  --mode rollout  (headline) one spl_rollout launch per 64 env steps: state stays in registers,
+                  each step's stores drain while the next step computes, and step k's outputs go
+                  to block k of a [64, T, ...] rollout store (≈10 GB at 65536 tables: far larger
+                  than the 256 MiB Infinity Cache, so every output byte reaches HBM)
+  --mode step     one spl_step launch per env step (the drop-in SplendorEnv.step path), timed as
+                  captured HIP graphs of whole refill periods
+The mode not selected is measured too ("other_mode"), and the rollout kernel is measured a second
+time writing every step into the same [T, ...] block ("in_place_l3": that ~81 MB block stays
+resident in the Infinity Cache, so it is NOT an HBM figure and is never the headline).
+
+--steps / --warmup are rounded UP to whole plan units (step_plan): a unit is two launches (the
+action buffers alternate) and whole pool-refill periods; "steps" in the JSON line is the number
+of env steps actually timed.  Warm-up is at least one unit (one full launch and one refill cycle).
 
 Weak scaling: each rank owns `--tables` tables (global ids rank*T ...), no collective in the
 step path; after the timed region one all-gather (RCCL) collects episode returns.  value =
 tables x world x steps / max-over-ranks wall time.
 
-Printed on rank 0: ONE JSON line with the roofline of the mode's kernel (HIP events around each
-launch of an eager window right after the timed replays; algorithmic bytes per SURVEY.md §8d:
-1370 B per 2-player table-step) and, at N=1, the CPU baseline (the C oracle port, one process
-per core).
+Printed on rank 0: ONE JSON line with the roofline of the headline kernel (HIP events around each
+launch inside the timed region, on the launch stream) and, at N=1, the CPU baseline (the C oracle
+port, one process per core, bounded sample).
 """
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -37,11 +44,55 @@ for _p in (REPO, os.path.join(REPO, "splendor-gym_amd")):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
-ALGO_BYTES = {2: 1370, 3: 1408, 4: 1446}  # 2*S_P + 297*4 + 45 + 4 + 4 + 1 (3p interpolated)
+HBM_ACHIEVABLE_GBS = 6290.0    # the guide's measured float4-copy ceiling (MI355X_MICROARCH.md:36)
+# canonical packed mutable state per table (S_2 = 64 B, S_4 = 102 B; 3p interpolated)
+STATE_BYTES = {2: 64, 3: 83, 4: 102}
+# per table-step outputs of both kernels: obs int32[297] + mask int8[45] + reward f32 + terminated u8
+# + flags u8 + winner i8
+OUT_BYTES = 297 * 4 + 45 + 4 + 1 + 1 + 1
+OBS_ROW = 297 * 4
+# SURVEY.md §8d drop-in figure for k_step: 2*S_P + obs + mask + action + reward + terminated
+STEP_ALGO_BYTES = {p: 2 * s + 297 * 4 + 45 + 4 + 4 + 1 for p, s in STATE_BYTES.items()}  # 2p: 1370
 # pool refill period per player count: three pool deals per table must cover the resets between
 # refills (random games last ~77 plies at 2p, ~29 at 4p)
 REFILL_EVERY = {2: 64, 3: 32, 4: 16}
 ROLLOUT_K = 64     # env steps per spl_rollout launch (one fused pool refill per launch at 2p)
+
+
+def step_plan(mode, steps, warmup, refill_period, rollout_k=ROLLOUT_K, graph_steps=128):
+    """Turn the requested --steps/--warmup into what is actually run.
+
+    unit   = lcm(2 launches, refill period): the two action buffers alternate per launch, and a
+             captured graph must hold whole refill periods (the library schedules refills from
+             the arena's step counter, which the graph bakes in).
+    K      = steps timed    = --steps rounded up to whole units (>= 1 unit)
+    W      = warm-up steps  = --warmup rounded up to whole units (>= 1 unit: one full launch + a
+             refill cycle, whatever --warmup says)
+    G      = steps per captured graph (step mode only; 0 = eager launches): the largest multiple
+             of unit that divides K and is <= max(graph_steps, unit); rollout mode is timed eagerly
+             (one ~0.8 ms launch per 64 steps: launch overhead is hidden by the queue)
+    launches = K / per (per = steps per launch)
+    """
+    if mode not in ("step", "rollout"):
+        raise ValueError(mode)
+    per = 1 if mode == "step" else int(rollout_k)
+    if per <= 0:
+        raise ValueError("rollout_k must be positive")
+    r = int(refill_period)
+    unit = 2 * per if r <= 0 else (2 * per) * r // math.gcd(2 * per, r)
+    k = max(1, -(-max(int(steps), 1) // unit)) * unit
+    w = max(1, -(-max(int(warmup), 0) // unit)) * unit
+    g = 0
+    if mode == "step" and graph_steps and graph_steps > 0:
+        cap = max(int(graph_steps), unit)
+        g = unit
+        m = unit
+        while m <= min(cap, k):
+            if k % m == 0:
+                g = m
+            m += unit
+    return {"mode": mode, "per": per, "unit": unit, "K": k, "W": w, "G": g, "launches": k // per,
+            "requested_steps": int(steps), "requested_warmup": int(warmup)}
 
 
 def cpu_baseline(players, procs, steps_per_proc):
@@ -79,23 +130,21 @@ def cpu_baseline(players, procs, steps_per_proc):
                        "engine measured at 5.4k steps/s/core in SURVEY.md §6")}
 
 
-def load_pmc_traffic(players, tables, mode, steps_per_launch):
-    """HBM bytes per launch of the mode's kernel from the committed rocprofv3 PMC summary."""
+def load_pmc_traffic(players, tables, variant, steps_per_launch):
+    """HBM bytes per launch of the variant's kernel from the committed rocprofv3 PMC summary."""
     path = os.path.join(REPO, "profiles", "pmc_summary.json")
-    kern = "k_step" if mode == "step" else "k_rollout"
     try:
         with open(path) as f:
             d = json.load(f)
         if (d.get("players") == players and d.get("tables") == tables
-                and d.get("steps_per_launch", {}).get(kern) == steps_per_launch):
-            return d.get("hbm_bytes_per_launch", {}).get(kern), os.path.relpath(path, REPO)
+                and d.get("steps_per_launch", {}).get(variant) == steps_per_launch):
+            return d.get("hbm_bytes_per_launch", {}).get(variant), os.path.relpath(path, REPO)
     except (OSError, ValueError, AttributeError):
         pass
     return None, None
 
 
 def main():
-    global ROLLOUT_K
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1024)
@@ -107,12 +156,15 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--cpu-steps", type=int, default=1_000_000, help="env steps per CPU process")
     ap.add_argument("--graph-steps", type=int, default=128,
-                    help="steps per captured HIP graph (multiple of 128); 0 = eager launches")
+                    help="step mode: steps per captured HIP graph (rounded to whole plan units); 0 = eager")
     ap.add_argument("--mode", choices=("step", "rollout"), default="rollout",
                     help="rollout: one spl_rollout launch per "
                          f"{ROLLOUT_K} env steps; step: one spl_step launch per env step (same trajectories "
                          "and per-step outputs, tests/test_gpu_parity.py::test_rollout_equals_step_chain)")
-    ap.add_argument("--only", action="store_true", help="skip measuring the other mode (reported as other_mode)")
+    ap.add_argument("--only", action="store_true", help="measure only --mode's headline variant")
+    ap.add_argument("--outputs", choices=("store", "inplace"), default="store",
+                    help="rollout mode: per-step blocks of a [K, T, ...] rollout store (headline) or every "
+                         "step into the same block (L3-resident; labelled in_place_l3)")
     ap.add_argument("--rollout-k", type=int, default=ROLLOUT_K, help="env steps per spl_rollout launch")
     ap.add_argument("--refill-every", type=int, default=0, help="0 = per player count (64/32/16)")
     ap.add_argument("--refill", choices=("fused", "separate"), default="fused",
@@ -122,7 +174,6 @@ def main():
                     help="rollout mode: two-wave pipelined kernel (auto: 32 or 64 tables per workgroup by grid "
                          "size; always: 64; half: 32) vs one wave per 64 tables (off)")
     args = ap.parse_args()
-    ROLLOUT_K = args.rollout_k
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank_env = int(os.environ.get("RANK", "0"))
@@ -143,9 +194,8 @@ def main():
     torch.cuda.set_device(dev)
     T, P = args.tables, args.players
     R = args.refill_every or REFILL_EVERY[P]
+    RK = args.rollout_k
     table0 = rank * T
-    # the library schedules the pool refills: every R steps (spl_step: a spl_refill launch; spl_rollout:
-    # inside the rollout launch unless --refill separate)
     pipe = {"auto": True, "always": "always", "half": "half", "off": False}[args.pipeline]
     eng = Engine(T, P, device=dev, refill_period=R, table0=table0, refill_fused=args.refill == "fused",
                  pipeline=pipe)
@@ -155,61 +205,85 @@ def main():
     eng.sample_uniform(out=buf[0], seed=args.seed, ply=0)
     ep_ret = torch.zeros(T, dtype=torch.float32, device=dev)
     ep_cnt = torch.zeros(T, dtype=torch.int32, device=dev)
-    ply_base = torch.zeros(1, dtype=torch.int64, device=dev)  # policy counter base, advanced per replay
+    ply_base = torch.zeros(1, dtype=torch.int64, device=dev)  # policy counter base (graph replays advance it)
 
-    def mkargs(a_in, a_out):
-        return _native.StepArgs(actions=a_in.data_ptr(), obs=eng.obs.data_ptr(), mask=eng.mask.data_ptr(),
-                                reward=eng.reward.data_ptr(), terminated=eng.terminated.data_ptr(),
-                                flags=eng.flags.data_ptr(), winner=eng.winner.data_ptr(),
-                                final_obs=eng.final_obs.data_ptr(), autoreset=1, next_actions=a_out.data_ptr(),
+    # rollout store: step k of a launch writes block k (obs/final_obs 5 GB each at 65536 tables)
+    store = None
+
+    def get_store():
+        nonlocal store
+        if store is None:
+            store = dict(obs=torch.empty((RK, T, 297), dtype=torch.int32, device=dev),
+                         mask=torch.empty((RK, T, 45), dtype=torch.int8, device=dev),
+                         reward=torch.empty((RK, T), dtype=torch.float32, device=dev),
+                         terminated=torch.empty((RK, T), dtype=torch.uint8, device=dev),
+                         flags=torch.empty((RK, T), dtype=torch.uint8, device=dev),
+                         winner=torch.empty((RK, T), dtype=torch.int8, device=dev),
+                         final_obs=torch.empty((RK, T, 297), dtype=torch.int32, device=dev))
+        return store
+
+    def mkargs(a_in, a_out, bufs):
+        return _native.StepArgs(actions=a_in.data_ptr(), obs=bufs["obs"].data_ptr(), mask=bufs["mask"].data_ptr(),
+                                reward=bufs["reward"].data_ptr(), terminated=bufs["terminated"].data_ptr(),
+                                flags=bufs["flags"].data_ptr(), winner=bufs["winner"].data_ptr(),
+                                final_obs=bufs["final_obs"].data_ptr(), autoreset=1, next_actions=a_out.data_ptr(),
                                 ply_base=ply_base.data_ptr(), policy_seed=args.seed, ply=0, table0=table0,
-                                ep_return=ep_ret.data_ptr(),
-                                ep_count=ep_cnt.data_ptr())
+                                ep_return=ep_ret.data_ptr(), ep_count=ep_cnt.data_ptr())
 
-    step_args = [mkargs(buf[0], buf[1]), mkargs(buf[1], buf[0])]
+    eng_bufs = dict(obs=eng.obs, mask=eng.mask, reward=eng.reward, terminated=eng.terminated, flags=eng.flags,
+                    winner=eng.winner, final_obs=eng.final_obs)
     ctx, desc = eng.ctx, ctypes.byref(eng.desc)
     stream = eng.stream()
 
-    def run(mode, k0, k1, strm, ev=None):
-        """Steps k0..k1-1 (ply k+1 relative to ply_base).  mode "step": one spl_step launch per
-        step; "rollout": one spl_rollout launch per ROLLOUT_K steps.  Refills every R steps are
-        issued by the library (the arena's step counter)."""
-        per = 1 if mode == "step" else ROLLOUT_K
+    def run(variant, k0, k1, strm, ev=None):
+        """Env steps k0..k1-1 (ply k+1 relative to ply_base).  variant "step": one spl_step launch
+        per step; "rollout_store"/"rollout_inplace": one spl_rollout launch per RK steps with
+        per-step blocks / in place.  Refills every R steps are issued by the library."""
+        per = 1 if variant == "step" else RK
+        bufs = get_store() if variant == "rollout_store" else eng_bufs
+        sargs = [mkargs(buf[0], buf[1], bufs), mkargs(buf[1], buf[0], bufs)]
         for i, k in enumerate(range(k0, k1, per)):
-            sa = step_args[(k // per) & 1]
+            sa = sargs[(k // per) & 1]
             sa.ply = k + 1
             if ev is not None:
                 ev[0][i].record()
-            if mode == "step":
+            if variant == "step":
                 _native.check(lib, lib.spl_step(ctx, desc, ctypes.byref(sa), strm))
             else:
-                _native.check(lib, lib.spl_rollout(ctx, desc, ctypes.byref(sa), ROLLOUT_K, 0, strm))
+                _native.check(lib, lib.spl_rollout(ctx, desc, ctypes.byref(sa), RK,
+                                                   1 if variant == "rollout_store" else 0, strm))
             if ev is not None:
                 ev[1][i].record()
 
-    def measure(mode, k_base):
-        """Warm up, capture, time K steps; returns the timing record.  Steps are numbered from
-        k_base so every measurement continues the same trajectories (ply_base)."""
-        W = (args.warmup // (2 * R)) * (2 * R)  # action-buffer parity and refill alignment
+    def events(n):
+        return ([torch.cuda.Event(enable_timing=True) for _ in range(n)],
+                [torch.cuda.Event(enable_timing=True) for _ in range(n)])
+
+    def measure(variant, k_base):
+        """Warm up, time K steps; returns the timing record.  Steps are numbered from k_base so
+        every measurement continues the same trajectories with fresh policy counters."""
+        plan = step_plan("step" if variant == "step" else "rollout", args.steps, args.warmup, R, RK,
+                         args.graph_steps)
+        K, W, G, per = plan["K"], plan["W"], plan["G"], plan["per"]
+        # warm-up: W steps, eager (also allocates the rollout store outside the timed region)
         ply_base.fill_(k_base)
-        run(mode, 0, W, stream)
-        K, G = args.steps, args.graph_steps
-        graph, how = None, "eager"
+        run(variant, 0, W, stream)
+        graph = None
+        how = "eager launches, HIP events around each launch"
         if G > 0:
-            if G % (2 * R) or K % G:
-                raise SystemExit(f"--graph-steps must be a multiple of {2 * R} that divides --steps")
             try:
                 torch.cuda.synchronize(dev)
                 ply_base.fill_(k_base + W)
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
-                    run(mode, 0, G, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+                    run(variant, 0, G, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
                     ply_base.add_(G)
                 how = f"hipGraph replays of {G} steps"
             except Exception as exc:  # capture unsupported: time eager launches instead
                 print(f"graph capture failed ({exc}); timing eager launches", file=sys.stderr)
                 graph, G = None, 0
-        per = 1 if mode == "step" else ROLLOUT_K
+        torch.cuda.synchronize(dev)
+        eps0 = int(ep_cnt.sum().item())
         barrier(dev)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
@@ -218,86 +292,114 @@ def main():
                 graph.replay()
             ev = None
         else:
-            ev = ([torch.cuda.Event(enable_timing=True) for _ in range(K // per)],
-                  [torch.cuda.Event(enable_timing=True) for _ in range(K // per)])
+            ev = events(K // per)
             ply_base.fill_(k_base + W)
-            run(mode, 0, K, stream, ev)
+            run(variant, 0, K, stream, ev)
         torch.cuda.synchronize(dev)
         barrier(dev)
         elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
+        terminations = int(ep_cnt.sum().item()) - eps0
+        kt = "HIP events around each launch in the timed region"
+        k_next = k_base + W + K + 1
         if ev is None:
             # ROCm rejects timing events as graph nodes ("External events are disallowed"), so the
             # kernel duration comes from HIP events around each launch of an eager window of the
             # same loop, run right after the timed replays on the same stream and state.
-            nwin = max(64, 4 * per)  # at least four launches
-            ev = ([torch.cuda.Event(enable_timing=True) for _ in range(nwin // per)],
-                  [torch.cuda.Event(enable_timing=True) for _ in range(nwin // per)])
-            ply_base.fill_(k_base + W + K + 1)
-            run(mode, 0, nwin, stream, ev)
+            nwin = plan["unit"] * max(1, -(-64 // plan["unit"]))
+            ev = events(nwin // per)
+            ply_base.fill_(k_next)
+            run(variant, 0, nwin, stream, ev)
             torch.cuda.synchronize(dev)
+            kt = f"HIP events around each of {nwin // per} eager launches right after the timed replays"
+            k_next += nwin + 1
         nev = len(ev[0])
         launch_s = sum(ev[0][i].elapsed_time(ev[1][i]) for i in range(nev)) / nev / 1e3
-        return {"mode": mode, "elapsed": elapsed, "launch_s": launch_s, "steps_per_launch": per, "how": how,
-                "nev": nev, "k_next": k_base + W + K + 1 + max(64, 4 * per) + 1}
+        return {"variant": variant, "plan": plan, "elapsed": elapsed, "launch_s": launch_s, "how": how,
+                "kernel_timing": kt, "terminations": terminations, "k_next": k_next}
 
-    main_rec = measure(args.mode, 0)
-    alt_rec = None
+    headline = "step" if args.mode == "step" else ("rollout_store" if args.outputs == "store" else "rollout_inplace")
+    variants = [headline]
     if not args.only:
-        alt_rec = measure("rollout" if args.mode == "step" else "step", main_rec["k_next"])
-    K = args.steps
+        variants += [v for v in ("rollout_store", "rollout_inplace", "step") if v != headline]
+    recs, k_next = {}, 0
+    for v in variants:
+        recs[v] = measure(v, k_next)
+        k_next = recs[v]["k_next"]
     # correctness canaries on the measured run: no error flags, episodes completed
     bad = int(((eng.flags & (_native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT)) != 0).sum().item())
     rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
     episodes = int(cnts.sum().item())
 
+    def kernel_name(variant):
+        if variant == "step":
+            return f"spl::k_step<{P}>"
+        rk = "k_rollout" if args.pipeline == "off" else "k_rollout_ws"
+        return f"spl::{rk}<{P}> ({RK} steps per launch, {'per-step store' if variant == 'rollout_store' else 'in place'})"
+
     def summary(rec):
-        total_steps = T * world * K
-        algo = ALGO_BYTES[P] * T * rec["steps_per_launch"]
-        rk = "k_rollout" if args.pipeline == "off" else "k_rollout_ws"  # two-wave pipelined kernel
-        kname = f"spl::k_step<{P}>" if rec["mode"] == "step" else f"spl::{rk}<{P}> ({ROLLOUT_K} steps per launch)"
-        return {"mode": rec["mode"], "value": round(total_steps / rec["elapsed"], 1),
-                "ms_per_step": round(rec["elapsed"] / K * 1e3, 4),
-                "roofline": {"bound": "hbm", "achieved": round(algo / rec["launch_s"] / 1e9, 1),
-                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(algo / rec["launch_s"] / 1e9 / HBM_PEAK_GBS, 4),
-                             "kernel": kname, "kernel_avg_us": round(rec["launch_s"] * 1e6, 2),
-                             "kernel_timing": ("HIP events around each launch in the timed region" if rec["how"] == "eager"
-                                               else f"HIP events around each of {rec['nev']} eager launches right "
-                                                    "after the timed replays"),
-                             "algo_bytes_per_launch": algo},
-                "launch": rec["how"]}
+        v, plan = rec["variant"], rec["plan"]
+        K, per = plan["K"], plan["per"]
+        launches = K // per
+        if v == "step":
+            algo = STEP_ALGO_BYTES[P] * T
+            algo_note = f"{STEP_ALGO_BYTES[P]} B per table-step (SURVEY.md §8d: 2*S_P + obs + mask + action + reward + terminated)"
+        else:
+            # state read+write once per launch, first/next actions, per-step outputs, terminal rows
+            term_per_launch = rec["terminations"] / launches
+            algo = (2 * STATE_BYTES[P] + 8) * T + OUT_BYTES * T * per + OBS_ROW * term_per_launch
+            algo_note = (f"2*S_P/{per} + {OUT_BYTES} B per table-step (obs 1188 + mask 45 + reward 4 + terminated/flags/"
+                         f"winner 3) + 8 B/table of actions per launch + 1188 B per terminal row "
+                         f"({term_per_launch:.0f} per launch, counted in the timed region)")
+        achieved = algo / rec["launch_s"] / 1e9
+        return {"variant": v, "value": round(T * world * K / rec["elapsed"], 1),
+                "steps": K, "ms_per_step": round(rec["elapsed"] / K * 1e3, 4),
+                "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(achieved / HBM_PEAK_GBS, 4),
+                             "frac_of_achievable": round(achieved / HBM_ACHIEVABLE_GBS, 4),
+                             "kernel": kernel_name(v), "kernel_avg_us": round(rec["launch_s"] * 1e6, 2),
+                             "kernel_timing": rec["kernel_timing"], "algo_bytes_per_launch": round(algo),
+                             "algo_bytes_note": algo_note},
+                "launch": rec["how"], "plan": plan}
 
     if rank == 0:
-        main = summary(main_rec)
-        traffic, traffic_src = load_pmc_traffic(P, T, main_rec["mode"], main_rec["steps_per_launch"])
-        roof = dict(main["roofline"], traffic=traffic, traffic_source=traffic_src)
+        main_s = summary(recs[headline])
+        pmc_key = {"step": "k_step", "rollout_store": "k_rollout_store", "rollout_inplace": "k_rollout"}[headline]
+        traffic, traffic_src = load_pmc_traffic(P, T, pmc_key, main_s["plan"]["per"])
+        roof = dict(main_s["roofline"], traffic=traffic, traffic_source=traffic_src,
+                    traffic_over_algo=None if traffic is None else round(traffic / main_s["roofline"]["algo_bytes_per_launch"], 4))
+        plan = main_s["plan"]
         out = {
             "metric": f"env-steps/sec (whole node), {P}p {T} tables/GPU",
-            "value": main["value"],
+            "value": main_s["value"],
             "unit": "env-steps/s",
             "n_gpus": world,
-            "steps": K,
-            "warmup": args.warmup,
-            "ms_per_step": main["ms_per_step"],
+            "steps": plan["K"],
+            "warmup": plan["W"],
+            "ms_per_step": main_s["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic: seeded deals (table id = env seed), device uniform-random legal policy",
             "config": {"workload": f"{P}-player SplendorEnv.step x {T} tables per GPU, legal mask + uniform-random "
-                                   "policy, same-step autoreset, obs int32[297] + mask int8[45] per table-step",
+                                   "policy, same-step autoreset, obs int32[297] + mask int8[45] per table-step"
+                                   + (" into a per-step rollout store" if headline == "rollout_store" else ""),
                        "tables_per_gpu": T, "players": P, "parallelism": f"table-sharded x{world}",
-                       "refill_every": R, "refill": args.refill if main_rec["mode"] == "rollout" else "separate", "pipeline": args.pipeline,
-                       "rollout_steps_per_launch": ROLLOUT_K, "mode": main["mode"],
-                       "launch": main["launch"]},
+                       "refill_every": R, "refill": args.refill if headline != "step" else "separate",
+                       "pipeline": args.pipeline, "rollout_steps_per_launch": RK, "variant": headline,
+                       "launch": main_s["launch"], "requested_steps": plan["requested_steps"],
+                       "requested_warmup": plan["requested_warmup"],
+                       "step_rounding": f"steps/warmup rounded up to whole units of {plan['unit']} (step_plan)"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "episodes": episodes,
             "mean_final_reward_p0": round(float(rets.sum().item()) / max(1, episodes), 4),
             "error_flags": bad,
         }
-        if alt_rec is not None:
-            out["other_mode"] = summary(alt_rec)
+        for v in variants[1:]:
+            s = summary(recs[v])
+            s.pop("plan")
+            out["in_place_l3" if v == "rollout_inplace" else ("other_mode" if v == "step" else v)] = s
         print(json.dumps(out))
     eng.close()
     if world > 1:

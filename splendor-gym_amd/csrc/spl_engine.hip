@@ -73,7 +73,7 @@ constexpr int kObsDim = 297;
 #endif
 constexpr int ABL_LEGAL_PRE = 1, ABL_APPLY = 2, ABL_LEGAL_POST = 4, ABL_FINAL = 8, ABL_RESET = 16, ABL_ENCODE = 32,
               ABL_STORE = 64, ABL_MASK_STORE = 128, ABL_SMALL_OUT = 256, ABL_TAB_STORE = 512, ABL_OBS_STORE = 1024,
-              ABL_LOAD = 2048, ABL_TOKLIM = 4096, ABL_NOBLE = 8192;
+              ABL_LOAD = 2048, ABL_TOKLIM = 4096, ABL_NOBLE = 8192, ABL_DECK_GATHER = 16384, ABL_LUT_GATHER = 32768;
 __device__ __forceinline__ bool abl(int bit) { return (SPL_ABL & bit) != 0; }
 
 // Phase stamps for the diagnostic build only (-DSPL_STAMPS, tools/stamps.py): lane 0 of every
@@ -98,7 +98,27 @@ __device__ uint64_t *g_rstamps;
         rst_hi[i] = lane_id() == (k) ? (int)(uint32_t)(tt_ >> 32) : rst_hi[i];                   \
         __builtin_amdgcn_sched_barrier(0);                                                       \
     } while (0)
+// k_rollout_ws: both waves keep kWsStamps stamps per step in registers (lane k = step k, K <= 64),
+// written to g_wsstamps[workgroup][wave][step][kWsStamps] at the end.
+constexpr int kWsStamps = 4;
+__device__ uint64_t *g_wsstamps;
+__device__ uint32_t *g_wshwid;  // [workgroup][wave][2]: HW_ID (SIMD, CU, SE) and XCC_ID of each wave
+__device__ uint64_t *g_wsclk;   // [workgroup][4]: s_memtime / s_memrealtime at the rules wave's start and end
+#define WSHWID(wave)                                                                             \
+    do {                                                                                         \
+        if (g_wshwid && lane_id() == 0) {                                                        \
+            g_wshwid[((size_t)blockIdx.x * 2 + (wave)) * 2 + 0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  \
+            g_wshwid[((size_t)blockIdx.x * 2 + (wave)) * 2 + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20); \
+        }                                                                                        \
+    } while (0)
+#define WSSTAMP(i, k) RSTAMP(i, k)
 #else
+#define WSHWID(wave) \
+    do {             \
+    } while (0)
+#define WSSTAMP(i, k) \
+    do {              \
+    } while (0)
 #define STAMP(i) \
     do {         \
     } while (0)
@@ -828,12 +848,24 @@ __device__ __forceinline__ void store_row_direct(const Tab<P> &T, const Consts &
 // unrolled copy, splits every store into four strided dword stores (half the store bandwidth).
 typedef int v4i __attribute__((ext_vector_type(4)));
 
+// Output-stream store of one 16-byte vector.  NT (the per-step rollout store, written once and
+// not read back by this launch): non-temporal, so the 5 GB stream does not push the token table,
+// deck records and state out of L2 / the Infinity Cache — the rules wave's gathers stay fast
+// (rollout store 1225 -> 1109 us per 64 steps at 65 536 tables).  In-place outputs keep plain
+// stores: their block stays Infinity-Cache resident for the consumer (NT: 794 -> 1020 us).
+template <bool NT>
+__device__ __forceinline__ void st_v4(v4i *p, v4i v) {
+    if (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 __device__ __forceinline__ v4i expand4(uint32_t w) {
     v4i v = {(int)(w & 0xFFu), (int)((w >> 8) & 0xFFu), (int)((w >> 16) & 0xFFu), (int)(w >> 24)};
     return v;
 }
 
 // Part [d0, d1) (LDS words, multiples of 64*5 except the end) of a FULL wave's observation block.
+template <bool NT = false>
 __device__ __forceinline__ void store_obs_range(const uint8_t *rows_lds, int32_t *dst, int d0, int d1) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
     v4i *out = reinterpret_cast<v4i *>(dst);
@@ -845,14 +877,14 @@ __device__ __forceinline__ void store_obs_range(const uint8_t *rows_lds, int32_t
 #pragma unroll
         for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
 #pragma unroll
-        for (int u = 0; u < U; ++u) out[d + 64 * u] = expand4(w[u]);
+        for (int u = 0; u < U; ++u) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
     }
     uint32_t w[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) w[u] = (d + 64 * u < d1) ? src[d + 64 * u] : 0u;
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        if (d + 64 * u < d1) out[d + 64 * u] = expand4(w[u]);
+        if (d + 64 * u < d1) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
 }
 constexpr int kObsBlockWords = 64 * kObsDim / 4;  // 4752 LDS words = 4752 16-byte stores per wave
 constexpr int kObsSplit = 64 * 5 * 7;             // 2240: 35 stores per lane in the first part
@@ -860,7 +892,7 @@ constexpr int kObsSplit = 64 * 5 * 7;             // 2240: 35 stores per lane in
 // Block store of this wave's observation rows: LDS bytes [rows][297] -> int32 [rows][297] at
 // dst (16-byte aligned: 64-row blocks are 76032 B).  Dword d of the block is LDS word d.
 // R = the workgroup's table count (64, or 32 in the half-populated two-wave rollout).
-template <int R = 64>
+template <int R = 64, bool NT = false>
 __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int rows, int32_t *dst) {
     const int nbytes = rows * kObsDim;
     const int full = nbytes >> 2;
@@ -876,17 +908,17 @@ __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int row
 #pragma unroll
             for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
 #pragma unroll
-            for (int u = 0; u < U; ++u) out[d + 64 * u] = expand4(w[u]);
+            for (int u = 0; u < U; ++u) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
         }
         uint32_t w[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) w[u] = (d + 64 * u < kFull) ? src[d + 64 * u] : 0u;
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (d + 64 * u < kFull) out[d + 64 * u] = expand4(w[u]);
+            if (d + 64 * u < kFull) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
         return;
     }
-    for (; d < full; d += 64) out[d] = expand4(src[d]);
+    for (; d < full; d += 64) st_v4<NT>(out + d, expand4(src[d]));
     for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) dst[b] = (int32_t)rows_lds[b];
 }
 
@@ -894,6 +926,7 @@ __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int row
 // bits are first laid out as ONE bit stream in LDS (row r at bits 45r..45r+44; each stream
 // dword is cut from at most two rows), so every output dword is one nibble of the stream,
 // spread to 4 bytes by a multiply: bit i of n moves to bit 8i in n * 0x204081.
+template <bool NT = false>
 __device__ __forceinline__ void store_mask_block(const uint64_t *mask, uint32_t *mbits, int rows, int8_t *dst) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -915,7 +948,7 @@ __device__ __forceinline__ void store_mask_block(const uint64_t *mask, uint32_t 
             v4i v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = (int)((((half >> (4 * q)) & 0xFu) * 0x00204081u) & 0x01010101u);
-            out4[c] = v;
+            st_v4<NT>(out4 + c, v);
         }
         return;
     }
@@ -1221,7 +1254,7 @@ __device__ __forceinline__ StepPre step_prefetch(const Tab<P> &T, int action, bo
     if (live_tab && ptier >= 0) {
         const int len = (int)bget(T.sw[SW_DECK], ptier);
         const uint8_t *live = live_rec(A, t, T.sw[SW_MISC]);
-        if (len > 0) pre.top = live[tier_base(ptier) + len - 1];
+        if (len > 0) pre.top = abl(ABL_DECK_GATHER) ? (uint32_t)(len + 3 * ptier) : live[tier_base(ptier) + len - 1];
     }
     if (live_tab && action >= 0 && action < SPL_NUM_ACTIONS) {
         const int tp = get_to_play(T.sw);
@@ -1230,7 +1263,7 @@ __device__ __forceinline__ StepPre step_prefetch(const Tab<P> &T, int action, bo
         int bank[6];
         get_bank(T.sw, bank);
         pre.key = predict_lut_key(unpack_pl(pw4), bank, action, get_turn(T.sw), tp);
-        if (pre.key >= 0) pre.e = Tb.lut[pre.key];
+        if (pre.key >= 0) pre.e = abl(ABL_LUT_GATHER) ? make_uint4(0x12345678u, 0x9abcdef0u, 0x0fedcba9u, (uint32_t)pre.key) : Tb.lut[pre.key];
     }
     return pre;
 }
@@ -1638,6 +1671,7 @@ struct __align__(16) WsLDS : Consts {
     static_assert(!kScrInSlot || kW * 64 * 4 >= 64 * kScrStride, "scratch must fit the state slot");
     uint32_t st[2][kW][64];
     uint32_t tst[2][kTerm][kW];
+    uint32_t small[2][64];  // the step's reward / terminated / flags / winner / episode event (pack_small)
     uint64_t mask[2][64];
     uint64_t fin[2];
     uint32_t mbits[96];
@@ -1658,6 +1692,30 @@ template <int P>
 __device__ __forceinline__ void set_tab_word(Tab<P> &T, int w, uint32_t v) {
     if (w < SW_COUNT) T.sw[w] = v;
     else T.pw[(w - SW_COUNT) >> 2][(w - SW_COUNT) & 3] = v;
+}
+
+// The rules wave's per-step small outputs, packed for the hand-off: the OUTPUT wave issues every
+// global write of a step.  A store the rules wave issued would sit in its vmcnt queue ahead of
+// the next step's deck / token-table gathers (gfx9 counts loads and stores in one in-order
+// counter), so each step's first use of a gathered value would wait for a write acknowledgement
+// from behind the whole chip's observation stream: 12.8 -> 19.6 us per step once that stream
+// goes to HBM instead of the Infinity Cache (rollout store, 65 536 tables).
+// bits 0-7 flags, 8 terminated, 9 valid, 10-12 winner + 1, 13-15 reward code, 16-17 code of
+// player 0's final reward (envs/splendor_env.py:92-115), 18 episode ended (ep_return / ep_count).
+__device__ __forceinline__ uint32_t reward_code(float r) {
+    return r == 0.0f ? 0u : (r == -0.01f ? 1u : (r == -0.1f ? 2u : (r == 1.0f ? 3u : 4u)));
+}
+__device__ __forceinline__ float reward_of_code(uint32_t c) {
+    return c == 0u ? 0.0f : (c == 1u ? -0.01f : (c == 2u ? -0.1f : (c == 3u ? 1.0f : -1.0f)));
+}
+// player 0's final reward is one of 0, -1, -0.1, 1 (final_reward_p0)
+__device__ __forceinline__ uint32_t ep_code(float r) { return r == 0.0f ? 0u : (r == -1.0f ? 1u : (r == -0.1f ? 2u : 3u)); }
+__device__ __forceinline__ float ep_of_code(uint32_t c) {
+    return c == 0u ? 0.0f : (c == 1u ? -1.0f : (c == 2u ? -0.1f : 1.0f));
+}
+__device__ __forceinline__ uint32_t pack_small(bool valid, const StepOut &o, int winner, bool ep, float ep_add) {
+    return (o.flags & 0xFFu) | (o.term ? 1u << 8 : 0u) | (valid ? 1u << 9 : 0u) | ((uint32_t)(winner + 1) & 7u) << 10 |
+           reward_code(o.reward) << 13 | ep_code(ep_add) << 16 | (ep ? 1u << 18 : 0u);
 }
 
 __device__ __forceinline__ void ws_sync() {
@@ -1686,6 +1744,10 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
     load_tables_lds(L, Tb);
     ws_sync();
 
+    WSHWID(rules_wave ? 0 : 1);
+#ifdef SPL_STAMPS
+    const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (rules_wave) {
         const RefillSlots rs = refill_slots(K, S.autoreset ? refill : 0);
         Tab<P> T;
@@ -1703,10 +1765,15 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
         const uint64_t ply0 = S.ply + (S.ply_base ? *S.ply_base : 0ull);
         uint64_t cur_mask = 0ull;
         const uint64_t below = (1ull << lane) - 1ull;
+#ifdef SPL_STAMPS
+        int rst_lo[kWsStamps] = {0}, rst_hi[kWsStamps] = {0};
+#endif
         for (int k = 0; k < K; ++k) {
             const int b = k & 1;
             const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
+            WSSTAMP(0, k);
             StepOut o = step_rules(T, action, pre, valid, L, Tb, k > 0, cur_mask);
+            WSSTAMP(1, k);
             if (rs.due(k) && valid && pend_of(T.sw[SW_MISC]) > 0)  // fused pool refill
                 T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], L.scratch(b, lane), pool, pool_dirty);
             const int8_t wnr = (int8_t)get_winner(T.sw);
@@ -1721,17 +1788,9 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
                     store_row_direct(T, L, S.final_obs + (blk + (size_t)t) * kObsDim);
                 }
             }
-            if (valid && o.term) {  // per termination, as k_step (same float rounding)
-                if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], final_reward_p0(T));
-                if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
-            }
+            const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;  // per termination, as k_step
             if (valid && o.term && S.autoreset) autoreset_table(T, A, t, pool, L.scratch(b, lane), o, pool_dirty);
-            if (valid) {
-                S.reward[blk + t] = o.reward;
-                S.terminated[blk + t] = o.term ? 1 : 0;
-                S.flags[blk + t] = (uint8_t)o.flags;
-                if (S.winner) S.winner[blk + t] = wnr;
-            }
+            L.small[b][lane] = pack_small(valid, o, wnr, valid && o.term, ep_add);  // stored by the output wave
             action = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
             cur_mask = o.mask;
             if (k + 1 < K) pre = step_prefetch(T, action, valid, A, t, Tb);
@@ -1740,8 +1799,25 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
             L.mask[b][lane] = o.mask;
             const uint64_t fin_listed = __ballot(fin_me && idx < WsLDS<P>::kTerm);  // outside the lane-0 branch
             if (lane == 0) L.fin[b] = fin_listed;
+            WSSTAMP(2, k);
             ws_sync();  // hand-off of step k
+            WSSTAMP(3, k);
         }
+#ifdef SPL_STAMPS
+        {
+            const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+            if (g_wsclk && lane == 0) {
+                g_wsclk[blockIdx.x * 4 + 0] = clk0;
+                g_wsclk[blockIdx.x * 4 + 1] = rt0;
+                g_wsclk[blockIdx.x * 4 + 2] = clk1;
+                g_wsclk[blockIdx.x * 4 + 3] = rt1;
+            }
+        }
+        if (g_wsstamps && lane < K)
+            for (int i = 0; i < kWsStamps; ++i)
+                g_wsstamps[(((size_t)blockIdx.x * 2 + 0) * 64 + lane) * kWsStamps + i] =
+                    ((uint64_t)(uint32_t)rst_hi[i] << 32) | (uint32_t)rst_lo[i];
+#endif
         if (valid) {
             if (S.next_actions) S.next_actions[t] = action;
             store_tab(T, A, t);
@@ -1749,8 +1825,12 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
         }
     } else {
         const uint64_t below = (1ull << lane) - 1ull;
+#ifdef SPL_STAMPS
+        int rst_lo[kWsStamps] = {0}, rst_hi[kWsStamps] = {0};
+#endif
         for (int k = 0; k < K; ++k) {
             ws_sync();  // hand-off of step k
+            WSSTAMP(0, k);
             const int b = k & 1;
             const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
             Tab<P> T;
@@ -1777,14 +1857,44 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
             }
             encode_row(T, L.rows, L);
             wave_lds_sync();
+            WSSTAMP(1, k);
             int32_t *obs = S.obs + blk * kObsDim;
-            store_obs_block<TPW>(L.rows, rows, obs + (size_t)t0 * kObsDim);
-            store_mask_block(L.mask[b], L.mbits, rows, S.mask + blk * 45 + (size_t)t0 * 45);
+            if (abl(ABL_OBS_STORE)) {
+            } else if (per_step) {
+                store_obs_block<TPW, true>(L.rows, rows, obs + (size_t)t0 * kObsDim);
+            } else {
+                store_obs_block<TPW, false>(L.rows, rows, obs + (size_t)t0 * kObsDim);
+            }
+            WSSTAMP(2, k);
+            if (abl(ABL_MASK_STORE)) {
+            } else if (per_step) {
+                store_mask_block<true>(L.mask[b], L.mbits, rows, S.mask + blk * 45 + (size_t)t0 * 45);
+            } else {
+                store_mask_block<false>(L.mask[b], L.mbits, rows, S.mask + blk * 45 + (size_t)t0 * 45);
+            }
+            const uint32_t sm = L.small[b][lane];
+            if (sm & (1u << 9)) {  // valid lane: the rules wave's small outputs and episode statistics
+                S.reward[blk + t] = reward_of_code((sm >> 13) & 7u);
+                S.terminated[blk + t] = (uint8_t)((sm >> 8) & 1u);
+                S.flags[blk + t] = (uint8_t)(sm & 0xFFu);
+                if (S.winner) S.winner[blk + t] = (int8_t)((int)((sm >> 10) & 7u) - 1);
+                if (sm & (1u << 18)) {  // same per-table order and float rounding as k_step
+                    if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_of_code((sm >> 16) & 3u));
+                    if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
+                }
+            }
             if (__any(valid && get_moves(T.sw) > 255)) {
                 __builtin_amdgcn_s_waitcnt(0);
                 if (valid && get_moves(T.sw) > 255) obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
             }
+            WSSTAMP(3, k);
         }
+#ifdef SPL_STAMPS
+        if (g_wsstamps && lane < K)
+            for (int i = 0; i < kWsStamps; ++i)
+                g_wsstamps[(((size_t)blockIdx.x * 2 + 1) * 64 + lane) * kWsStamps + i] =
+                    ((uint64_t)(uint32_t)rst_hi[i] << 32) | (uint32_t)rst_lo[i];
+#endif
     }
 }
 
@@ -2094,6 +2204,18 @@ int spl_abi_version(void) { return SPL_ABI_VERSION; }
 #ifdef SPL_STAMPS
 int spl_debug_set_stamps(void *buf) {
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &buf, sizeof(buf)));
+    return SPL_OK;
+}
+int spl_debug_set_ws_clk(void *buf) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wsclk), &buf, sizeof(buf)));
+    return SPL_OK;
+}
+int spl_debug_set_ws_hwid(void *buf) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wshwid), &buf, sizeof(buf)));
+    return SPL_OK;
+}
+int spl_debug_set_ws_stamps(void *buf) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wsstamps), &buf, sizeof(buf)));
     return SPL_OK;
 }
 int spl_debug_set_rollout_stamps(void *buf) {

@@ -1,0 +1,50 @@
+"""bench.py's step plan: the driver's `--steps 20 --warmup 5` (and any other value) must run,
+time whole launches, and report the steps actually timed (VERDICT r01 "What's weak" 1)."""
+import pytest
+
+import bench
+
+
+@pytest.mark.parametrize("steps", [1, 20, 100, 1024])
+@pytest.mark.parametrize("players", [2, 3, 4])
+def test_rollout_plan_rounds_up_to_whole_launches(steps, players):
+    r = bench.REFILL_EVERY[players]
+    p = bench.step_plan("rollout", steps, 5, r, rollout_k=64)
+    assert p["per"] == 64
+    assert p["K"] >= steps and p["K"] % p["unit"] == 0
+    assert p["K"] % 64 == 0 and (p["K"] // 64) % 2 == 0  # action buffers alternate per launch
+    assert p["K"] % r == 0                                # whole refill periods
+    assert p["launches"] * p["per"] == p["K"]
+    assert p["W"] >= 64 + r or p["W"] >= p["unit"]        # one full launch and a refill cycle
+    assert p["W"] >= 64 and p["W"] % p["unit"] == 0
+    assert p["G"] == 0                                    # rollout mode is timed eagerly
+    assert p["K"] - steps < p["unit"]                     # smallest whole-unit cover
+
+
+@pytest.mark.parametrize("steps", [1, 20, 100, 1024])
+def test_step_plan_graph_divides_timed_steps(steps):
+    p = bench.step_plan("step", steps, 5, 64, graph_steps=128)
+    assert p["per"] == 1 and p["unit"] == 64
+    assert p["K"] >= steps and p["K"] % 64 == 0
+    assert p["G"] > 0 and p["G"] % p["unit"] == 0 and p["K"] % p["G"] == 0
+    assert p["G"] <= max(128, p["unit"])
+    assert p["W"] >= 64
+
+
+def test_driver_command_values():
+    p = bench.step_plan("rollout", 20, 5, 64)
+    assert (p["K"], p["W"], p["launches"]) == (128, 128, 2)
+    s = bench.step_plan("step", 20, 5, 64)
+    assert (s["K"], s["W"], s["G"]) == (64, 64, 64)
+
+
+def test_eager_step_plan_and_disabled_refill():
+    p = bench.step_plan("step", 20, 0, 0, graph_steps=0)
+    assert p["G"] == 0 and p["unit"] == 2 and p["K"] == 20 and p["launches"] == 20
+    q = bench.step_plan("rollout", 200, 0, 0, rollout_k=16)
+    assert q["unit"] == 32 and q["K"] == 224 and q["launches"] == 14
+
+
+def test_algorithmic_bytes_constants():
+    assert bench.STEP_ALGO_BYTES[2] == 1370 and bench.STEP_ALGO_BYTES[4] == 1446
+    assert bench.OUT_BYTES == 1240

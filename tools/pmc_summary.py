@@ -41,7 +41,10 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--tables", type=int, default=65536)
     ap.add_argument("--players", type=int, default=2)
-    ap.add_argument("--rollout-steps", type=int, default=16, help="env steps per k_rollout launch in the run")
+    ap.add_argument("--rollout-steps", type=int, default=64, help="env steps per k_rollout launch in the run")
+    ap.add_argument("--rollout-key", default="k_rollout_store",
+                    help="name under which the rollout kernel's traffic is recorded: k_rollout_store (bench "
+                         "--outputs store, per-step blocks) or k_rollout (--outputs inplace)")
     a = ap.parse_args()
     per, dur = load(a.pmc_dir)
     summary = {"tables": a.tables, "players": a.players, "source": a.pmc_dir, "kernels": {}}
@@ -76,11 +79,11 @@ def main():
             d["wrreq_bytes_64B"] = mean.get("TCC_EA0_WRREQ", 0) * 64
         summary["kernels"][k] = d
     summary["hbm_bytes_per_launch"] = {}
-    for k in ("k_step", "k_rollout"):
+    for k, name in (("k_step", "k_step"), ("k_rollout", a.rollout_key)):
         st = summary["kernels"].get(k, {})
         if "fetch_bytes" in st and "write_bytes" in st:
-            summary["hbm_bytes_per_launch"][k] = round(st["fetch_bytes"] + st["write_bytes"])
-    summary["steps_per_launch"] = {"k_step": 1, "k_rollout": a.rollout_steps}
+            summary["hbm_bytes_per_launch"][name] = round(st["fetch_bytes"] + st["write_bytes"])
+    summary["steps_per_launch"] = {"k_step": 1, a.rollout_key: a.rollout_steps}
     summary["hbm_bytes_note"] = ("FETCH_SIZE + WRITE_SIZE (KiB x 1024) per launch, uncorrected: the kernels' reads "
                                  "are 4-byte-per-lane planes and gathers, outside the guide's 16 B/lane calibration")
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
