@@ -9,6 +9,8 @@
  *                      once; also builds the token-return RNG table (engine/rules.py:170-176)
  *   spl_reset          envs/splendor_env.py:41-48 SplendorEnv.reset -> engine/state.py:181-211
  *                      initial_state (CPython MT19937 shuffles on device)
+ *   spl_deal           engine/rules.py:33-34 initial_state(num_players, seed) with the engine seed
+ *                      given directly (the functional engine API)
  *   spl_step           envs/splendor_env.py:51-90 SplendorEnv.step = rules.py:40-93 legal_moves,
  *                      :196-287 apply_action, encode.py:124-187 encode_observation, reward /
  *                      termination, plus gymnasium-0.29 SyncVectorEnv same-step autoreset
@@ -136,6 +138,14 @@ int spl_arena_init(spl_ctx_t *ctx, spl_arena_t *arena, void *stream);
  * observation / action mask after the reset. */
 int spl_reset(spl_ctx_t *ctx, spl_arena_t *arena, const uint64_t *pcg, const uint8_t *reset_mask,
               int32_t *obs, int8_t *mask, void *stream);
+
+/* engine/state.py:181-211 initial_state(players, seed) (engine/rules.py:33-34) from an explicit engine
+ * seed per table (device [n] uint32; CPython seeds abs(seed) < 2^32), for tables with a non-zero
+ * deal_mask byte (NULL = all).  Unlike spl_reset it does not touch the table's engine-seed stream and
+ * deals no pool records.  obs/mask (nullable) as in spl_reset.  The functional engine API
+ * (splendor_gym.engine.initial_state) runs on this. */
+int spl_deal(spl_ctx_t *ctx, spl_arena_t *arena, const uint32_t *engine_seeds, const uint8_t *deal_mask,
+             int32_t *obs, int8_t *mask, void *stream);
 
 int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *args, void *stream);
 

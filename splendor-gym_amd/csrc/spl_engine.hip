@@ -1901,7 +1901,7 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
 // Explicit reset (SplendorEnv.reset / VectorEnv.reset), then observation + mask of all tables.
 template <int P>
 __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64_t *pcg_in, const uint8_t *mask_in,
-                                              int32_t *obs, int8_t *mask_out) {
+                                              int32_t *obs, int8_t *mask_out, const uint32_t *eseed_in) {
     __shared__ BlockLDS L;
     const int lane = lane_id();
     const int t0 = blockIdx.x * 64;
@@ -1916,7 +1916,11 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
     const bool doit = valid && (mask_in == nullptr || mask_in[t] != 0);
     uint8_t *scr = &L.rows[lane * kScratchStride];
     if (doit) {
-        if (pcg_in) {  // reset(seed=...): restart this table's np_random stream, deal every record
+        if (eseed_in) {  // engine/state.py:181-211 initial_state(P, seed) from an explicit engine seed
+            Deal d0;     // no pool: a later reset() without a seed deals inline
+            deal_into(eseed_in[t], P, slot_rec(A, t, 0), scr, d0);
+            fresh_state(T, ring_bits(0, kSlotRecords - 1), d0);
+        } else if (pcg_in) {  // reset(seed=...): restart this table's np_random stream, deal every record
             Pcg64 g;
             g.s_hi = pcg_in[4 * (size_t)t];
             g.s_lo = pcg_in[4 * (size_t)t + 1];
@@ -2352,10 +2356,24 @@ int spl_reset(spl_ctx_t *ctx, spl_arena_t *arena, const uint64_t *pcg, const uin
     const KArena A = karena(arena);
     hipStream_t s = static_cast<hipStream_t>(stream);
     DISPATCH_P(arena->players, hipLaunchKernelGGL(k_reset<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
-                                                  ktables(ctx), pcg, reset_mask, obs, mask));
+                                                  ktables(ctx), pcg, reset_mask, obs, mask, (const uint32_t *)nullptr));
     if (int r = launch_check()) return r;
     arena->steps = 0;
     return SPL_OK;
+}
+
+int spl_deal(spl_ctx_t *ctx, spl_arena_t *arena, const uint32_t *engine_seeds, const uint8_t *deal_mask,
+             int32_t *obs, int8_t *mask, void *stream) {
+    if (int r = check_arena(ctx, arena)) return r;
+    if (!engine_seeds) return fail(SPL_E_ARG, "engine_seeds is required");
+    if (obs && ((uintptr_t)obs & 15u)) return fail(SPL_E_ARG, "obs must be 16-byte aligned");
+    if (mask && ((uintptr_t)mask & 3u)) return fail(SPL_E_ARG, "mask must be 4-byte aligned");
+    const KArena A = karena(arena);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    DISPATCH_P(arena->players, hipLaunchKernelGGL(k_reset<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
+                                                  ktables(ctx), (const uint64_t *)nullptr, deal_mask, obs, mask,
+                                                  engine_seeds));
+    return launch_check();
 }
 
 int spl_arena_init(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {

@@ -121,6 +121,26 @@ class Engine:
         self._keep = (pcg, m)  # alive until the async reset has consumed them
         return self.obs, self.mask
 
+    def deal(self, engine_seeds, mask=None, obs=True):
+        """initial_state(P, seed) for every table (or where `mask` is true) from explicit engine
+        seeds (engine/state.py:181-211; CPython seeds are taken by absolute value, < 2**32)."""
+        torch = self.torch
+        seeds = np.asarray([abs(int(x)) for x in engine_seeds], dtype=np.uint64)
+        if len(seeds) != self.n:
+            raise ValueError(f"expected {self.n} engine seeds")
+        if (seeds >= 2**32).any():
+            raise ValueError("engine seeds must satisfy abs(seed) < 2**32 on the device")
+        es = torch.from_numpy(seeds.astype(np.uint32)).to(self.device)
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_deal(self.ctx, ctypes.byref(self.desc), ptr(es), ptr(m),
+                                              ptr(self.obs) if obs else None, ptr(self.mask) if obs else None,
+                                              self.stream()))
+        self._keep = (es, m)
+        return self.obs, self.mask
+
     def step(self, actions=None, autoreset=True, final_obs=True, next_actions=None, policy_seed=0, ply=0,
              ep_return=None, ep_count=None, ply_base=None, policy=0, small=None):
         """One env step on every table (SplendorEnv.step semantics per table).  autoreset: False,

@@ -66,3 +66,9 @@ def encode_reserve_blind_index(tier):
 
 def encode_buy_reserved_index(slot):
     return BUY_RESERVED_OFFSET + slot
+
+
+def encode_observation(state):
+    """encode.py:124-187 for a host view, evaluated on the GPU (engine.rules.encode_observation)."""
+    from .rules import encode_observation as _enc
+    return _enc(state)

@@ -10,6 +10,7 @@ Noble, PlayerState, SplendorState field names) so code that reads ``env.state`` 
 import json
 import os
 from dataclasses import dataclass, field
+from types import MappingProxyType
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -59,10 +60,13 @@ def cards_by_id():
     global _CARDS, _NOBLES
     if _CARDS is None:
         c, n = load_tables()
+        # read-only costs: the device holds one constant card table, so an edited cost could not
+        # reach it (the reference tests edit card.cost in place; here that raises)
         _CARDS = [Card(i, int(r[0]), STANDARD_COLORS[int(r[1])], int(r[2]),
-                       {STANDARD_COLORS[k]: int(r[3 + k]) for k in range(5) if r[3 + k]}) for i, r in enumerate(c)]
-        _NOBLES = [Noble(1000 + i, {STANDARD_COLORS[k]: int(r[k]) for k in range(5) if r[k]}, int(r[5]))
-                   for i, r in enumerate(n)]
+                       MappingProxyType({STANDARD_COLORS[k]: int(r[3 + k]) for k in range(5) if r[3 + k]}))
+                  for i, r in enumerate(c)]
+        _NOBLES = [Noble(1000 + i, MappingProxyType({STANDARD_COLORS[k]: int(r[k]) for k in range(5) if r[k]}),
+                         int(r[5])) for i, r in enumerate(n)]
     return _CARDS
 
 
@@ -80,6 +84,16 @@ class PlayerState:
     revealed_reserved: List[bool] = field(default_factory=list)
     nobles: List[Noble] = field(default_factory=list)
 
+    def can_afford(self, card):
+        """(affordable, discounted cost per colour) — state.py:61-71: colour tokens pay what the
+        bonuses leave, gold covers the rest."""
+        need, gold = [], 0
+        for i, c in enumerate(STANDARD_COLORS):
+            d = max(0, card.cost.get(c, 0) - self.bonuses[i])
+            need.append(d)
+            gold += d - min(self.tokens[i], d)
+        return self.tokens[5] >= gold, need
+
 
 @dataclass
 class SplendorState:
@@ -96,6 +110,17 @@ class SplendorState:
     game_over: bool = False
     winner_index: Optional[int] = None
     turn_limit_reached: bool = False
+
+    def copy(self) -> "SplendorState":
+        """Independent lists, shared (immutable) cards and nobles (state.py:89-104)."""
+        return SplendorState(
+            num_players=self.num_players, bank=list(self.bank),
+            players=[PlayerState(tokens=list(p.tokens), bonuses=list(p.bonuses), prestige=p.prestige,
+                                 reserved=list(p.reserved), revealed_reserved=list(p.revealed_reserved),
+                                 nobles=list(p.nobles)) for p in self.players],
+            board={t: list(v) for t, v in self.board.items()}, decks={t: list(v) for t, v in self.decks.items()},
+            nobles=list(self.nobles), to_play=self.to_play, turn_count=self.turn_count, move_count=self.move_count,
+            game_over=self.game_over, winner_index=self.winner_index, turn_limit_reached=self.turn_limit_reached)
 
     @classmethod
     def from_record(cls, r):

@@ -30,6 +30,8 @@ class SplendorEnv(Env):
         self.current_player = 0
         self._device = device
         self._eng = None
+        self._view = None        # host view handed out by .state (write-through, see `state`)
+        self._view_rec = None    # its record bytes when handed out
         self._seeded = False
         self._terminal = False
         _native.load_library()  # fail loudly at construction if the HIP engine is missing
@@ -67,6 +69,7 @@ class SplendorEnv(Env):
             self._seeded = True
         else:                                     # continue this env's np_random stream
             eng.reset(seeds=None)
+        self._view = None
         obs, mask = self._fetch()
         self._terminal = False
         self.current_player = int(obs[294])
@@ -81,8 +84,10 @@ class SplendorEnv(Env):
         except (TypeError, ValueError):
             raise ValueError("Action out of bounds for action_space")
         a = max(min(a, 2**31 - 1), -(2**31))
+        self._flush_view()
         e.actions.fill_(a)
         e.step(e.actions, autoreset=False)
+        self._view = None
         obs, mask = self._fetch()
         o = self._out
         flags = o["flags"]
@@ -123,25 +128,46 @@ class SplendorEnv(Env):
     # ---- host view of the device table ---------------------------------------------------
     @property
     def state(self) -> Optional[SplendorState]:
-        """A host SNAPSHOT of the device table (mutations do not write back: use set_state)."""
+        """The table as a reference-shaped SplendorState, WRITE-THROUGH: the same object is returned
+        until the next step/reset, and in-place edits of it (bank, players, board, decks, nobles,
+        counters — tests/utils.py:25-53 style) are uploaded to the device before the next step,
+        legal_mask() or render().  Card/noble data itself is the constant device table."""
         if self._eng is None:
             return None
-        return SplendorState.from_record(self._eng.download(0, 1)[0])
+        if self._view is None:
+            self._view = SplendorState.from_record(self._eng.download(0, 1)[0])
+            self._view_rec = self._view.to_record().tobytes()
+        return self._view
+
+    def _flush_view(self):
+        """Upload host edits of the view handed out by `state` (no-op when unchanged)."""
+        if self._view is None:
+            return
+        rec = self._view.to_record()
+        if rec.tobytes() != self._view_rec:
+            self._eng.upload(rec)
+            self._view_rec = rec.tobytes()
 
     def set_state(self, state: SplendorState) -> None:
+        """Replace the device table by `state` (also what in-place edits of .state do implicitly)."""
         self._engine().upload(state.to_record())
+        self._view = None
 
     def legal_mask(self) -> np.ndarray:
         """engine legal_moves(self.state) as int8[45], computed on the device (rules.py:40-93)."""
         e = self._engine()
+        self._flush_view()
         e.legal()
         return e.mask[0].cpu().numpy()
 
     def render(self):
+        """Print the reference logger's compact text of the table (envs/splendor_env.py:119-126)."""
         if self.render_mode not in ("human", None):
             return
-        from ..render import format_game_state
-        print(format_game_state(self.state))
+        assert self.state is not None
+        self._flush_view()
+        from ..scripts.game_logger import SplendorGameLogger
+        print(SplendorGameLogger().format_game_state(self.state))
 
 
 def make(num_players: int = 2, render_mode: Optional[str] = None, seed: Optional[int] = None) -> SplendorEnv:

@@ -3,14 +3,11 @@ envs/splendor_env.py:41-115) computed by the CPU oracle, so host-side wrappers c
 against the reference's fixtures without a GPU.  Test infrastructure only."""
 import numpy as np
 
-from oracle.oracle import PCG, Oracle, mask_bits_to_int8, pcg_state_of
+from oracle.oracle import PCG, Oracle, mask_bits_to_int8, pcg_state_of, view_to_table
 
 F_ILLEGAL, F_DRAW, F_TURN_LIMIT, F_AFTER_TERMINAL, F_OOB = 0x01, 0x02, 0x04, 0x08, 0x10
 
 
-class _State:
-    def __init__(self, view):
-        self.to_play = view["to_play"]
 
 
 class OracleSplendorEnv:
@@ -24,7 +21,12 @@ class OracleSplendorEnv:
 
     @property
     def state(self):
-        return None if self.view is None else _State(self.view)
+        """Reference-shaped snapshot (this package's host view type) of the oracle table."""
+        from splendor_gym.engine.state import SplendorState
+        return None if self.view is None else SplendorState.from_record(view_to_table(self.view))
+
+    def close(self):
+        pass
 
     def reset(self, *, seed=None, options=None):
         import ctypes

@@ -93,37 +93,151 @@ def test_render_no_crash(capsys):  # test_gym_compat.py:127-132
     assert "Bank" in capsys.readouterr().out
 
 
-def test_no_legal_move_draw():  # test_draw_rule.py:7-24
-    env = make_env()
-    env.reset(seed=0)
-    s = env.state
-    s.bank[:] = [0, 0, 0, 0, 0, 0]
-    p = s.players[s.to_play]
+def mask_from_state(env):  # reference tests/utils.py:15-16
+    from splendor_gym.engine import legal_moves
+    return np.array(legal_moves(env.state), dtype=np.int8)
+
+
+def test_no_legal_move_draw():  # test_draw_rule.py:7-24, in-place edits of env.state (no set_state)
+    from splendor_gym.envs import SplendorEnv
+    env = SplendorEnv(seed=0)
+    obs, info = env.reset()
+    env.state.bank[:] = [0, 0, 0, 0, 0, 0]
+    p = env.state.players[env.state.to_play]
     p.tokens[:] = [10, 0, 0, 0, 0, 0]
-    p.reserved = s.decks[1][:3]
-    p.revealed_reserved = [False] * 3
+    p.reserved = env.state.decks[1][:3]
     for t in (1, 2, 3):
-        s.board[t] = [None] * 4
-    env.set_state(s)
+        env.state.board[t] = [None, None, None, None]
+    assert not np.any(mask_from_state(env))
     assert not env.legal_mask().any()
-    obs, r, term, trunc, info = env.step(0)
-    assert term and r == 0 and info.get("draw") and env.state.winner_index is None
+    obs, reward, terminated, truncated, info = env.step(0)
+    assert terminated and reward == 0 and info.get("draw") and env.state.winner_index is None
 
 
-@pytest.mark.parametrize("bank,n_legal,taken", [([1, 0, 2, 0, 0, 0], 3, 2), ([0, 0, 0, 0, 3, 0], 6, 1)])
-def test_take_reduced_colours(bank, n_legal, taken):  # test_take_reduced_colors.py:7-36
+def test_take_two_when_only_two_colors():  # test_take_reduced_colors.py:7-21
+    from splendor_gym.engine.state import COLOR_INDEX
     env = make_env()
     env.reset(seed=123)
-    s = env.state
-    s.bank[:] = bank
-    env.set_state(s)
-    m = env.legal_mask()
-    legal = [i for i in range(10) if m[i]]
-    assert len(legal) == n_legal
+    env.state.bank[:] = [0, 0, 0, 0, 0, 0]
+    env.state.bank[COLOR_INDEX["white"]] = 1
+    env.state.bank[COLOR_INDEX["green"]] = 2
+    m = mask_from_state(env)
+    legal = [i for i in range(0, 10) if m[i] == 1]
+    assert legal == [0, 3, 4]
     env.step(legal[0])
+    last = env.state.players[(env.state.to_play - 1) % env.state.num_players]
+    assert last.tokens[COLOR_INDEX["white"]] + last.tokens[COLOR_INDEX["green"]] == 2
+
+
+def test_take_one_when_only_one_color():  # test_take_reduced_colors.py:24-36
+    from splendor_gym.engine.state import COLOR_INDEX
+    env = make_env()
+    env.reset(seed=123)
+    env.state.bank[:] = [0, 0, 0, 0, 0, 0]
+    env.state.bank[COLOR_INDEX["black"]] = 3
+    m = mask_from_state(env)
+    legal = [i for i in range(0, 10) if m[i] == 1]
+    assert legal == [2, 4, 5, 7, 8, 9]
+    env.step(legal[0])
+    last = env.state.players[(env.state.to_play - 1) % env.state.num_players]
+    assert last.tokens[COLOR_INDEX["black"]] == 1
+
+
+def test_token_return_behavior_random_non_gold():  # test_afford_nobles_obs.py:58-71
+    env = make_env()
+    obs, info = env.reset(seed=7)
+    state = env.state
+    p = state.players[state.to_play]
+    p.tokens = [3, 3, 3, 3, 3, 0]
+    prev_bank = list(state.bank)
+    env.step(int(np.flatnonzero(info["action_mask"])[0]))
+    prev = env.state.players[(env.state.to_play - 1) % env.state.num_players]
+    assert sum(prev.tokens) == 10 and sum(env.state.bank) >= sum(prev_bank)
+
+
+def test_state_view_edits_match_the_oracle():
+    """An edited env.state steps exactly like the same state in the CPU oracle."""
+    from oracle.oracle import Oracle, table_to_view
+    o = Oracle()
+    env = make_env()
+    env.reset(seed=11)
     s = env.state
-    last = s.players[(s.to_play - 1) % s.num_players]
-    assert sum(last.tokens) == taken
+    s.players[0].tokens[:] = [2, 2, 2, 2, 1, 1]
+    s.bank[:] = [2, 2, 2, 2, 3, 4]
+    s.players[0].bonuses[:] = [1, 0, 2, 0, 1]
+    view = table_to_view(s.to_record())
+    for a in range(45):
+        if mask_from_state(env)[a]:
+            break
+    obs, r, term, trunc, info = env.step(a)
+    ref = o.env_step(view, a)
+    np.testing.assert_array_equal(obs, ref["obs"])
+    from schema import canon
+    assert canon(table_to_view(env.state.to_record())) == canon(ref["after"])
+
+
+def test_render_text_matches_reference(capsys):  # envs/splendor_env.py:119-126 -> game_logger.py:159-220
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "render.json")) as f:
+        cases = json.load(f)["env"]
+    for c in cases:
+        env = make_env()
+        env.reset(seed=c["seed"])
+        for a in c["actions"]:
+            env.step(a)
+        capsys.readouterr()
+        env.render()
+        assert capsys.readouterr().out == c["text"], c["seed"]
+
+
+def test_functional_engine_api_matches_reference():
+    """engine.initial_state / legal_moves / apply_action / encode_observation on host views
+    (evaluated on the GPU) against the reference's deals (deals.npz), legal masks of 148 logged
+    states (render.json) and crafted/fuzzed steps (edge_cases.json)."""
+    import json
+    import os
+    from oracle.oracle import table_to_view, view_to_table
+    from splendor_gym.engine import apply_action, initial_state, legal_moves
+    from splendor_gym.engine.encode import encode_observation
+    from splendor_gym.engine.state import SplendorState
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    d = np.load(os.path.join(gold, "deals.npz"))
+    for P in (2, 3, 4):
+        for i in range(0, 512, 37):
+            v = table_to_view(initial_state(P, int(d["seeds"][i])).to_record())
+            assert v["board"] == [int(x) for x in d[f"board_p{P}"][i]]
+            for t in range(3):
+                dk = [int(x) for x in d[f"decks_p{P}"][i, t] if x >= 0]
+                assert v["decks"][t] == dk
+            assert v["nobles"] == [int(x) for x in d[f"nobles_p{P}"][i] if x >= 0]
+    with open(os.path.join(gold, "render.json")) as f:
+        states = json.load(f)["states"]
+    for c in states:
+        s = SplendorState.from_record(view_to_table(c["view"]))
+        assert legal_moves(s) == c["mask"], c["name"]
+    with open(os.path.join(gold, "edge_cases.json")) as f:
+        cases = json.load(f)
+    done = 0
+    for c in cases:
+        if c["exception"] is not None or c["flags"] != 0 or not (c["legal"] >> c["action"]) & 1:
+            continue
+        s = SplendorState.from_record(view_to_table(c["before"]))
+        nxt = apply_action(s, c["action"])
+        got = table_to_view(nxt.to_record())
+        want = table_to_view(view_to_table(c["after"]))
+        for p in got["players"] + want["players"]:
+            p["nobles"] = sorted(p["nobles"])
+        assert got == want, c["name"]
+        np.testing.assert_array_equal(encode_observation(nxt), np.array(c["obs"], np.int32), err_msg=c["name"])
+        assert s.to_record().tobytes() == view_to_table(c["before"]).tobytes()  # input not modified
+        done += 1
+    assert done > 300
+    s = initial_state(2, 0)
+    with pytest.raises(ValueError):
+        apply_action(s, 45)
+    with pytest.raises(ValueError):
+        apply_action(s, 15)  # buying a card with no tokens: illegal
 
 
 def test_reserved_card_visibility():  # test_reserved_card_observation.py:85-371
@@ -242,3 +356,28 @@ def test_rollout_perf_smoke():  # test_gym_compat.py:135-157 (threshold 6000 SPS
     sps = steps / (time.time() - t0)
     print(f"SPS={sps:.0f}")
     assert sps > 6000
+
+
+def test_engine_rules_reference_cases():  # test_rules.py:8-43, test_afford_nobles_obs.py:31-55
+    from splendor_gym.engine import apply_action, initial_state, legal_moves
+    from splendor_gym.engine.encode import OBSERVATION_DIM, TOTAL_ACTIONS, encode_observation
+    s = initial_state(seed=42)
+    m = legal_moves(s)
+    assert len(m) == TOTAL_ACTIONS and any(m)
+    s = initial_state(seed=1)
+    a = next(i for i, v in enumerate(legal_moves(s)) if v == 1)
+    nxt = apply_action(s, a)
+    assert sum(nxt.bank) == sum(s.bank) - (3 if a < 10 else 2 if a < 15 else 0)
+    assert nxt.turn_count == s.turn_count
+    s = initial_state(seed=0)
+    m = legal_moves(s)
+    assert all(m[10 + c] == 0 for c in range(5) if s.bank[c] < 4)
+    s.players[s.to_play].tokens = [5, 5, 5, 5, 5, 0]  # token return seeded outside the table's domain
+    nxt = apply_action(s, 0)
+    assert sum(nxt.players[s.to_play - 1].tokens) <= 10
+    s = initial_state(seed=999)
+    s.players[s.to_play].bonuses = [4, 4, 4, 4, 4]
+    nxt = apply_action(s, int(np.flatnonzero(legal_moves(s))[0]))
+    assert sum(1 for n in nxt.nobles if n is None) == 1  # exactly one noble per turn
+    obs = encode_observation(initial_state(seed=0))
+    assert obs.shape == (OBSERVATION_DIM,) and obs.dtype == np.int32

@@ -117,7 +117,7 @@ def test_constants_match_reference_layout():
 def test_host_state_record_roundtrip():
     from oracle.oracle import Oracle, view_to_table
     from splendor_gym.engine.state import SplendorState
-    from splendor_gym.render import format_game_state
+    from splendor_gym.scripts.game_logger import format_game_state
     o = Oracle()
     v = o.initial_state(2, 42)
     rec = view_to_table(v)
