@@ -7,11 +7,14 @@
  * masked_categorical (ppo_splendor.py:27-37) for sampling and the greedy masked argmax of
  * training_utils.py:263-276 frozen_policy_from / scripts/eval_suite.py model_greedy_policy_from
  * for opponents.  These entry points evaluate that network for a whole batch of tables in one
- * launch: observations (int32 [n][297]) and masks (int8 [n][45]) straight from the engine, bf16
- * MFMA (v_mfma_f32_32x32x16_bf16) with fp32 accumulation, tanh / softmax / sampling fused.
+ * launch: observations (int32 [n][297]) and masks (int8 [n][45]) straight from the engine, tanh /
+ * softmax / sampling fused.  Two precisions:
+ *   SPL_PREC_FP32 (default)  the reference's fp32: exact fp32 products and accumulation on
+ *                            v_mfma_f32_16x16x4_f32 (spl_policy32.hip), tanhf
+ *   SPL_PREC_BF16 (opt-in)   bf16 MFMA (v_mfma_f32_32x32x16_bf16) with fp32 accumulation (spl_policy.hip)
  *
- *   spl_policy_bytes   size of a packed weight image (actor only, or actor + critic)
- *   spl_policy_pack    nn.Linear fp32 weights [out][in] + biases -> packed bf16 image (device)
+ *   spl_policy_bytes   size of a packed weight image (actor only, or actor + critic; per precision)
+ *   spl_policy_pack    nn.Linear fp32 weights [out][in] + biases -> packed image (device)
  *   spl_policy_act     ActorCritic.get_action_and_value (SAMPLE) or the greedy masked argmax
  *                      (GREEDY) for n tables
  *
@@ -27,7 +30,11 @@
 extern "C" {
 #endif
 
-#define SPL_POLICY_ABI 1
+#define SPL_POLICY_ABI 2  /* 2: precision argument, args->image describes the image */
+
+#define SPL_PREC_FP32 0
+#define SPL_PREC_BF16 1
+#define SPL_IMG_CRITIC 1 /* spl_act_args_t.image bit 0: the image holds the critic; bits 1-2: SPL_PREC_* */
 
 /* one nn.Sequential(Linear(297,256), Tanh, Linear(256,256), Tanh, Linear(256,out)):
  * weights row-major [out][in] (torch's nn.Linear.weight), biases [out], fp32, device memory */
@@ -53,14 +60,16 @@ typedef struct {
     const uint64_t *ply_base; /* device, nullable: added to `ply` (lets a captured graph replay)  */
     int64_t table0;
     int32_t mode;        /* SPL_ACT_*                                                            */
-    int32_t reserved;
+    int32_t image;       /* how the image was packed: SPL_IMG_CRITIC if with a critic | precision << 1;
+                            packed_bytes must equal spl_policy_bytes(critic, precision)              */
 } spl_act_args_t;
 
-/* bytes of a packed image: with_critic 0 = actor only (greedy opponents), 1 = actor + critic */
-int64_t spl_policy_bytes(int32_t with_critic);
-/* pack `actor` (and `critic` unless NULL) into `packed` (spl_policy_bytes(critic != NULL) bytes,
- * 256-byte aligned device memory); asynchronous on `stream` */
-int spl_policy_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream);
+/* bytes of a packed image: with_critic 0 = actor only (greedy opponents), 1 = actor + critic;
+ * SPL_E_ARG for an unknown precision */
+int64_t spl_policy_bytes(int32_t with_critic, int32_t precision);
+/* pack `actor` (and `critic` unless NULL) into `packed` (spl_policy_bytes(critic != NULL, precision)
+ * bytes, 256-byte aligned device memory); asynchronous on `stream` */
+int spl_policy_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, int32_t precision, void *packed, void *stream);
 /* evaluate the packed network on n tables; SAMPLE with args->value != NULL needs a packed image
  * that holds the critic */
 int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const spl_act_args_t *args,

@@ -472,18 +472,27 @@ __global__ __launch_bounds__(512) void k_act(const uint8_t *__restrict__ W, ActA
 
 using namespace splp;
 
+int64_t splp32_bytes(int with_critic);  // spl_policy32.hip: the fp32 image
+int splp32_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream);
+int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, int32_t n, const spl_act_args_t *args,
+               void *stream);
+
 extern "C" {
 
-int64_t spl_policy_bytes(int32_t with_critic) {
+int64_t spl_policy_bytes(int32_t with_critic, int32_t precision) {
+    if (precision == SPL_PREC_FP32) return splp32_bytes(with_critic ? 1 : 0);
+    if (precision != SPL_PREC_BF16) return SPL_E_ARG;
     return with_critic ? (int64_t)kAllChunks * kChunk + kCriticTail : (int64_t)kActorChunks * kChunk;
 }
 
-int spl_policy_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream) {
+int spl_policy_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, int32_t precision, void *packed, void *stream) {
     if (!actor || !actor->w1 || !actor->b1 || !actor->w2 || !actor->b2 || !actor->w3 || !actor->b3)
         return spl_fail(SPL_E_ARG, "actor weights missing");
     if (critic && (!critic->w1 || !critic->b1 || !critic->w2 || !critic->b2 || !critic->w3 || !critic->b3))
         return spl_fail(SPL_E_ARG, "critic weights incomplete");
     if (!packed || ((uintptr_t)packed & 255u)) return spl_fail(SPL_E_ARG, "packed image must be 256-byte aligned");
+    if (precision == SPL_PREC_FP32) return splp32_pack(actor, critic, packed, stream);
+    if (precision != SPL_PREC_BF16) return spl_fail(SPL_E_ARG, "unknown precision");
     const PackNet A{actor->w1, actor->b1, actor->w2, actor->b2, actor->w3, actor->b3, kAct};
     const PackNet C = critic ? PackNet{critic->w1, critic->b1, critic->w2, critic->b2, critic->w3, critic->b3, 1} : A;
     const int chunks = critic ? kAllChunks : kActorChunks;
@@ -497,24 +506,30 @@ int spl_policy_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packe
 int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const spl_act_args_t *args, void *stream) {
     if (!args) return spl_fail(SPL_E_ARG, "null args");
     if (!packed || ((uintptr_t)packed & 255u)) return spl_fail(SPL_E_ARG, "packed image must be 256-byte aligned");
-    if (packed_bytes < spl_policy_bytes(0)) return spl_fail(SPL_E_ARG, "packed image too small");
+    const int precision = (args->image >> 1) & 3;
+    const bool has_critic = (args->image & SPL_IMG_CRITIC) != 0;
+    if (precision != SPL_PREC_FP32 && precision != SPL_PREC_BF16) return spl_fail(SPL_E_ARG, "unknown precision");
+    // the image is described by args->image, and its size must be exactly that image's: a full image
+    // passed as actor-only (or the reverse) would evaluate the wrong chunks
+    if (packed_bytes != spl_policy_bytes(has_critic ? 1 : 0, precision))
+        return spl_fail(SPL_E_ARG, "packed_bytes does not match the image described by args->image");
     if (n <= 0) return spl_fail(SPL_E_ARG, "n must be positive");
     if (!args->obs || ((uintptr_t)args->obs & 15u)) return spl_fail(SPL_E_ARG, "obs must be 16-byte aligned");
     if (!args->mask || ((uintptr_t)args->mask & 3u)) return spl_fail(SPL_E_ARG, "mask must be 4-byte aligned");
     if (!args->action) return spl_fail(SPL_E_ARG, "action output missing");
     if (args->mode != SPL_ACT_SAMPLE && args->mode != SPL_ACT_GREEDY) return spl_fail(SPL_E_ARG, "unknown mode");
-    const bool has_critic = packed_bytes >= spl_policy_bytes(1);  // critic chunks follow the actor's
     const bool sample = args->mode == SPL_ACT_SAMPLE;
     const bool critic = sample && args->value;
     if (critic && !has_critic) return spl_fail(SPL_E_ARG, "value requested from an actor-only image");
     const uint8_t *img = static_cast<const uint8_t *>(packed);
+    if (precision == SPL_PREC_FP32) return splp32_act(img, has_critic, critic, sample, n, args, stream);
     const float *critic_out = has_critic ? reinterpret_cast<const float *>(img + (size_t)kAllChunks * kChunk) : nullptr;
     const ActArgs a{args->obs,   args->mask,       args->action,   args->logprob, args->entropy,
                     args->value, args->logits,     critic_out,     args->seed,    args->ply,
                     args->ply_base, args->table0, n};
     const dim3 grid((unsigned)((n + kRowsPerBlock - 1) / kRowsPerBlock)), block(kWaves * 64);
     const hipStream_t s = (hipStream_t)stream;
-    const uint8_t *W = static_cast<const uint8_t *>(packed);
+    const uint8_t *W = img;
     if (has_critic && !critic) W += (size_t)kCriticChunks * kChunk;  // the actor part of a full image
     if (critic)
         hipLaunchKernelGGL((k_act<true, true>), grid, block, 0, s, W, a);

@@ -1,0 +1,352 @@
+// spl_policy32.hip — the fused ActorCritic forward at fp32 (the reference's precision) on MI355X.
+//
+// Same network and epilogue as spl_policy.hip's bf16 kernel (ppo_splendor.py:27-59: actor and
+// critic Linear(297,256)-Tanh-Linear(256,256)-Tanh-Linear(256,{45|1}); masked_categorical sample,
+// log_prob, entropy, critic value; or the greedy masked argmax of training_utils.py:263-276), but
+// every product is an exact fp32 FMA: v_mfma_f32_16x16x4_f32 (fp32 in, fp32 accumulate — the chip's
+// fp32 matrix peak, bitwise an fmaf chain), tanh as the correctly rounded-to-2-ulp tanhf.  Logits and
+// values therefore agree with torch's fp32 nn.Linear stack to summation-order rounding.
+//
+//   * a wave = 16 tables = the 16 columns of every 16x16x4 tile; a workgroup = 8 waves = 128 tables
+//     (two waves per SIMD).  Activations are TRANSPOSED (hidden unit on the accumulator row, table
+//     on the lane): accumulator register i of lane group g holds unit 16t + 4g + i of tile t, which
+//     is exactly lane group g's B operand of k-step 4t + i of the next layer — no LDS round trip
+//     between layers (the packed weights carry the matching input-unit order).
+//   * the observation (int32 -> fp32, exact) loads into registers as the 76 layer-1 B fragments
+//     and stays there through both networks' layer 1; hidden layers hold 64 fp32 per lane.
+//   * weights stream once per workgroup through the same 6-slot LDS ring as the bf16 kernel
+//     (20-KB chunks = one 16-row output tile of one layer, [k-step/4][lane][4 fp32] + bias,
+//     global_load_lds, 5 chunks in flight), shared by the 8 waves.
+//   * the critic's one-unit output layer is a per-lane fp32 FMA chain over its layer-2 tiles.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/splendor_amd.h"
+#include "../../include/splendor_policy.h"
+#include "spl_rng.h"
+
+int spl_fail(int code, const std::string &msg);  // spl_engine.hip: sets spl_last_error()
+
+namespace splp32 {
+
+using spl::philox4x32;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kObs = 297, kAct = 45, kHid = 256;
+constexpr int kKs1 = 76;  // layer-1 k-steps of 4: 297 inputs padded to 304
+constexpr int kKs2 = 64;  // layers 2 and 3: 256 inputs
+constexpr int kChunk = 20480;
+constexpr int kBiasOff = kKs1 * 256;  // 19 456: after the largest weight block
+constexpr int kTiles = kHid / 16;     // 16 output tiles of 16 rows per hidden layer
+constexpr int kActTiles = 3;          // 48 rows >= 45 logits
+constexpr int kActorChunks = 2 * kTiles + kActTiles, kCriticChunks = 2 * kTiles;  // 35, 32
+constexpr int kAllChunks = kActorChunks + kCriticChunks;                          // 67
+constexpr int kCriticTail = 272 * 4;  // fp32 critic output layer: w3 [256], b3, padding
+
+constexpr int kWaves = 8, kRowsPerWave = 16, kRowsPerBlock = kWaves * kRowsPerWave;  // 128 tables
+constexpr int kSlots = 6;
+constexpr int kMaskWave = kRowsPerWave * kAct;  // 720 B
+constexpr int kLogitRow = 49;                   // floats per staged logit row (odd: conflict-free)
+constexpr int kLdsMask = kSlots * kChunk;
+constexpr int kLds = kLdsMask + kWaves * kMaskWave;  // 128 640 B
+static_assert(kWaves * kRowsPerWave * kLogitRow * 4 <= kLdsMask, "logits reuse the weight ring");
+static_assert(kLds <= 160 * 1024, "LDS");
+static_assert(kKs1 % 4 == 0 && kKs2 % 4 == 0, "k-steps in groups of four");
+
+// chunk order of an image (the order a forward pass consumes them): with a critic
+// [critic L1 x16][critic L2 x16], then [actor L1 x16][actor L2 x16][actor L3 x3]; the actor part of
+// a full image (its last 35 chunks) is laid out exactly as an actor-only image.
+
+struct PackNet {
+    const float *w1, *b1, *w2, *b2, *w3, *b3;
+    int out;
+};
+
+// input unit fed by lane group g at k-step s: natural order in layer 1 (the observation), the
+// accumulator order of the previous layer's tiles in layers 2-3 (k-step 4t + i <- tile t, reg i)
+__device__ __forceinline__ int unit_of(int layer, int s, int g) {
+    return layer == 1 ? 4 * s + g : 16 * (s >> 2) + 4 * g + (s & 3);
+}
+
+// one block per physical chunk
+__global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, int with_critic, uint8_t *dst) {
+    const int ch = blockIdx.x;
+    const int net = with_critic && ch < kCriticChunks ? 1 : 0;  // 0 actor, 1 critic
+    const int local = ch - (with_critic && !net ? kCriticChunks : 0);
+    const int layer = local < kTiles ? 1 : local < 2 * kTiles ? 2 : 3;
+    const int tile = local - (layer - 1) * kTiles;
+    const PackNet &P = net ? critic : actor;
+    const float *W = layer == 1 ? P.w1 : layer == 2 ? P.w2 : P.w3;
+    const float *B = layer == 1 ? P.b1 : layer == 2 ? P.b2 : P.b3;
+    const int in = layer == 1 ? kObs : kHid, rows = layer == 3 ? P.out : kHid;
+    const int ks = layer == 1 ? kKs1 : kKs2;
+    float *out = reinterpret_cast<float *>(dst + (size_t)ch * kChunk);
+    // [k-step group q][lane][4]: lane l = (g = l >> 4, r = l & 15) holds W[row 16*tile + r][unit(4q + j, g)]
+    for (int v = threadIdx.x; v < (ks / 4) * 64 * 4; v += blockDim.x) {
+        const int j = v & 3, lane = (v >> 2) & 63, q = v >> 8;
+        const int r = lane & 15, g = lane >> 4, row = 16 * tile + r, k = unit_of(layer, 4 * q + j, g);
+        out[v] = (row < rows && k < in) ? W[(size_t)row * in + k] : 0.f;
+    }
+    for (int v = (ks / 4) * 256 + threadIdx.x; v < kBiasOff / 4; v += blockDim.x) out[v] = 0.f;
+    if (threadIdx.x < 16) {  // bias in row order
+        const int row = 16 * tile + threadIdx.x;
+        out[kBiasOff / 4 + threadIdx.x] = row < rows ? B[row] : 0.f;
+    }
+    if (net == 1 && layer == 2 && tile == 0) {  // the critic's output layer as fp32 (evaluated on VALU)
+        float *tail = reinterpret_cast<float *>(dst + (size_t)kAllChunks * kChunk);
+        for (int k = threadIdx.x; k < 272; k += blockDim.x) tail[k] = k < kHid ? P.w3[k] : k == kHid ? P.b3[0] : 0.f;
+    }
+}
+
+struct ActArgs {
+    const int32_t *obs;
+    const int8_t *mask;
+    int32_t *action;
+    float *logprob, *entropy, *value, *logits;
+    const float *critic_out;
+    uint64_t seed, ply;
+    const uint64_t *ply_base;
+    int64_t table0;
+    int n;
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int kChunkBlocks = kChunk / 1024;  // 20
+__device__ __forceinline__ void issue_chunk(const uint8_t *W, int chunk, uint8_t *slot, int wave, int lane) {
+    const uint8_t *src = W + (size_t)chunk * kChunk + lane * 16;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int blk = wave + kWaves * i;
+        if (blk < kChunkBlocks)
+            __builtin_amdgcn_global_load_lds(src + blk * 1024, (lds_void *)(slot + blk * 1024), 16, 0, 0);
+    }
+}
+
+// one 16-row output tile: bias + sum over KS k-steps; B fragments (one fp32 per lane and k-step) in
+// registers, A fragments read from the ring slot four k-steps per 16-byte LDS read, one group ahead
+template <int KS, int NB>
+__device__ __forceinline__ f32x4 tile_mma(const uint8_t *slot, const float (&B)[NB], int lane) {
+    static_assert(KS <= NB && KS % 4 == 0, "B fragments");
+    constexpr int NG = KS / 4;
+    const float *bias = reinterpret_cast<const float *>(slot + kBiasOff) + 4 * (lane >> 4);
+    f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
+    const f32x4 *A = reinterpret_cast<const f32x4 *>(slot) + lane;
+    f32x4 af[2];
+    af[0] = A[0];
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+        if (q + 1 < NG) af[(q + 1) & 1] = A[(q + 1) * 64];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[q & 1][j], B[4 * q + j], acc, 0, 0, 0);
+        if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    return acc;
+}
+
+// a hidden layer: 16 tiles, each tile's tanh is the next layer's B fragments 4t..4t+3
+template <int KS, int NB, typename Enter>
+__device__ __forceinline__ void layer_tanh(Enter &enter, const float (&B)[NB], float (&H)[kKs2], int lane) {
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) {
+        const f32x4 acc = tile_mma<KS>(enter(), B, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) H[4 * t + i] = tanhf(acc[i]);
+    }
+}
+
+template <bool kCritic, bool kSample>
+__global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, ActArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
+    constexpr int kTotal = kCritic ? kAllChunks : kActorChunks;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+    const int64_t tbase = (int64_t)blockIdx.x * kRowsPerBlock + wave * kRowsPerWave;
+    const int valid = (int)max<int64_t>(0, min<int64_t>(kRowsPerWave, (int64_t)a.n - tbase));
+    uint8_t *ring = lds;
+    uint8_t *ms = lds + kLdsMask + wave * kMaskWave;
+
+#pragma unroll
+    for (int c = 0; c < kSlots - 1; ++c) issue_chunk(W, c, ring + c * kChunk, wave, lane);
+
+    // observation B fragments: lane (r, g), k-step s = obs[table r][4s + g] (exact in fp32)
+    const int32_t *xrow = a.obs + (size_t)min<int64_t>(tbase + r, (int64_t)a.n - 1) * kObs;
+    float X[kKs1];
+#pragma unroll
+    for (int s = 0; s < kKs1; ++s) {
+        const int k = 4 * s + g;
+        X[s] = k < kObs ? (float)xrow[k < kObs ? k : 0] : 0.f;
+    }
+    if (valid == kRowsPerWave) {
+        constexpr int kMQ = kMaskWave / 4;  // 180 dwords
+        const uint32_t *msrc = reinterpret_cast<const uint32_t *>(a.mask + tbase * kAct);
+        for (int q = lane; q < kMQ; q += 64) reinterpret_cast<uint32_t *>(ms)[q] = msrc[q];
+    } else {
+        const int8_t *msrc = a.mask + tbase * kAct;
+        for (int e = lane; e < valid * kAct; e += 64) ms[e] = (uint8_t)msrc[e];
+    }
+
+    int c = 0;
+    auto enter = [&]() -> const uint8_t * {
+        // this wave's part of chunk c landed (later chunks' loads may stay outstanding)
+        if (wave < kChunkBlocks - 2 * kWaves) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // everyone's part landed; slot c-1 is free
+        asm volatile("" ::: "memory");
+        const int nxt = c + kSlots - 1 < kTotal ? c + kSlots - 1 : kTotal - 1;  // past the end: harmless reload
+        issue_chunk(W, nxt, ring + ((c + kSlots - 1) % kSlots) * kChunk, wave, lane);
+        const uint8_t *slot = ring + (c % kSlots) * kChunk;
+        ++c;
+        return slot;
+    };
+    static_assert((kSlots - 2) * 3 == 12 && (kSlots - 2) * 2 == 8, "vmcnt immediates");
+
+    float H1[kKs2];
+    float value = 0.f;
+    if constexpr (kCritic) {
+        layer_tanh<kKs1>(enter, X, H1, lane);
+        // layer 2 tile t -> tanh -> its units' share of the fp32 output unit, on the spot
+#pragma unroll 1
+        for (int t = 0; t < kTiles; ++t) {
+            const f32x4 acc = tile_mma<kKs2>(enter(), H1, lane);
+            const float4 w = *reinterpret_cast<const float4 *>(a.critic_out + 16 * t + 4 * g);
+            value = __builtin_fmaf(w.x, tanhf(acc[0]), value);
+            value = __builtin_fmaf(w.y, tanhf(acc[1]), value);
+            value = __builtin_fmaf(w.z, tanhf(acc[2]), value);
+            value = __builtin_fmaf(w.w, tanhf(acc[3]), value);
+        }
+        value += __shfl_xor(value, 16);  // the other lane groups' units, then the bias
+        value += __shfl_xor(value, 32);
+        value += a.critic_out[kHid];
+    }
+    layer_tanh<kKs1>(enter, X, H1, lane);
+    float H2[kKs2];
+    layer_tanh<kKs2>(enter, H1, H2, lane);
+    f32x4 L[kActTiles];
+#pragma unroll
+    for (int t = 0; t < kActTiles; ++t) L[t] = tile_mma<kKs2>(enter(), H2, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing reloads
+    __builtin_amdgcn_s_barrier();                      // every wave is done with the ring
+
+    // logits -> LDS [table][action] (reusing the ring), then the per-table epilogue
+    float *lg = reinterpret_cast<float *>(ring) + wave * kRowsPerWave * kLogitRow;
+#pragma unroll
+    for (int t = 0; t < kActTiles; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int act = 16 * t + 4 * g + i;
+            if (act < kAct) lg[r * kLogitRow + act] = L[t][i];
+        }
+    wave_lds_sync();
+    if (a.logits) {
+        float *dst = a.logits + tbase * kAct;
+        for (int i = lane; i < valid * kAct; i += 64) dst[i] = lg[(i / kAct) * kLogitRow + i % kAct];
+    }
+    if (g == 0 && r < valid) {
+        const int64_t t = tbase + r;
+        const float *row = lg + r * kLogitRow;
+        const uint8_t *mrow = ms + r * kAct;
+        float lv[kAct];
+        uint64_t legal = 0;
+#pragma unroll
+        for (int k = 0; k < kAct; ++k) {
+            lv[k] = row[k];
+            legal |= (uint64_t)(mrow[k] != 0) << k;
+        }
+        int act = 0;
+        if constexpr (!kSample) {
+            // logits.masked_fill(mask < 0.5, -inf).argmax(): first maximum; all-illegal -> 0
+            float best = -__builtin_inff();
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) {
+                const bool better = ((legal >> k) & 1) && lv[k] > best;
+                best = better ? lv[k] : best;
+                act = better ? k : act;
+            }
+        } else {
+            // masked_categorical: illegal -> -inf unless the row has no legal action; fp32 softmax
+            const uint64_t allow = legal ? legal : (1ull << kAct) - 1;
+            float mx = -__builtin_inff();
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) mx = ((allow >> k) & 1) ? fmaxf(mx, lv[k]) : mx;
+            float S = 0.f, T = 0.f;
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) {
+                const float d = lv[k] - mx, p = ((allow >> k) & 1) ? expf(d) : 0.f;
+                lv[k] = p;
+                S += p;
+                T += p * d;
+            }
+            const float logS = logf(S);
+            const uint64_t ply = a.ply + (a.ply_base ? *a.ply_base : 0ull);
+            const uint4 rnd = philox4x32(make_uint4((uint32_t)(a.table0 + t), (uint32_t)((uint64_t)(a.table0 + t) >> 32),
+                                                    (uint32_t)ply, (uint32_t)(ply >> 32)),
+                                         make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32) ^ 0xA5C3E1F7u));
+            const float target = (float)(rnd.x >> 8) * (1.f / 16777216.f) * S;
+            float cum = 0.f;
+            int last = 0;
+            bool found = false;
+#pragma unroll
+            for (int k = 0; k < kAct; ++k) {
+                const bool al = (allow >> k) & 1;
+                cum += lv[k];
+                last = al ? k : last;
+                const bool hit = al && !found && cum > target;
+                act = hit ? k : act;
+                found = found || hit;
+            }
+            if (!found) act = last;
+            if (a.logprob) a.logprob[t] = row[act] - mx - logS;
+            if (a.entropy) a.entropy[t] = logS - T / S;
+            if (kCritic) a.value[t] = value;
+        }
+        a.action[t] = act;
+    }
+}
+
+}  // namespace splp32
+
+using namespace splp32;
+
+int64_t splp32_bytes(int with_critic) {
+    return with_critic ? (int64_t)kAllChunks * kChunk + kCriticTail : (int64_t)kActorChunks * kChunk;
+}
+
+int splp32_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream) {
+    const PackNet A{actor->w1, actor->b1, actor->w2, actor->b2, actor->w3, actor->b3, kAct};
+    const PackNet C = critic ? PackNet{critic->w1, critic->b1, critic->w2, critic->b2, critic->w3, critic->b3, 1} : A;
+    hipLaunchKernelGGL(k_pack32, dim3(critic ? kAllChunks : kActorChunks), dim3(256), 0, (hipStream_t)stream, A, C,
+                       critic ? 1 : 0, static_cast<uint8_t *>(packed));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return spl_fail(SPL_E_HIP, std::string("k_pack32 launch: ") + hipGetErrorString(e));
+    return SPL_OK;
+}
+
+// image: a packed fp32 image (full when has_critic); critic: evaluate the critic (SAMPLE with value)
+int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, int32_t n, const spl_act_args_t *args,
+               void *stream) {
+    const float *critic_out = has_critic ? reinterpret_cast<const float *>(img + (size_t)kAllChunks * kChunk) : nullptr;
+    const ActArgs a{args->obs,   args->mask,     args->action,  args->logprob, args->entropy,
+                    args->value, args->logits,   critic_out,    args->seed,    args->ply,
+                    args->ply_base, args->table0, n};
+    const dim3 grid((unsigned)((n + kRowsPerBlock - 1) / kRowsPerBlock)), block(kWaves * 64);
+    const hipStream_t s = (hipStream_t)stream;
+    const uint8_t *W = img;
+    if (has_critic && !critic) W += (size_t)kCriticChunks * kChunk;  // the actor part of a full image
+    if (critic)
+        hipLaunchKernelGGL((k_act32<true, true>), grid, block, 0, s, W, a);
+    else if (sample)
+        hipLaunchKernelGGL((k_act32<false, true>), grid, block, 0, s, W, a);
+    else
+        hipLaunchKernelGGL((k_act32<false, false>), grid, block, 0, s, W, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return spl_fail(SPL_E_HIP, std::string("k_act32 launch: ") + hipGetErrorString(e));
+    return SPL_OK;
+}

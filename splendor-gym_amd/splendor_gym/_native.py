@@ -48,10 +48,12 @@ class ActArgs(ctypes.Structure):
     """spl_act_args_t (include/splendor_policy.h)"""
     _fields_ = [("obs", c_void_p), ("mask", c_void_p), ("action", c_void_p), ("logprob", c_void_p),
                 ("entropy", c_void_p), ("value", c_void_p), ("logits", c_void_p), ("seed", c_uint64),
-                ("ply", c_uint64), ("ply_base", c_void_p), ("table0", c_int64), ("mode", c_int32), ("reserved", c_int32)]
+                ("ply", c_uint64), ("ply_base", c_void_p), ("table0", c_int64), ("mode", c_int32), ("image", c_int32)]
 
 
 ACT_SAMPLE, ACT_GREEDY = 0, 1  # SPL_ACT_*
+PREC_FP32, PREC_BF16 = 0, 1    # SPL_PREC_*
+IMG_CRITIC = 1                 # SPL_IMG_CRITIC
 
 
 class DualIo(ctypes.Structure):
@@ -102,8 +104,8 @@ SIGNATURES = {
     "spl_table_upload": ([c_void_p, ctypes.POINTER(ArenaDesc), c_int32, c_int32, c_void_p, c_void_p],
                          c_int32),
     # include/splendor_policy.h
-    "spl_policy_bytes": ([c_int32], c_int64),
-    "spl_policy_pack": ([ctypes.POINTER(MlpDesc), ctypes.POINTER(MlpDesc), c_void_p, c_void_p], c_int32),
+    "spl_policy_bytes": ([c_int32, c_int32], c_int64),
+    "spl_policy_pack": ([ctypes.POINTER(MlpDesc), ctypes.POINTER(MlpDesc), c_int32, c_void_p, c_void_p], c_int32),
     "spl_policy_act": ([c_void_p, c_int64, c_int32, ctypes.POINTER(ActArgs), c_void_p], c_int32),
     # include/splendor_dual.h
     "spl_dual_gate": ([c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int32),

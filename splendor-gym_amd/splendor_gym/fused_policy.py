@@ -1,7 +1,7 @@
 """Fused, batched ActorCritic forward on the GPU (include/splendor_policy.h).
 
 `FusedActorCritic(model)` packs a reference-architecture ActorCritic (ppo_splendor.py:40-59;
-splendor_gym.policy.ActorCritic) into a bf16 image once, then evaluates it for a whole batch of
+splendor_gym.policy.ActorCritic) into a weight image once, then evaluates it for a whole batch of
 tables in one HIP launch straight from the engine's int32 observations and int8 masks:
 
   * ``act(obs, mask)`` = ``model.get_action_and_value(obs.float(), mask.float())`` without
@@ -12,14 +12,19 @@ tables in one HIP launch straight from the engine's int32 observations and int8 
   * ``greedy(obs, mask)`` = ``argmax(actor(obs).masked_fill(mask < 0.5, -inf))`` (first maximum;
     0 when nothing is legal) — the frozen-opponent policy of training_utils.py:263-276.
 
-Matrix products run on bf16 MFMA with fp32 accumulation; logits and values match the fp32
-module to bf16 accuracy (tests/test_gpu_policy.py states the tolerance).  Call ``refresh()``
-after the module's weights change (e.g. after each PPO update).
+precision="fp32" (default, the reference's precision): exact fp32 products and accumulation on
+v_mfma_f32_16x16x4_f32 — logits and values equal the fp32 module's to summation-order rounding
+(tests/test_gpu_policy.py: 1e-5 relative).  precision="bf16" (opt-in): bf16 MFMA with fp32
+accumulation, logits to bf16 accuracy.  Call ``refresh()`` after the module's weights change (e.g.
+after each PPO update).
 """
 import ctypes
 
 from . import _native
-from ._native import ACT_GREEDY, ACT_SAMPLE, NUM_ACTIONS, OBS_DIM, ActArgs, MlpDesc, check, ptr
+from ._native import (ACT_GREEDY, ACT_SAMPLE, IMG_CRITIC, NUM_ACTIONS, OBS_DIM, PREC_BF16, PREC_FP32, ActArgs, MlpDesc,
+                      check, ptr)
+
+_PRECISIONS = {"fp32": PREC_FP32, "bf16": PREC_BF16}
 
 
 def _mlp_desc(seq, keep):
@@ -39,16 +44,21 @@ def _mlp_desc(seq, keep):
 
 
 class FusedActorCritic:
-    def __init__(self, model, with_critic=True, device=None):
+    def __init__(self, model, with_critic=True, device=None, precision="fp32"):
         torch = _native.require_gpu()
         self.torch = torch
         self.lib = _native.load_library()
         self.model = model
         self.with_critic = bool(with_critic)
+        if precision not in _PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(_PRECISIONS)}")
+        self.precision = precision
+        self._prec = _PRECISIONS[precision]
+        self._image_flags = (IMG_CRITIC if self.with_critic else 0) | (self._prec << 1)
         self.device = torch.device(device) if device is not None else next(model.parameters()).device
         if self.device.type != "cuda":
             raise ValueError("FusedActorCritic: the model must live on a GPU (no CPU fallback)")
-        nbytes = self.lib.spl_policy_bytes(1 if self.with_critic else 0)
+        nbytes = self.lib.spl_policy_bytes(1 if self.with_critic else 0, self._prec)
         self.image = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         self.refresh()
 
@@ -68,7 +78,7 @@ class FusedActorCritic:
             critic = _mlp_desc(self.model.critic, keep)
         with self.torch.cuda.device(self.device):
             check(self.lib, self.lib.spl_policy_pack(ctypes.byref(actor), ctypes.byref(critic) if critic else None,
-                                                     self.image.data_ptr(), self._stream()))
+                                                     self._prec, self.image.data_ptr(), self._stream()))
         self._keep = keep  # the pack kernel reads them asynchronously
 
     def _check_inputs(self, obs, mask):
@@ -87,7 +97,7 @@ class FusedActorCritic:
         n = self._check_inputs(obs, mask)
         a = ActArgs(obs=obs.data_ptr(), mask=mask.data_ptr(), action=action.data_ptr(), logprob=ptr(logprob),
                     entropy=ptr(entropy), value=ptr(value), logits=ptr(logits), seed=int(seed) & (2**64 - 1),
-                    ply=int(ply) & (2**64 - 1), ply_base=ptr(ply_base), table0=int(table0), mode=mode, reserved=0)
+                    ply=int(ply) & (2**64 - 1), ply_base=ptr(ply_base), table0=int(table0), mode=mode, image=self._image_flags)
         with self.torch.cuda.device(self.device):
             check(self.lib, self.lib.spl_policy_act(self.image.data_ptr(), self.image.numel(), n, ctypes.byref(a),
                                                     self._stream()))

@@ -1,0 +1,176 @@
+"""Full-size and configuration-5 checks on the GPU:
+
+  * the exact headline variant of bench.py (2 players, 65 536 tables, spl_rollout of K = 64 steps,
+    pool refill every 64 steps fused into the launch, two-wave kernel at 64 tables per workgroup,
+    per-step rollout store with non-temporal stores) equals chained spl_step launches bit for bit,
+    and a 256-table subset of the chain is replayed through the CPU oracle;
+  * 4-player sharding invariance (two shards == one engine);
+  * BASELINE config 5: batched self-play with the fused fp32 ActorCritic as agent AND opponent
+    (DualStepVectorEnv) equals the same loop driven by the torch fp32 module, table by table.
+Reference: scripts/random_rollout.py:13-28, envs/splendor_env.py:51-90, ppo_splendor.py:219-297."""
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle, OracleVec
+
+pytestmark = pytest.mark.gpu
+
+
+def engine(n, P, **kw):
+    from splendor_gym.device import Engine
+    return Engine(n, P, **kw)
+
+
+def bits_of(mask_i8):
+    m = np.asarray(mask_i8).astype(np.uint64)
+    return (m << np.arange(45, dtype=np.uint64)).sum(axis=-1).astype(np.uint64)
+
+
+def store(K, n, dev):
+    import torch
+    return {"obs": torch.empty((K, n, 297), dtype=torch.int32, device=dev),
+            "mask": torch.empty((K, n, 45), dtype=torch.int8, device=dev),
+            "reward": torch.empty((K, n), dtype=torch.float32, device=dev),
+            "terminated": torch.empty((K, n), dtype=torch.uint8, device=dev),
+            "flags": torch.empty((K, n), dtype=torch.uint8, device=dev),
+            "winner": torch.empty((K, n), dtype=torch.int8, device=dev),
+            "final_obs": torch.zeros((K, n, 297), dtype=torch.int32, device=dev)}
+
+
+def test_headline_rollout_65536_equals_step_chain_and_oracle():
+    import torch
+    n, P, K, R, seed, launches = 65536, 2, 64, 64, 0, 2
+    chain = engine(n, P, refill_period=R)
+    roll = engine(n, P, refill_period=R, refill_fused=True, pipeline=True)  # bench.py defaults
+    chain.reset(seeds=range(n))
+    roll.reset(seeds=range(n))
+    dev = chain.device
+    a_c = torch.zeros(n, dtype=torch.int32, device=dev)
+    chain.sample_uniform(out=a_c, seed=seed, ply=0)
+    a_r = a_c.clone()
+    st = {k: (torch.zeros(n, dtype=torch.float32, device=dev), torch.zeros(n, dtype=torch.int32, device=dev))
+          for k in "cr"}
+    sub = np.arange(0, n, 256)  # the oracle replays these tables
+    vec = OracleVec(Oracle(), len(sub), P, [int(t) for t in sub])
+    out = store(K, n, dev)
+    for launch in range(launches):
+        ply0 = 1 + launch * K
+        na = torch.empty_like(a_r)
+        roll.rollout(K, actions=a_r, next_actions=na, policy_seed=seed, ply=ply0, out=out,
+                     ep_return=st["r"][0], ep_count=st["r"][1])
+        a_r = na
+        for k in range(K):
+            acts = a_c[sub].cpu().numpy().copy()
+            na = torch.empty_like(a_c)
+            chain.step(a_c, next_actions=na, policy_seed=seed, ply=ply0 + k, ep_return=st["c"][0],
+                       ep_count=st["c"][1])
+            for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
+                assert torch.equal(out[name][k], getattr(chain, name)), (launch, k, name)
+            term = chain.terminated.bool()
+            assert torch.equal(out["final_obs"][k][term], chain.final_obs[term]), (launch, k)
+            ref = vec.step(acts, want_final=True)
+            np.testing.assert_array_equal(chain.obs[sub].cpu().numpy(), ref["obs"], err_msg=f"{launch} {k}")
+            assert np.array_equal(bits_of(chain.mask[sub].cpu().numpy()), ref["mask"]), (launch, k)
+            assert np.array_equal(chain.reward[sub].cpu().numpy(), ref["reward"]), (launch, k)
+            assert np.array_equal(chain.flags[sub].cpu().numpy(), ref["flags"]), (launch, k)
+            a_c = na
+        assert torch.equal(a_r, a_c), launch
+    assert torch.equal(st["c"][0], st["r"][0]) and torch.equal(st["c"][1], st["r"][1])
+    assert int(st["c"][1].sum()) > 50_000  # about one episode per table per 77 plies
+    assert chain.download().tobytes() == roll.download().tobytes()
+
+
+def test_sharded_equals_whole_4p():
+    """4 players: two shards (global ids 0..1023, 1024..2047) evolve exactly as one engine of 2048,
+    through the rollout kernel and its fused refills (every 16 steps at 4 players)."""
+    import torch
+    n, half, K, launches = 2048, 1024, 64, 3
+    whole = engine(n, 4)
+    parts = [engine(half, 4, table0=0), engine(half, 4, table0=half)]
+    whole.reset(seeds=range(n))
+    parts[0].reset(seeds=range(half))
+    parts[1].reset(seeds=range(half, n))
+    a_w = torch.zeros(n, dtype=torch.int32, device=whole.device)
+    a_p = [torch.zeros(half, dtype=torch.int32, device=whole.device) for _ in parts]
+    whole.sample_uniform(out=a_w, seed=9, ply=0)
+    for p, a in zip(parts, a_p):
+        p.sample_uniform(out=a, seed=9, ply=0)
+    for launch in range(launches):
+        ow, op = store(K, n, whole.device), [store(K, half, whole.device) for _ in parts]
+        na = torch.empty_like(a_w)
+        whole.rollout(K, actions=a_w, next_actions=na, policy_seed=9, ply=1 + K * launch, out=ow)
+        a_w = na
+        for i, p in enumerate(parts):
+            na = torch.empty_like(a_p[i])
+            p.rollout(K, actions=a_p[i], next_actions=na, policy_seed=9, ply=1 + K * launch, out=op[i])
+            a_p[i] = na
+        for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
+            assert torch.equal(torch.cat([op[0][name], op[1][name]], dim=1), ow[name]), (launch, name)
+        assert torch.equal(torch.cat(a_p), a_w)
+    assert whole.download().tobytes() == np.concatenate([p.download() for p in parts]).tobytes()
+
+
+def test_selfplay_fused_fp32_actor_matches_torch():
+    """Config 5 (ppo_splendor.py:219-297 with the frozen-opponent dual step): 4096 tables x 120
+    dual steps, agent = greedy fused fp32 actor, opponent = greedy fused fp32 frozen actor, against
+    the same loop with the torch fp32 modules.  Every table must match step for step (obs, masks,
+    rewards, done, opponent actions), except tables where one of the two sides met a NEAR TIE — top
+    two legal logits within 1e-5 of each other, where the two fp32 summation orders may pick
+    different actions; those tables leave the comparison (at most 1 % of them)."""
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic
+    from splendor_gym.policy import ActorCritic
+    from splendor_gym.selfplay import DualStepVectorEnv
+    N, steps = 4096, 120
+    torch.manual_seed(7)
+    agent = ActorCritic().cuda().eval()
+    opp = ActorCritic().cuda().eval()
+    fa = FusedActorCritic(agent, with_critic=True)   # precision fp32
+    fo = FusedActorCritic(opp, with_critic=False)
+    rec = {}
+
+    def torch_opponent(obs, mask):
+        with torch.no_grad():
+            lg = opp.actor(obs.float())
+        rec["opp_logits"], rec["opp_mask"] = lg, mask.clone()
+        return torch.argmax(lg.masked_fill(mask < 1, float("-inf")), dim=-1).to(torch.int32)
+
+    envF = DualStepVectorEnv(N, opponent=fo.opponent())
+    envT = DualStepVectorEnv(N, opponent=torch_opponent)
+    oF, iF = envF.reset(seed=100)
+    oT, iT = envT.reset(seed=100)
+    tainted = torch.zeros(N, dtype=torch.bool, device=oF.device)
+
+    def near_tie(logits, mask, rows):
+        m = logits[rows].masked_fill(mask[rows] < 1, float("-inf"))
+        top2 = torch.topk(m, 2, dim=-1).values
+        return ((top2[:, 0] - top2[:, 1]) <= 1e-5).all().item()
+
+    done_total = 0
+    for k in range(steps):
+        ok = ~tainted
+        assert torch.equal(oF[ok], oT[ok]), k
+        assert torch.equal(iF["action_mask"][ok], iT["action_mask"][ok]), k
+        aF = fa.greedy(oF, iF["action_mask"])
+        with torch.no_grad():
+            lgT = agent.actor(oT.float())
+        aT = torch.argmax(lgT.masked_fill(iT["action_mask"] < 1, float("-inf")), dim=-1).to(torch.int32)
+        diff = (aF != aT) & ok
+        if diff.any():
+            assert near_tie(lgT, iT["action_mask"], diff), k
+            tainted |= diff
+        oF, rF, _, orF, dF, iF = envF.dual_step(aF)
+        oT, rT, _, orT, dT, iT = envT.dual_step(aT)
+        ok = ~tainted
+        oppF, oppT = iF["opponent_action"], iT["opponent_action"]
+        odiff = (oppF != oppT) & ok
+        if odiff.any():
+            assert near_tie(rec["opp_logits"], rec["opp_mask"], odiff), k
+            tainted |= odiff
+            ok = ~tainted
+        assert torch.equal(rF[ok], rT[ok]) and torch.equal(orF[ok], orT[ok]), k
+        assert torch.equal(dF[ok], dT[ok]), k
+        assert torch.equal(iF["final_observation"][ok & dF], iT["final_observation"][ok & dT]), k
+        done_total += int(dF[ok].sum())
+    assert tainted.float().mean().item() <= 0.01, int(tainted.sum())
+    assert done_total > 1000  # many games finished and were re-dealt inside the loop

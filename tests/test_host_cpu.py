@@ -48,20 +48,31 @@ def test_policy_abi_host_side_errors():
     """spl_policy_* argument checks (include/splendor_policy.h) run before any device work."""
     from splendor_gym import _native
     lib = _native.load_library()
-    # actor: 18 bf16 chunks; full image: 35 chunks + the fp32 critic output layer (w3, b3, padding)
-    assert lib.spl_policy_bytes(0) == 18 * 20480 and lib.spl_policy_bytes(1) == 35 * 20480 + 272 * 4
-    assert lib.spl_policy_pack(None, None, None, None) == -1
+    # bf16: actor 18 chunks, full image 35 chunks + the fp32 critic output layer; fp32: 35 / 67 chunks + tail
+    assert lib.spl_policy_bytes(0, 1) == 18 * 20480 and lib.spl_policy_bytes(1, 1) == 35 * 20480 + 272 * 4
+    assert lib.spl_policy_bytes(0, 0) == 35 * 20480 and lib.spl_policy_bytes(1, 0) == 67 * 20480 + 272 * 4
+    assert lib.spl_policy_bytes(0, 9) == -1
+    assert lib.spl_policy_pack(None, None, 0, None, None) == -1
     assert b"actor" in lib.spl_last_error()
     assert lib.spl_policy_act(None, 0, 1, None, None) == -1
-    args = _native.ActArgs(obs=256, mask=256, action=256, mode=0)
+    args = _native.ActArgs(obs=256, mask=256, action=256, mode=0, image=0)
     args.obs = 258  # misaligned observations
-    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0), 1, ctypes.byref(args), None) == -1
+    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0, 0), 1, ctypes.byref(args), None) == -1
     assert b"obs" in lib.spl_last_error()
     args.obs, args.value = 256, 256  # critic requested from an actor-only image
-    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0), 1, ctypes.byref(args), None) == -1
+    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0, 0), 1, ctypes.byref(args), None) == -1
     assert b"critic" in lib.spl_last_error() or b"value" in lib.spl_last_error()
+    # an image size that does not match args->image (a full image passed as actor-only, or the
+    # reverse) is refused instead of evaluating the wrong chunks (ADVICE r01)
+    args.value = None
+    for image, size in ((0, lib.spl_policy_bytes(1, 0)), (1, lib.spl_policy_bytes(0, 0)),
+                        (2, lib.spl_policy_bytes(0, 0)), (0, lib.spl_policy_bytes(0, 1)), (3, 35 * 20480)):
+        args.image = image
+        assert lib.spl_policy_act(ctypes.c_void_p(4096), size, 1, ctypes.byref(args), None) == -1
+        assert b"packed_bytes" in lib.spl_last_error()
+    args.image = 0
     args.value, args.mode = None, 7
-    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0), 1, ctypes.byref(args), None) == -1
+    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0, 0), 1, ctypes.byref(args), None) == -1
 
 
 def test_arena_layout_sizes():

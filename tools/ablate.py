@@ -29,7 +29,7 @@ def build():
         bits = VARIANTS[name]
         out = os.path.join(OUTD, f"lib_{name}.so")
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", f"-DSPL_ABL={bits}",
-                        "-shared", "-o", out, *[os.path.join(CSRC, f) for f in ("spl_engine.hip", "spl_policy.hip", "spl_dual.hip")]], check=True)
+                        "-shared", "-o", out, *[os.path.join(CSRC, f) for f in ("spl_engine.hip", "spl_policy.hip", "spl_policy32.hip", "spl_dual.hip")]], check=True)
 
 
 CHILD = r'''

@@ -37,7 +37,8 @@ def main():
     obs, mask = e.obs, e.mask
     torch.manual_seed(0)
     m = ActorCritic().to(e.device).eval()
-    f = FusedActorCritic(m)
+    f = FusedActorCritic(m)                       # fp32 (exact products, v_mfma_f32_16x16x4_f32)
+    f16 = FusedActorCritic(m, precision="bf16")   # opt-in bf16 MFMA
 
     def timeit(fn):
         for _ in range(5):
@@ -52,8 +53,10 @@ def main():
         return s.elapsed_time(t) * 1e3 / args.iters
 
     res = {}
-    res["fused_sample_us"] = timeit(lambda: f.act(obs, mask, seed=1, ply=2))
-    res["fused_greedy_us"] = timeit(lambda: f.greedy(obs, mask))
+    res["fused_fp32_sample_us"] = timeit(lambda: f.act(obs, mask, seed=1, ply=2))
+    res["fused_fp32_greedy_us"] = timeit(lambda: f.greedy(obs, mask))
+    res["fused_bf16_sample_us"] = timeit(lambda: f16.act(obs, mask, seed=1, ply=2))
+    res["fused_bf16_greedy_us"] = timeit(lambda: f16.greedy(obs, mask))
 
     def torch_sample():
         with torch.no_grad():
@@ -69,8 +72,10 @@ def main():
         res["torch_fp32_greedy_us"] = timeit(lambda: greedy_actions(m, obs, mask))
     fl_s = 2.0 * n * (MACS_ACTOR + MACS_CRITIC)
     fl_g = 2.0 * n * MACS_ACTOR
-    res["fused_sample_tflops"] = fl_s / res["fused_sample_us"] / 1e6
-    res["fused_greedy_tflops"] = fl_g / res["fused_greedy_us"] / 1e6
+    for p in ("fp32", "bf16"):
+        res[f"fused_{p}_sample_tflops"] = fl_s / res[f"fused_{p}_sample_us"] / 1e6
+        res[f"fused_{p}_greedy_tflops"] = fl_g / res[f"fused_{p}_greedy_us"] / 1e6
+    res["peak_tflops"] = {"fp32": 157.3, "bf16": 2500.0}  # dense MFMA peaks (MI355X_MICROARCH.md)
     res["tables"] = n
     print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in res.items()}))
 

@@ -26,9 +26,12 @@ def main():
     ap.add_argument("--tables", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=16)
-    ap.add_argument("--bf16", action="store_true", help="torch actor under bf16 autocast")
+    ap.add_argument("--bf16", action="store_true",
+                    help="opt-in reduced precision: the fused kernel's bf16 MFMA image, or the torch actor under bf16 "
+                         "autocast (default fp32, the reference's precision)")
     ap.add_argument("--actor", choices=["fused", "torch"], default="fused",
-                    help="fused: spl_policy_act (bf16 MFMA kernel) for agent and opponent; torch: the nn.Module")
+                    help="fused: spl_policy_act (fp32 MFMA kernel, bf16 with --bf16) for agent and opponent; "
+                         "torch: the nn.Module")
     ap.add_argument("--no-graph", action="store_true")
     args = ap.parse_args()
 
@@ -47,14 +50,15 @@ def main():
     opp_model = ActorCritic().to(dev).eval()
     fused = args.actor == "fused"
     if fused:
-        agent_k = FusedActorCritic(agent)
-        opponent = FusedActorCritic(opp_model, with_critic=False).opponent()
+        prec = "bf16" if args.bf16 else "fp32"
+        agent_k = FusedActorCritic(agent, precision=prec)
+        opponent = FusedActorCritic(opp_model, with_critic=False, precision=prec).opponent()
     else:
         opponent = greedy_opponent_from(opp_model)
     env = DualStepVectorEnv(N, device=dev, opponent=opponent, table0=rank * N, opponent_obs=False)
     obs, info = env.reset(seed=rank * N)
     mask = info["action_mask"]
-    amp = torch.autocast("cuda", dtype=torch.bfloat16) if args.bf16 else torch.autocast("cuda", enabled=False)
+    amp = torch.autocast("cuda", dtype=torch.bfloat16) if (args.bf16 and not fused) else torch.autocast("cuda", enabled=False)
 
     ply_t = torch.zeros(1, dtype=torch.int64, device=dev)  # advanced inside the graph: fresh draws per replay
 
@@ -107,11 +111,12 @@ def main():
             "metric": f"env-steps/sec (whole node), 2p self-play with on-device ActorCritic actor, {N} tables/GPU",
             "value": round(steps / full, 1), "unit": "env-steps/s", "n_gpus": world, "iters": args.iters,
             "ms_per_dual_step": round(full / args.iters * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-            "dtype": "bf16" if (args.bf16 or fused) else "fp32", "data": "synthetic: seeded deals, random-init ActorCritic",
+            "dtype": "bf16" if args.bf16 else "fp32", "data": "synthetic: seeded deals, random-init ActorCritic",
             "config": {"workload": "PPO rollout step: ActorCritic.get_action_and_value + DualStepVectorEnv.dual_step "
                                    "(greedy frozen-ActorCritic opponent, reset after done)",
                        "tables_per_gpu": N, "players": 2, "launch": "hipGraph replay" if graph is not None else "eager",
-                       "actor": "spl_policy_act (fused bf16 MFMA)" if fused else "torch nn.Module"},
+                       "actor": (f"spl_policy_act (fused, {'bf16' if args.bf16 else 'fp32'} MFMA)" if fused
+                                 else "torch nn.Module" + (" (bf16 autocast)" if args.bf16 else ""))},
             "env_only": {"value": round(steps / env_only, 1), "ms_per_dual_step": round(env_only / args.iters * 1e3, 4),
                          "note": "same loop with the agent's forward replaced by device uniform sampling (eager)"},
         }))

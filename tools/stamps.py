@@ -46,7 +46,7 @@ def main():
         extra = os.environ.get("STAMP_DEFS", "").split()  # e.g. STAMP_DEFS=-DSPL_ABL=4096
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-DSPL_STAMPS",
                         *extra, "-shared", "-o", LIB, *[os.path.join(REPO, "splendor-gym_amd", "csrc", f)
-                        for f in ("spl_engine.hip", "spl_policy.hip", "spl_dual.hip")]],
+                        for f in ("spl_engine.hip", "spl_policy.hip", "spl_policy32.hip", "spl_dual.hip")]],
                        check=True)
         if "--build-only" in sys.argv:
             return 0

@@ -13,7 +13,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "splendor-gym_amd", "csrc")
 OUTD = os.path.join(REPO, "splendor-gym_amd", "ablate")
-SRCS = [os.path.join(CSRC, f) for f in ("spl_engine.hip", "spl_policy.hip", "spl_dual.hip")]
+SRCS = [os.path.join(CSRC, f) for f in ("spl_engine.hip", "spl_policy.hip", "spl_policy32.hip", "spl_dual.hip")]
 
 
 def build(specs):

@@ -65,7 +65,7 @@ def main():
         os.makedirs(os.path.dirname(LIB), exist_ok=True)
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-DSPL_STAMPS", "-w",
                         "-shared", "-o", LIB, *[os.path.join(REPO, "splendor-gym_amd", "csrc", f)
-                                                  for f in ("spl_engine.hip", "spl_policy.hip", "spl_dual.hip")]],
+                                                  for f in ("spl_engine.hip", "spl_policy.hip", "spl_policy32.hip", "spl_dual.hip")]],
                        check=True)
         if "--build-only" in sys.argv:
             return 0
