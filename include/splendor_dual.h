@@ -51,6 +51,15 @@ int spl_dual_gate(int32_t n, const uint8_t *terminated_a, const uint8_t *flags_a
                   void *stream);
 int spl_dual_finish(int32_t n, const spl_dual_io_t *io, void *stream);
 
+/* ppo_splendor.py:137-143 opponent_supplier, per table: every table with draw[t] != 0 (draw NULL = all)
+ * starts an episode against group_of[t] = 0 (the current policy) with probability p_current or when
+ * pool_len == 0, else pool_slots[i] for i uniform in 0..pool_len-1 (one of the <= pool_size frozen
+ * snapshots, ppo_splendor.py:366-370).  Draws come from a Philox stream keyed by (seed; table0 + t,
+ * episode[t]) and episode[t] is incremented, so results do not depend on sharding or batching. */
+int spl_dual_draw_opponents(int32_t n, const uint8_t *draw, uint32_t *episode, int32_t *group_of,
+                            const int32_t *pool_slots, int32_t pool_len, float p_current, uint64_t seed, int64_t table0,
+                            void *stream);
+
 #ifdef __cplusplus
 }
 #endif

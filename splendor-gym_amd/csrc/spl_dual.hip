@@ -8,6 +8,7 @@
 
 #include "../../include/splendor_amd.h"
 #include "../../include/splendor_dual.h"
+#include "spl_rng.h"
 
 int spl_fail(int code, const std::string &msg);  // spl_engine.hip
 
@@ -79,6 +80,22 @@ __global__ __launch_bounds__(256) void k_dual_opp_obs(int n, const uint8_t *__re
     }
 }
 
+// ppo_splendor.py:137-143 opponent_supplier for every table starting an episode
+__global__ __launch_bounds__(256) void k_draw_opponents(int n, const uint8_t *__restrict__ draw,
+                                                        uint32_t *__restrict__ episode, int32_t *__restrict__ group_of,
+                                                        const int32_t *__restrict__ pool_slots, int pool_len,
+                                                        float p_current, uint64_t seed, int64_t table0) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || (draw && draw[i] == 0)) return;
+    const uint32_t ep = episode[i];
+    episode[i] = ep + 1;
+    const uint64_t t = (uint64_t)(table0 + i);
+    const uint4 r = spl::philox4x32(make_uint4((uint32_t)t, (uint32_t)(t >> 32), ep, 0x6F70706Fu),
+                                    make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    const float u = (float)(r.x >> 8) * (1.f / 16777216.f);
+    group_of[i] = (pool_len <= 0 || u < p_current) ? 0 : pool_slots[(uint32_t)(((uint64_t)r.y * (uint32_t)pool_len) >> 32)];
+}
+
 }  // namespace spld
 
 using namespace spld;
@@ -115,6 +132,18 @@ int spl_dual_finish(int32_t n, const spl_dual_io_t *io, void *stream) {
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? SPL_OK : spl_fail(SPL_E_HIP, std::string("k_dual_finish: ") + hipGetErrorString(e));
+}
+
+int spl_dual_draw_opponents(int32_t n, const uint8_t *draw, uint32_t *episode, int32_t *group_of,
+                            const int32_t *pool_slots, int32_t pool_len, float p_current, uint64_t seed, int64_t table0,
+                            void *stream) {
+    if (n <= 0) return spl_fail(SPL_E_ARG, "n must be positive");
+    if (!episode || !group_of || (pool_len > 0 && !pool_slots)) return spl_fail(SPL_E_ARG, "null buffer");
+    if (!(p_current >= 0.f && p_current <= 1.f)) return spl_fail(SPL_E_ARG, "p_current must be in [0, 1]");
+    hipLaunchKernelGGL(k_draw_opponents, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, draw, episode,
+                       group_of, pool_slots, pool_len, p_current, seed, table0);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? SPL_OK : spl_fail(SPL_E_HIP, std::string("k_draw_opponents: ") + hipGetErrorString(e));
 }
 
 }  // extern "C"

@@ -475,7 +475,9 @@ using namespace splp;
 int64_t splp32_bytes(int with_critic);  // spl_policy32.hip: the fp32 image
 int splp32_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream);
 int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, int32_t n, const spl_act_args_t *args,
-               void *stream);
+               void *stream, int groups = 0, int64_t image_stride = 0, const int32_t *group_of = nullptr,
+               void *scratch = nullptr);
+int64_t splp32_group_scratch(int32_t n, int32_t groups);
 
 extern "C" {
 
@@ -540,6 +542,32 @@ int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const sp
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return spl_fail(SPL_E_HIP, std::string("k_act launch: ") + hipGetErrorString(e));
     return SPL_OK;
+}
+
+int64_t spl_policy_group_scratch_bytes(int32_t n, int32_t n_images) {
+    if (n <= 0 || n_images <= 0) return SPL_E_ARG;
+    return splp32_group_scratch(n, n_images);
+}
+
+int spl_policy_act_grouped(const void *images, int64_t image_bytes, int32_t n_images, const int32_t *group_of,
+                           void *scratch, int32_t n, const spl_act_args_t *args, void *stream) {
+    if (!args || !group_of || !scratch) return spl_fail(SPL_E_ARG, "null argument");
+    if (!images || ((uintptr_t)images & 255u) || (image_bytes & 255))
+        return spl_fail(SPL_E_ARG, "images must be 256-byte aligned, image_bytes a multiple of 256");
+    if (n_images <= 0 || n_images > 64) return spl_fail(SPL_E_ARG, "n_images must be 1..64");
+    if (((uintptr_t)scratch & 3u)) return spl_fail(SPL_E_ARG, "scratch must be 4-byte aligned");
+    const int precision = (args->image >> 1) & 3;
+    const bool has_critic = (args->image & SPL_IMG_CRITIC) != 0;
+    if (precision != SPL_PREC_FP32) return spl_fail(SPL_E_ARG, "grouped evaluation is implemented for fp32 images");
+    if (has_critic) return spl_fail(SPL_E_ARG, "grouped evaluation serves actor-only images");
+    if (image_bytes < spl_policy_bytes(0, precision)) return spl_fail(SPL_E_ARG, "image_bytes smaller than an image");
+    if (n <= 0) return spl_fail(SPL_E_ARG, "n must be positive");
+    if (!args->obs || ((uintptr_t)args->obs & 15u)) return spl_fail(SPL_E_ARG, "obs must be 16-byte aligned");
+    if (!args->mask || !args->action) return spl_fail(SPL_E_ARG, "mask / action missing");
+    if (args->mode != SPL_ACT_SAMPLE && args->mode != SPL_ACT_GREEDY) return spl_fail(SPL_E_ARG, "unknown mode");
+    if (args->value) return spl_fail(SPL_E_ARG, "grouped evaluation has no critic");
+    return splp32_act(static_cast<const uint8_t *>(images), false, false, args->mode == SPL_ACT_SAMPLE, n, args, stream,
+                      n_images, image_bytes, group_of, scratch);
 }
 
 }  // extern "C"

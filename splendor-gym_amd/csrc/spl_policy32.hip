@@ -110,6 +110,12 @@ struct ActArgs {
     const uint64_t *ply_base;
     int64_t table0;
     int n;
+    // grouped evaluation (spl_policy_act_grouped): tables sorted by network (order[n]), per group
+    // g its first workgroup gtab[g] (g <= G) and its first position in order gtab[G + 1 + g]
+    const int32_t *order;
+    const int32_t *gtab;
+    int groups;
+    int64_t image_stride;
 };
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -168,8 +174,23 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
     constexpr int kTotal = kCritic ? kAllChunks : kActorChunks;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
-    const int64_t tbase = (int64_t)blockIdx.x * kRowsPerBlock + wave * kRowsPerWave;
-    const int valid = (int)max<int64_t>(0, min<int64_t>(kRowsPerWave, (int64_t)a.n - tbase));
+    // rows [rbase, rend) of this workgroup: tables rbase.. directly, or positions of the grouped
+    // order (one network per workgroup: the group whose workgroup range holds blockIdx.x)
+    int64_t rbase = (int64_t)blockIdx.x * kRowsPerBlock, rend = a.n;
+    if (a.order) {
+        const int b = (int)blockIdx.x;
+        if (b >= a.gtab[a.groups]) return;  // past the last group's workgroups (every wave leaves)
+        int grp = 0;
+        for (int i = 1; i < a.groups; ++i) grp = a.gtab[i] <= b ? i : grp;
+        W += (size_t)grp * a.image_stride;
+        const int64_t first = a.gtab[a.groups + 1 + grp];
+        rbase = first + (int64_t)(b - a.gtab[grp]) * kRowsPerBlock;
+        rend = a.gtab[a.groups + 2 + grp];
+    }
+    const int64_t tbase = rbase + wave * kRowsPerWave;
+    const int valid = (int)max<int64_t>(0, min<int64_t>(kRowsPerWave, rend - tbase));
+    // table of row i of this wave (i < valid)
+    auto table_of = [&](int i) -> int64_t { return a.order ? (int64_t)a.order[tbase + i] : tbase + i; };
     uint8_t *ring = lds;
     uint8_t *ms = lds + kLdsMask + wave * kMaskWave;
 
@@ -177,14 +198,17 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
     for (int c = 0; c < kSlots - 1; ++c) issue_chunk(W, c, ring + c * kChunk, wave, lane);
 
     // observation B fragments: lane (r, g), k-step s = obs[table r][4s + g] (exact in fp32)
-    const int32_t *xrow = a.obs + (size_t)min<int64_t>(tbase + r, (int64_t)a.n - 1) * kObs;
+    const int64_t xt = valid > 0 ? table_of(r < valid ? r : 0) : 0;
+    const int32_t *xrow = a.obs + (size_t)xt * kObs;
     float X[kKs1];
 #pragma unroll
     for (int s = 0; s < kKs1; ++s) {
         const int k = 4 * s + g;
         X[s] = k < kObs ? (float)xrow[k < kObs ? k : 0] : 0.f;
     }
-    if (valid == kRowsPerWave) {
+    if (a.order) {  // gathered rows
+        for (int e = lane; e < valid * kAct; e += 64) ms[e] = (uint8_t)a.mask[table_of(e / kAct) * kAct + e % kAct];
+    } else if (valid == kRowsPerWave) {
         constexpr int kMQ = kMaskWave / 4;  // 180 dwords
         const uint32_t *msrc = reinterpret_cast<const uint32_t *>(a.mask + tbase * kAct);
         for (int q = lane; q < kMQ; q += 64) reinterpret_cast<uint32_t *>(ms)[q] = msrc[q];
@@ -246,11 +270,11 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         }
     wave_lds_sync();
     if (a.logits) {
-        float *dst = a.logits + tbase * kAct;
-        for (int i = lane; i < valid * kAct; i += 64) dst[i] = lg[(i / kAct) * kLogitRow + i % kAct];
+        for (int i = lane; i < valid * kAct; i += 64)
+            a.logits[table_of(i / kAct) * kAct + i % kAct] = lg[(i / kAct) * kLogitRow + i % kAct];
     }
     if (g == 0 && r < valid) {
-        const int64_t t = tbase + r;
+        const int64_t t = table_of(r);
         const float *row = lg + r * kLogitRow;
         const uint8_t *mrow = ms + r * kAct;
         float lv[kAct];
@@ -329,14 +353,74 @@ int splp32_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, v
     return SPL_OK;
 }
 
+// ---- grouping: counting sort of tables by network ------------------------------------------
+// scratch (int32): counts[G] | cursor[G] | gtab[2G + 2] (workgroup starts G+1, order starts G+1) | order[n]
+__global__ __launch_bounds__(256) void k_group_count(int n, int G, const int32_t *group_of, int32_t *counts) {
+    __shared__ int32_t h[64];
+    if (threadIdx.x < 64) h[threadIdx.x] = 0;
+    __syncthreads();
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const int g = group_of[i];
+        if (g >= 0 && g < G) atomicAdd(&h[g], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < G && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(64) void k_group_scan(int G, int32_t *counts, int32_t *cursor, int32_t *gtab) {
+    if (threadIdx.x != 0) return;
+    int wg = 0, pos = 0;
+    for (int g = 0; g < G; ++g) {
+        gtab[g] = wg;
+        gtab[G + 1 + g] = pos;
+        cursor[g] = pos;
+        wg += (counts[g] + kRowsPerBlock - 1) / kRowsPerBlock;
+        pos += counts[g];
+    }
+    gtab[G] = wg;
+    gtab[2 * G + 1] = pos;
+}
+
+__global__ __launch_bounds__(256) void k_group_scatter(int n, int G, const int32_t *group_of, int32_t *cursor,
+                                                       int32_t *order) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int g = group_of[i];
+    if (g >= 0 && g < G) order[atomicAdd(&cursor[g], 1)] = i;  // order within a group is irrelevant
+}
+
+constexpr int kMaxGroups = 64;
+
+int64_t splp32_group_scratch(int32_t n, int32_t groups) { return 4 * ((int64_t)4 * groups + 2 + n); }
+
 // image: a packed fp32 image (full when has_critic); critic: evaluate the critic (SAMPLE with value)
 int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, int32_t n, const spl_act_args_t *args,
-               void *stream) {
+               void *stream, int groups = 0, int64_t image_stride = 0, const int32_t *group_of = nullptr,
+               void *scratch = nullptr) {
     const float *critic_out = has_critic ? reinterpret_cast<const float *>(img + (size_t)kAllChunks * kChunk) : nullptr;
-    const ActArgs a{args->obs,   args->mask,     args->action,  args->logprob, args->entropy,
-                    args->value, args->logits,   critic_out,    args->seed,    args->ply,
-                    args->ply_base, args->table0, n};
-    const dim3 grid((unsigned)((n + kRowsPerBlock - 1) / kRowsPerBlock)), block(kWaves * 64);
+    ActArgs a{args->obs,      args->mask,   args->action, args->logprob, args->entropy, args->value,  args->logits,
+              critic_out,     args->seed,   args->ply,    args->ply_base, args->table0,  n,           nullptr,
+              nullptr,        0,            0};
+    dim3 grid((unsigned)((n + kRowsPerBlock - 1) / kRowsPerBlock)), block(kWaves * 64);
+    if (groups > 0) {  // sort the tables by network, then one workgroup per 128 tables of one group
+        if (groups > kMaxGroups) return spl_fail(SPL_E_ARG, "at most 64 networks per grouped call");
+        if (critic) return spl_fail(SPL_E_ARG, "grouped evaluation serves actor-only images");
+        int32_t *counts = static_cast<int32_t *>(scratch), *cursor = counts + groups, *gtab = cursor + groups;
+        int32_t *order = gtab + 2 * groups + 2;
+        const hipStream_t s = (hipStream_t)stream;
+        if (hipMemsetAsync(counts, 0, sizeof(int32_t) * groups, s) != hipSuccess)
+            return spl_fail(SPL_E_HIP, "group scratch clear");
+        const dim3 g256((unsigned)((n + 255) / 256));
+        hipLaunchKernelGGL(k_group_count, g256, dim3(256), 0, s, n, groups, group_of, counts);
+        hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(64), 0, s, groups, counts, cursor, gtab);
+        hipLaunchKernelGGL(k_group_scatter, g256, dim3(256), 0, s, n, groups, group_of, cursor, order);
+        a.order = order;
+        a.gtab = gtab;
+        a.groups = groups;
+        a.image_stride = image_stride;
+        grid.x += groups;  // every group may end in a partial workgroup
+    }
     const hipStream_t s = (hipStream_t)stream;
     const uint8_t *W = img;
     if (has_critic && !critic) W += (size_t)kCriticChunks * kChunk;  // the actor part of a full image

@@ -110,6 +110,11 @@ SIGNATURES = {
     # include/splendor_dual.h
     "spl_dual_gate": ([c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
     "spl_dual_finish": ([c_int32, ctypes.POINTER(DualIo), c_void_p], c_int32),
+    "spl_dual_draw_opponents": ([c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, ctypes.c_float, c_uint64,
+                                 c_int64, c_void_p], c_int32),
+    "spl_policy_group_scratch_bytes": ([c_int32, c_int32], c_int64),
+    "spl_policy_act_grouped": ([c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_int32, ctypes.POINTER(ActArgs),
+                                c_void_p], c_int32),
 }
 
 

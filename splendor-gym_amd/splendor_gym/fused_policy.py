@@ -129,3 +129,93 @@ class FusedActorCritic:
     def opponent(self):
         """A batched opponent for DualStepVectorEnv: (obs, mask) -> int32 actions."""
         return lambda obs, mask: self.greedy(obs, mask)
+
+
+class OpponentPool:
+    """The self-play opponent of ppo_splendor.py:137-143 / 366-370, batched: each table's episode
+    plays either the CURRENT policy (probability p_current, and always while the pool is empty) or
+    one of up to `pool_size` frozen snapshots chosen uniformly — drawn per table at every episode
+    start (spl_dual_draw_opponents: Philox keyed by (seed; table, episode), so results do not depend
+    on batching or sharding).  Every network is the greedy masked argmax of its actor
+    (model_greedy_policy_from / frozen_policy_from), evaluated for all tables in ONE launch
+    (spl_policy_act_grouped: tables sorted by network, one network per workgroup), fp32.
+
+    Images: slot 0 is the current policy (re-packed by refresh(), e.g. after each PPO update);
+    snapshots live in a ring of pool_size + 2 slots, so a snapshot that leaves the pool keeps its
+    weights until two more snapshots are added — episodes already playing it finish against it, as
+    the reference's per-episode frozen copies do.  (The reference appends agent.state_dict(), whose
+    tensors alias the live parameters, so its "frozen" pool entries are the current weights at the
+    episode's start; add_snapshot here copies the weights at the time it is called.)"""
+
+    def __init__(self, agent, pool_size: int = 12, p_current: float = 0.25, seed: int = 0, device=None):
+        torch = _native.require_gpu()
+        self.torch = torch
+        self.lib = _native.load_library()
+        self.agent = agent
+        self.pool_size, self.p_current, self.seed = int(pool_size), float(p_current), int(seed)
+        self.device = torch.device(device) if device is not None else next(agent.parameters()).device
+        self.image_bytes = int(self.lib.spl_policy_bytes(0, PREC_FP32))
+        self.n_images = 1 + self.pool_size + 2
+        if self.n_images > 64:
+            raise ValueError("pool_size at most 61")
+        self.images = torch.zeros(self.n_images * self.image_bytes, dtype=torch.uint8, device=self.device)
+        self.pool = []                      # image slots in pool order (oldest first)
+        self._next = 0                      # ring position of the next snapshot slot
+        self.slots = torch.zeros(max(1, self.pool_size), dtype=torch.int32, device=self.device)
+        self._scratch = None
+        self._keep = []
+        self.refresh()
+
+    def _stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _pack(self, model, slot):
+        keep = []
+        actor = _mlp_desc(model.actor, keep)
+        ptr_ = self.images.data_ptr() + slot * self.image_bytes
+        with self.torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_policy_pack(ctypes.byref(actor), None, PREC_FP32, ptr_, self._stream()))
+        self._keep.append(keep)
+        self._keep = self._keep[-8:]
+
+    def refresh(self):
+        """Re-pack the current policy (image 0) from the agent's live weights."""
+        self._pack(self.agent, 0)
+
+    def add_snapshot(self, model=None):
+        """pool.append(snapshot); pool.pop(0) beyond pool_size (ppo_splendor.py:366-370).  `model`
+        defaults to the agent (its weights now)."""
+        slot = 1 + self._next
+        self._next = (self._next + 1) % (self.n_images - 1)
+        self._pack(self.agent if model is None else model, slot)
+        self.pool.append(slot)
+        if len(self.pool) > self.pool_size:
+            self.pool.pop(0)
+        if self.pool:
+            self.slots[:len(self.pool)].copy_(self.torch.tensor(self.pool, dtype=self.torch.int32))
+
+    def draw(self, group_of, episode, draw_mask=None, table0=0):
+        """Choose each (draw_mask-selected) table's opponent for its next episode."""
+        with self.torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_dual_draw_opponents(
+                group_of.numel(), ptr(draw_mask), episode.data_ptr(), group_of.data_ptr(), self.slots.data_ptr(),
+                len(self.pool), ctypes.c_float(self.p_current), self.seed & (2**64 - 1), int(table0), self._stream()))
+
+    def act(self, obs, mask, group_of, out=None):
+        """Greedy action of each table's network: int32 [n]."""
+        t = self.torch
+        n = obs.shape[0]
+        if obs.dtype != t.int32 or not obs.is_contiguous() or mask.dtype != t.int8 or not mask.is_contiguous():
+            raise ValueError("obs int32 [n, 297] and mask int8 [n, 45], contiguous")
+        nbytes = int(self.lib.spl_policy_group_scratch_bytes(n, self.n_images))
+        if self._scratch is None or self._scratch.numel() < nbytes:
+            self._scratch = t.empty(nbytes, dtype=t.uint8, device=self.device)
+        action = out if out is not None else t.empty(n, dtype=t.int32, device=self.device)
+        a = ActArgs(obs=obs.data_ptr(), mask=mask.data_ptr(), action=action.data_ptr(), logprob=None, entropy=None,
+                    value=None, logits=None, seed=0, ply=0, ply_base=None, table0=0, mode=ACT_GREEDY,
+                    image=PREC_FP32 << 1)
+        with t.cuda.device(self.device):
+            check(self.lib, self.lib.spl_policy_act_grouped(self.images.data_ptr(), self.image_bytes, self.n_images,
+                                                            group_of.data_ptr(), self._scratch.data_ptr(), n,
+                                                            ctypes.byref(a), self._stream()))
+        return action

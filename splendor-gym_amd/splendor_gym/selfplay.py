@@ -10,7 +10,15 @@ opponent move) with the opponent's actions computed in between on the device, by
     "greedy_v1" / "basic_priority" (scripts/eval_suite.py:9-78; random choices are Philox draws),
   * or any batched callable (obs int32 [N,297], mask int8 [N,45]) -> actions [N], e.g.
     splendor_gym.policy.greedy_opponent_from(actor) for self-play against a network
-    (eval_suite.py:131-141 model_greedy_policy_from).
+    (eval_suite.py:131-141 model_greedy_policy_from),
+  * or an OpponentPool (splendor_gym.fused_policy): the opponent_supplier of ppo_splendor.py:137-143 —
+    each table's episode plays the current policy or a frozen snapshot, drawn per table at every
+    episode start (info["opponent_index"]: 0 = current, else the snapshot's image slot).
+
+random_starts (dual_step_native.py:61-77): the reference flips a coin only when the opponent is to
+play right after reset, and lets it move first on heads — then its loop moves the opponent while it
+is to play either way, so heads and tails play the same moves.  A fresh deal always has player 0
+to play, so the flip never happens; the flag is accepted for signature parity and changes nothing.
 
 Per table (reference semantics):
   * the agent's move ends the game (only the no-legal-move draw can: terminal needs to_play == 0):
@@ -61,7 +69,7 @@ class DualInfo(Mapping):
 
 class DualStepVectorEnv:
     def __init__(self, num_envs, device=None, opponent="random", policy_seed=0, refill_period=None, table0=0,
-                 opponent_obs=True):
+                 opponent_obs=True, random_starts=False):
         if isinstance(opponent, str) and opponent not in _DEVICE_POLICIES:
             raise ValueError(f"unknown device opponent {opponent!r}; choose {sorted(_DEVICE_POLICIES)} or a callable")
         self.eng = Engine(num_envs, 2, device=device, refill_period=refill_period, table0=table0)
@@ -78,6 +86,12 @@ class DualStepVectorEnv:
         self.agent_reward, self.opp_reward = z(t.float32), z(t.float32)
         self.done, self.game_ended_on, self.info_flags = z(t.bool), z(t.int8), z(t.uint8)  # done: 0/1 bytes
         self.opp_obs = t.zeros(n, _native.OBS_DIM, dtype=t.int32, device=dev) if opponent_obs else None
+        self.random_starts = bool(random_starts)
+        from .fused_policy import OpponentPool
+        self.pool = opponent if isinstance(opponent, OpponentPool) else None
+        if self.pool is not None:  # per-table opponent of the current episode, and each table's episode count
+            self.opp_group = z(t.int32)
+            self.episode = z(t.int32)
         e = self.eng
         ra, ta, fa, wa = self.small_a
         p = lambda x: None if x is None else x.data_ptr()
@@ -97,7 +111,11 @@ class DualStepVectorEnv:
         if seeds is None and seed is not None:
             seeds = range(int(seed), int(seed) + self.num_envs)
         obs, mask = self.eng.reset(seeds=seeds)
-        return obs, {"action_mask": mask, "to_play": obs[:, 294]}
+        info = {"action_mask": mask, "to_play": obs[:, 294]}
+        if self.pool is not None:  # every table starts an episode: draw its opponent
+            self.pool.draw(self.opp_group, self.episode, None, self.eng.table0)
+            info["opponent_index"] = self.opp_group
+        return obs, info
 
     def dual_step(self, actions):
         """wrappers/dual_step_native.py:90-193 on every table: spl_step (agent) -> opponent
@@ -113,6 +131,8 @@ class DualStepVectorEnv:
                policy_seed=self.policy_seed, ply=self._ply)
         if device_opp:
             opp = self.opp_actions
+        elif self.pool is not None:
+            opp = self.pool.act(e.obs, e.mask, self.opp_group, out=self.opp_actions)
         else:
             opp = self.opponent(e.obs, e.mask)
             if not (isinstance(opp, torch.Tensor) and opp.dtype == torch.int32 and opp.is_contiguous()
@@ -128,9 +148,14 @@ class DualStepVectorEnv:
             io = self._io
             io.opp_obs = self.opp_obs.data_ptr() if self.want_opp_obs else None
             _native.check(lib, lib.spl_dual_finish(self.num_envs, ctypes.byref(io), stream))
-        info = DualInfo({"action_mask": e.mask, "to_play": e.obs[:, 294], "final_observation": e.final_obs,
-                         "opponent_action": opp, "game_ended_on": self.game_ended_on, "agent_step_reward": ra},
-                        self.info_flags)
+        base = {"action_mask": e.mask, "to_play": e.obs[:, 294], "final_observation": e.final_obs,
+                "opponent_action": opp, "game_ended_on": self.game_ended_on, "agent_step_reward": ra}
+        if self.pool is not None:
+            # the opponent that played this step's episode, then the next episode's for re-dealt tables
+            base["episode_opponent_index"] = self.opp_group.clone()
+            self.pool.draw(self.opp_group, self.episode, self.done, self.eng.table0)
+            base["opponent_index"] = self.opp_group
+        info = DualInfo(base, self.info_flags)
         return e.obs, self.agent_reward, self.opp_obs, self.opp_reward, self.done, info
 
     def close(self):

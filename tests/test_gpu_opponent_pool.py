@@ -1,0 +1,164 @@
+"""The batched opponent pool of config-5 self-play (ppo_splendor.py:137-143 opponent_supplier,
+:366-370 snapshot pool): per-table networks in one grouped launch (spl_policy_act_grouped), the
+per-table opponent draw (spl_dual_draw_opponents), and DualStepVectorEnv with an OpponentPool against
+per-env DualStepNativeWrapper loops whose opponent_supplier makes the same draws (a host Philox
+restatement below) — wrappers/dual_step_native.py:45-79, 90-193."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+M32 = 0xFFFFFFFF
+
+
+def philox4x32(ctr, key):
+    """Philox4x32-10 (csrc/spl_rng.h) on Python ints: ctr 4 words, key 2 words."""
+    c0, c1, c2, c3 = ctr
+    k0, k1 = key
+    for _ in range(10):
+        p0, p1 = 0xD2511F53 * c0, 0xCD9E8D57 * c2
+        c0, c1, c2, c3 = ((p1 >> 32) ^ c1 ^ k0) & M32, p1 & M32, ((p0 >> 32) ^ c3 ^ k1) & M32, p0 & M32
+        k0, k1 = (k0 + 0x9E3779B9) & M32, (k1 + 0xBB67AE85) & M32
+    return c0, c1, c2, c3
+
+
+def host_draw(seed, table, episode, pool_slots, p_current):
+    """The group spl_dual_draw_opponents gives `table` for its `episode`-th draw."""
+    r = philox4x32((table & M32, table >> 32, episode & M32, 0x6F70706F), (seed & M32, seed >> 32))
+    u = np.float32(r[0] >> 8) * np.float32(1.0 / 16777216.0)
+    if not pool_slots or u < np.float32(p_current):
+        return 0
+    return pool_slots[(r[1] * len(pool_slots)) >> 32]
+
+
+def models(k, seed=0):
+    import torch
+    from splendor_gym.policy import ActorCritic
+    torch.manual_seed(seed)
+    return [ActorCritic().cuda().eval() for _ in range(k)]
+
+
+def states(n, seed=5, plies=10):
+    import torch
+    from splendor_gym.device import Engine
+    e = Engine(n, 2)
+    e.reset(seeds=range(seed, seed + n))
+    a = torch.zeros(n, dtype=torch.int32, device=e.device)
+    e.sample_uniform(out=a, seed=seed, ply=0)
+    for k in range(plies):
+        e.step(a, next_actions=a, policy_seed=seed, ply=k + 1)
+    return e.obs.clone(), e.mask.clone()
+
+
+def test_grouped_act_equals_each_network():
+    """Tables spread over 4 networks (current + 3 snapshots) by an arbitrary per-table index: every
+    table's action equals that network's own FusedActorCritic greedy action, bit for bit."""
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic, OpponentPool
+    ms = models(4, seed=3)
+    pool = OpponentPool(ms[0], pool_size=3)
+    for m in ms[1:]:
+        pool.add_snapshot(m)
+    assert pool.pool == [1, 2, 3]
+    n = 5000
+    obs, mask = states(n)
+    g = torch.randint(0, 4, (n,), dtype=torch.int32, device=obs.device)
+    g[:700] = 2  # a large group, a partial workgroup at the end of each group
+    act = pool.act(obs, mask, g)
+    for i, m in enumerate(ms):
+        want = FusedActorCritic(m, with_critic=False).greedy(obs, mask)
+        sel = g == i
+        assert torch.equal(act[sel], want[sel]), i
+    g2 = torch.full((n,), -1, dtype=torch.int32, device=obs.device)  # outside the images: untouched
+    out = torch.full((n,), 77, dtype=torch.int32, device=obs.device)
+    pool.act(obs, mask, g2, out=out)
+    assert (out == 77).all()
+
+
+def test_draw_matches_host_and_statistics():
+    import torch
+    from splendor_gym.fused_policy import OpponentPool
+    (m,) = models(1)
+    pool = OpponentPool(m, pool_size=12, p_current=0.25, seed=77)
+    n = 1 << 16
+    grp = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ep = torch.zeros(n, dtype=torch.int32, device="cuda")
+    pool.draw(grp, ep, table0=1000)
+    assert (grp == 0).all()  # empty pool: always the current policy
+    for _ in range(14):
+        pool.add_snapshot()  # ring of 14 snapshot slots, pool keeps the last 12
+    assert len(pool.pool) == 12 and pool.pool == list(range(3, 15))
+    draw = (torch.arange(n, device="cuda") % 3 == 0).to(torch.uint8)
+    pool.draw(grp, ep, draw, table0=1000)
+    g = grp.cpu().numpy()
+    e = ep.cpu().numpy()
+    assert (e == 1 + (np.arange(n) % 3 == 0)).all()
+    sel = np.arange(n) % 3 == 0
+    frac_cur = (g[sel] == 0).mean()
+    assert abs(frac_cur - 0.25) < 4 * np.sqrt(0.25 * 0.75 / sel.sum())
+    counts = np.bincount(g[sel], minlength=15)[3:15]
+    assert counts.min() > 0.6 * counts.mean()
+    for t in list(range(0, 60, 3)) + [n - 4]:
+        assert g[t] == host_draw(77, 1000 + t, 1, pool.pool, 0.25), t
+    assert (g[~sel] == 0).all()
+
+
+def test_pool_self_play_matches_per_env_wrappers():
+    """DualStepVectorEnv(opponent=OpponentPool) == per-env DualStepNativeWrapper loops whose
+    opponent_supplier draws the same network for each episode (host_draw), each network played by
+    its own single-table FusedActorCritic greedy call, with the PPO loop's reset after done."""
+    import torch
+    from splendor_gym.envs import SplendorEnv
+    from splendor_gym.fused_policy import FusedActorCritic, OpponentPool
+    from splendor_gym.selfplay import DualStepVectorEnv
+    from splendor_gym.wrappers import DualStepNativeWrapper
+    ms = models(3, seed=11)
+    pool = OpponentPool(ms[0], pool_size=2, p_current=0.4, seed=5)
+    pool.add_snapshot(ms[1])
+    pool.add_snapshot(ms[2])
+    fused = {0: FusedActorCritic(ms[0], with_critic=False), 1: FusedActorCritic(ms[1], with_critic=False),
+             2: FusedActorCritic(ms[2], with_critic=False)}
+    n, steps, seed = 8, 140, 300
+
+    def greedy_of(net):
+        def policy(obs, info):
+            o = torch.as_tensor(obs, dtype=torch.int32, device="cuda").reshape(1, 297).contiguous()
+            k = torch.as_tensor(info["action_mask"], dtype=torch.int8, device="cuda").reshape(1, 45).contiguous()
+            return int(fused[net].greedy(o, k)[0].item())
+        return policy
+
+    def supplier_for(i):
+        count = [0]
+
+        def supplier():
+            g = host_draw(5, i, count[0], pool.pool, 0.4)
+            count[0] += 1
+            supplier.groups.append(g)
+            return greedy_of(g)
+        supplier.groups = []
+        return supplier
+
+    vec = DualStepVectorEnv(n, opponent=pool)
+    obs_v, info_v = vec.reset(seed=seed)
+    sups = [supplier_for(i) for i in range(n)]
+    envs = [DualStepNativeWrapper(SplendorEnv(), opponent_policy=None, opponent_supplier=sups[i], random_starts=True)
+            for i in range(n)]
+    per = [w.reset(seed=seed + i) for i, w in enumerate(envs)]
+    assert info_v["opponent_index"].cpu().tolist() == [s.groups[0] for s in sups]
+    ended = 0
+    for k in range(steps):
+        acts = [int(np.flatnonzero(p[1]["action_mask"])[-1]) if p[1]["action_mask"].any() else 0 for p in per]
+        ao, ar, oo, orr, done, info_v = vec.dual_step(torch.tensor(acts, dtype=torch.int32, device=vec.device))
+        for i, w in enumerate(envs):
+            a_obs, a_rew, o_obs, o_rew, d, inf = w.dual_step(acts[i])
+            assert bool(done[i]) == bool(d), (k, i)
+            assert float(ar[i]) == pytest.approx(a_rew) and float(orr[i]) == pytest.approx(o_rew), (k, i)
+            if d:
+                ended += 1
+                per[i] = w.reset()
+            else:
+                per[i] = (a_obs, inf)
+            assert np.array_equal(ao[i].cpu().numpy(), per[i][0]), (k, i)
+        assert info_v["opponent_index"].cpu().tolist() == [s.groups[-1] for s in sups], k
+    assert ended >= n
+    assert len({g for s in sups for g in s.groups}) == 3  # all three networks played

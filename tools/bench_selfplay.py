@@ -33,11 +33,15 @@ def main():
                     help="fused: spl_policy_act (fp32 MFMA kernel, bf16 with --bf16) for agent and opponent; "
                          "torch: the nn.Module")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--opponent", choices=["pool", "frozen"], default="pool",
+                    help="pool: the reference's opponent_supplier (current policy p=0.25, else one of 12 frozen "
+                         "snapshots, drawn per episode; fused fp32 grouped kernel); frozen: one frozen greedy actor")
+    ap.add_argument("--pool-size", type=int, default=12)
     args = ap.parse_args()
 
     import torch
     from splendor_gym.parallel import barrier, init_distributed, local_device, max_over_ranks
-    from splendor_gym.fused_policy import FusedActorCritic
+    from splendor_gym.fused_policy import FusedActorCritic, OpponentPool
     from splendor_gym.policy import ActorCritic, greedy_opponent_from
     from splendor_gym.selfplay import DualStepVectorEnv
 
@@ -52,7 +56,14 @@ def main():
     if fused:
         prec = "bf16" if args.bf16 else "fp32"
         agent_k = FusedActorCritic(agent, precision=prec)
-        opponent = FusedActorCritic(opp_model, with_critic=False, precision=prec).opponent()
+        if args.opponent == "pool":
+            if args.bf16:
+                raise SystemExit("--opponent pool is fp32 (the grouped kernel); use --opponent frozen with --bf16")
+            opponent = OpponentPool(agent, pool_size=args.pool_size, p_current=0.25, seed=99)
+            for _ in range(args.pool_size):  # distinct random-init snapshots stand in for trained ones
+                opponent.add_snapshot(ActorCritic().to(dev).eval())
+        else:
+            opponent = FusedActorCritic(opp_model, with_critic=False, precision=prec).opponent()
     else:
         opponent = greedy_opponent_from(opp_model)
     env = DualStepVectorEnv(N, device=dev, opponent=opponent, table0=rank * N, opponent_obs=False)
@@ -113,7 +124,10 @@ def main():
             "ms_per_dual_step": round(full / args.iters * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "dtype": "bf16" if args.bf16 else "fp32", "data": "synthetic: seeded deals, random-init ActorCritic",
             "config": {"workload": "PPO rollout step: ActorCritic.get_action_and_value + DualStepVectorEnv.dual_step "
-                                   "(greedy frozen-ActorCritic opponent, reset after done)",
+                                   + ("(opponent pool: current policy p=0.25 else one of "
+                                      f"{args.pool_size} frozen snapshots per episode, greedy; reset after done)"
+                                      if fused and args.opponent == "pool" else
+                                      "(greedy frozen-ActorCritic opponent, reset after done)"),
                        "tables_per_gpu": N, "players": 2, "launch": "hipGraph replay" if graph is not None else "eager",
                        "actor": (f"spl_policy_act (fused, {'bf16' if args.bf16 else 'fp32'} MFMA)" if fused
                                  else "torch nn.Module" + (" (bf16 autocast)" if args.bf16 else ""))},
