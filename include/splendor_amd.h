@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 2
+#define SPL_ABI_VERSION 3
 
 /* ---- per-table flag bits (uint8) --------------------------------------------------- */
 #define SPL_F_ILLEGAL 0x01        /* info["illegal_action"]      envs/splendor_env.py:64-66 */
@@ -53,8 +53,8 @@ extern "C" {
 #define SPL_F_AFTER_TERMINAL 0x08 /* reference raises RuntimeError envs/splendor_env.py:53-54 */
 #define SPL_F_OOB 0x10            /* reference raises ValueError  envs/splendor_env.py:62-63 */
 #define SPL_F_RESET 0x20          /* autoreset: obs/mask describe the freshly dealt table   */
-#define SPL_F_RNG_LIMIT 0x40      /* a deal needed more MT outputs than the device streams; */
-                                  /* never observed, reported instead of guessed */
+#define SPL_F_RNG_LIMIT 0x40      /* reserved (ABI 2 raised it when a deal or token return   */
+                                  /* outran the MT stream; ABI 3 continues the stream instead) */
 
 /* ---- device policies for next_actions (scripts/eval_suite.py opponents) --------------- */
 #define SPL_POLICY_UNIFORM 0         /* uniform over legal (wrappers/selfplay.py:66-73 random_opponent) */
@@ -177,6 +177,12 @@ int spl_table_download(spl_ctx_t *ctx, spl_arena_t *arena, int32_t first, int32_
                        spl_table_t *host, void *stream);
 int spl_table_upload(spl_ctx_t *ctx, spl_arena_t *arena, int32_t first, int32_t count,
                      const spl_table_t *host, void *stream);
+
+/* TEST HOOK: how many MT19937 outputs a deal or token return takes from the register-only stream
+ * before the full-state continuation takes over (default and maximum 454, the stream's reach;
+ * process-wide, current device).  Results are identical for every value: the parity tests lower it
+ * to drive every deal and token return through the continuation. */
+int spl_debug_set_stream_limit(int outputs);
 
 /* Copy of the token-return RNG table (spl_ctx_create builds it on device), for tests.
  * Returns the number of uint32 words (4 per entry) when out == NULL. */

@@ -126,6 +126,11 @@ __device__ uint64_t *g_wsclk;   // [workgroup][4]: s_memtime / s_memrealtime at 
     do {             \
     } while (0)
 #endif
+// Outputs a lane takes from the register-only MTStream before a LaneMT continuation takes over
+// (MTStream::kMaxOut; lowered only by the test hook spl_debug_set_stream_limit, so the parity tests
+// can drive every deal and token return through the continuation path).
+__device__ int g_stream_limit = MTStream::kMaxOut;
+
 // Per-lane deal scratch in LDS: an odd number of dwords, so lanes at the same Fisher-Yates
 // position (the common case: lanes decrement their index in step) hit 64 different banks.
 #ifndef SPL_SCRATCH_STRIDE
@@ -443,26 +448,35 @@ __device__ __forceinline__ int non_gold_kinds(const Pl &p) {
 
 // engine/rules.py:150-185 auto_return_tokens on the full CPython MT stream (rare: seeds
 // outside the precomputed table, or a table entry that ran out of draws).
-__device__ __forceinline__ void token_return_mt(Pl &p, int bank[6], int remaining, uint64_t seed, uint32_t &flags) {
+__device__ __forceinline__ void token_return_mt(Pl &p, int bank[6], int remaining, uint64_t seed, uint32_t *mtx) {
     MTStream ms;
     ms.init(seed);
     bool done = false;
-    for (int j = 0;; ++j) {
+    auto draw = [&](uint32_t y) {  // rng.choice(choices) on output y
         const int nch = non_gold_kinds(p);
-        done = done || remaining <= 0 || nch == 0;
-        if (!__any(!done)) break;
-        if (j >= MTStream::kMaxOut) {
-            if (!done) flags |= SPL_F_RNG_LIMIT;
-            break;
+        const int kb = bit_length((uint32_t)nch);
+        const int r = (int)(y >> (32 - kb));
+        if (r < nch) {  // accepted
+            return_one(p, bank, r);
+            remaining -= 1;
         }
+    };
+    const int limit = min(g_stream_limit, MTStream::kMaxOut);
+    for (int j = 0;; ++j) {
+        done = done || remaining <= 0 || non_gold_kinds(p) == 0;
+        if (!__any(!done)) break;
+        if (j >= limit) break;  // lanes still returning continue below
         const uint32_t y = ms.next(j);
-        if (!done) {
-            const int kb = bit_length((uint32_t)nch);
-            const int r = (int)(y >> (32 - kb));
-            if (r < nch) {  // rng.choice(choices) accepted
-                return_one(p, bank, r);
-                remaining -= 1;
-            }
+        if (!done) draw(y);
+    }
+    // Continuation past the streamed outputs (crafted states with hundreds of tokens to return):
+    // one lane at a time, its full MT19937 state in the LDS region mtx, from output kMaxOut on.
+    for (uint64_t slow = __ballot(!done); slow; slow &= slow - 1) {
+        if (lane_id() == __ffsll((unsigned long long)slow) - 1) {
+            LaneMT mt{mtx, 0};
+            mt.init(seed);
+            mt.start_at(limit);
+            while (remaining > 0 && non_gold_kinds(p) > 0) draw(mt.next());
         }
     }
     if (remaining > 0 && p.tok[5] > 0) {
@@ -559,7 +573,7 @@ __device__ __forceinline__ bool token_return_lut(Pl &p, int bank[6], int remaini
 // engine/rules.py:188-193 _enforce_token_limit -> :150-185 auto_return_tokens.  `pre_key` /
 // `pre_e` are the prefetched table entry (predict_lut_key); any other key is loaded here.
 __device__ __forceinline__ void enforce_token_limit(Pl &p, int bank[6], int turn_count, int to_play,
-                                                    const uint4 *lut, int pre_key, uint4 pre_e, uint32_t &flags) {
+                                                    const uint4 *lut, int pre_key, uint4 pre_e, uint32_t *mtx) {
     int total = 0, bank_total = 0;
 #pragma unroll
     for (int c = 0; c < 6; ++c) total += p.tok[c];
@@ -586,7 +600,7 @@ __device__ __forceinline__ void enforce_token_limit(Pl &p, int bank[6], int turn
     if (need_mt) {
         const uint64_t seed = ((uint64_t)turn_count * 1315423911ull) ^ ((uint64_t)to_play * 2654435761ull) ^
                               ((uint64_t)total * 97531ull) ^ ((uint64_t)bank_total * 31337ull);
-        token_return_mt(p, bank, total - 10, seed, flags);
+        token_return_mt(p, bank, total - 10, seed, mtx);
     }
 }
 
@@ -652,7 +666,7 @@ __device__ __forceinline__ bool is_terminal(const uint32_t *sw) {
 // engine/rules.py:196-287 apply_action on the current player (action known legal)
 template <int P>
 __device__ __forceinline__ void apply_action(Tab<P> &T, int a, uint32_t top, const Consts &L, const uint4 *lut,
-                                             int pre_key, uint4 pre_e, uint32_t &flags) {
+                                             int pre_key, uint4 pre_e, uint32_t *mtx) {
     uint32_t *sw = T.sw;
     const int tp = get_to_play(sw);
     uint32_t w[4];
@@ -710,7 +724,7 @@ __device__ __forceinline__ void apply_action(Tab<P> &T, int a, uint32_t top, con
         pay_for_card(p, bank, card_rec(L, card));
     }
     if (!abl(ABL_NOBLE)) grant_noble(sw, p, tp, L);                         // :260
-    if (!abl(ABL_TOKLIM)) enforce_token_limit(p, bank, get_turn(sw), tp, lut, pre_key, pre_e, flags);  // :261
+    if (!abl(ABL_TOKLIM)) enforce_token_limit(p, bank, get_turn(sw), tp, lut, pre_key, pre_e, mtx);  // :261
     uint32_t misc = sw[SW_MISC];
     if (p.pres >= 15) misc |= ST_GAME_OVER;                                 // :264-265
     pack_pl(p, w);
@@ -975,26 +989,22 @@ struct Deal {
 };
 __device__ __forceinline__ Deal empty_deal() { return Deal{{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}, 0xFFFFFFFFu, 0xFFu}; }
 
-__device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec, uint8_t *scr, Deal &out) {
+__device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec, uint8_t *scr, Deal &out,
+                                              uint32_t *mtx) {
     for (int i = 0; i < 100; ++i) scr[i] = (uint8_t)(i < 90 ? i : i - 90);
     MTStream ms;
     ms.init(seed);
     int d = 0, base = 0, i = 39;
     uint32_t flags = 0;
-    uint32_t y = ms.next(0);
-    for (int j = 0;; ++j) {
-        if (!__any(d < 4)) break;
-        if (j >= MTStream::kMaxOut) {
-            if (d < 4) flags |= SPL_F_RNG_LIMIT;
-            break;
-        }
-        // _randbelow(i + 1) on output j; a rejected draw (or a finished lane) swaps x[i] with itself
+    // _randbelow(i + 1) on output y; a rejected draw (or a finished lane, or `on` false) swaps x[i]
+    // with itself.  The caller's LDS reads of the two bytes overlap the next output's computation.
+    auto shuffle_step = [&](uint32_t y, bool on, auto &&between) {
         const int n = i + 1;
         const int r = (int)(y >> (32 - bit_length((uint32_t)n)));
-        const bool acc = d < 4 && r < n;
+        const bool acc = on && d < 4 && r < n;
         const int ai = base + i, ar = base + (acc ? r : i);
         const uint8_t xi = scr[ai], xr = scr[ar];
-        if (j + 1 < MTStream::kMaxOut) y = ms.next(j + 1);  // overlaps the LDS reads
+        between();
         scr[ai] = xr;
         scr[ar] = xi;
         const int i2 = acc ? i - 1 : i;
@@ -1002,6 +1012,25 @@ __device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec
         d += adv ? 1 : 0;
         base = adv ? (d == 1 ? 40 : (d == 2 ? 70 : 90)) : base;
         i = adv ? (d == 1 ? 29 : (d == 2 ? 19 : 9)) : i2;
+    };
+    const int limit = min(g_stream_limit, MTStream::kMaxOut);
+    uint32_t y = ms.next(0);
+    for (int j = 0;; ++j) {
+        if (!__any(d < 4)) break;
+        if (j >= limit) break;  // lanes still shuffling continue below
+        shuffle_step(y, true, [&] {
+            if (j + 1 < limit) y = ms.next(j + 1);
+        });
+    }
+    // Continuation past the streamed outputs (never met in natural play): one lane at
+    // a time, its full MT19937 state in the LDS region mtx, from output kMaxOut on.
+    for (uint64_t slow = __ballot(d < 4); slow; slow &= slow - 1) {
+        if (lane_id() == __ffsll((unsigned long long)slow) - 1) {
+            LaneMT mt{mtx, 0};
+            mt.init(seed);
+            mt.start_at(limit);
+            while (d < 4) shuffle_step(mt.next(), true, [] {});
+        }
     }
     // deck bytes (list order; the 4 dealt cards per tier sit past deck_len)
     const uint32_t *s1 = reinterpret_cast<const uint32_t *>(scr);  // 4-byte aligned scratch
@@ -1101,14 +1130,14 @@ __device__ __forceinline__ void store_pool(const KArena &A, int t, const Deal &d
 // A table never reset with a seed has no stream: it deals engine seed 0 (documented in
 // splendor_amd.h) and its record stays unseeded.
 template <int P>
-__device__ __forceinline__ uint32_t deal_next(const KArena &A, int t, int slot, uint8_t *scr, Deal &d) {
+__device__ __forceinline__ uint32_t deal_next(const KArena &A, int t, int slot, uint8_t *scr, Deal &d, uint32_t *mtx) {
     Pcg64 g = load_pcg(A, t);
     uint32_t seed = 0u;
     if (g.valid()) {
         seed = g.engine_seed();
         store_pcg(A, t, g);
     }
-    return deal_into(seed, P, slot_rec(A, t, slot), scr, d);
+    return deal_into(seed, P, slot_rec(A, t, slot), scr, d, mtx);
 }
 
 template <int P>
@@ -1280,7 +1309,8 @@ struct StepOut {
 // so "any legal move?" and mask[action] need no re-evaluation.
 template <int P>
 __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepPre &pre, bool valid, const Consts &L,
-                                              const KTables &Tb, bool known = false, uint64_t known_mask = 0ull) {
+                                              const KTables &Tb, uint32_t *mtx, bool known = false,
+                                              uint64_t known_mask = 0ull) {
     StepOut o{0u, 0.0f, false, 0ull};
     bool want_mask = false;
     if (valid) {
@@ -1316,7 +1346,7 @@ __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepP
                 want_mask = true;
             } else {
                 STAMP(2);
-                if (!abl(ABL_APPLY)) apply_action(T, action, pre.top, L, Tb.lut, pre.key, pre.e, o.flags);  // :68
+                if (!abl(ABL_APPLY)) apply_action(T, action, pre.top, L, Tb.lut, pre.key, pre.e, mtx);  // :68
                 STAMP(3);
                 o.term = is_terminal(T.sw);                       // :70
                 if (o.term) {                                     // :71-80
@@ -1351,12 +1381,12 @@ __device__ __forceinline__ float final_reward_p0(const Tab<P> &T) {
 // planes); returns true in that case.
 template <int P>
 __device__ __forceinline__ bool flip_to_pool(Tab<P> &T, const KArena &A, int t, Deal &pool, uint8_t *scr,
-                                             uint32_t &flags) {
+                                             uint32_t *mtx, uint32_t &flags) {
     constexpr int kPools = kSlotRecords - 1;
     const uint32_t misc = T.sw[SW_MISC];
     const int a = active_of(misc), pend = pend_of(misc);
     const int nxt = (a + 1) % kSlotRecords;
-    if (pend >= kPools) flags |= deal_next<P>(A, t, nxt, scr, pool);
+    if (pend >= kPools) flags |= deal_next<P>(A, t, nxt, scr, pool, mtx);
     const int pend2 = pend >= kPools ? kPools : pend + 1;  // the old live record is free now
     fresh_state(T, ring_bits(nxt, pend2), pool);
     if (pend2 < kPools) pool = rec_deal(slot_rec(A, t, (nxt + 1) % kSlotRecords));
@@ -1368,12 +1398,12 @@ __device__ __forceinline__ bool flip_to_pool(Tab<P> &T, const KArena &A, int t, 
 // stream).  When that record is the next pool, its words go to `pool` (`pool_dirty`).  Returns
 // the new status word.
 template <int P>
-__device__ __forceinline__ uint32_t refill_table(const KArena &A, int t, uint32_t misc, uint8_t *scr, Deal &pool,
-                                                 bool &pool_dirty) {
+__device__ __forceinline__ uint32_t refill_table(const KArena &A, int t, uint32_t misc, uint8_t *scr, uint32_t *mtx,
+                                                 Deal &pool, bool &pool_dirty) {
     const int pend = pend_of(misc);
     const int slot = (active_of(misc) + kSlotRecords - pend) % kSlotRecords;
     Deal d;
-    deal_next<P>(A, t, slot, scr, d);
+    deal_next<P>(A, t, slot, scr, d, mtx);
     if (pend == kSlotRecords - 1) {
         pool = d;
         pool_dirty = true;
@@ -1384,8 +1414,8 @@ __device__ __forceinline__ uint32_t refill_table(const KArena &A, int t, uint32_
 // same-step autoreset of a terminal table; `pool_dirty` is set when the pool planes changed
 template <int P>
 __device__ __forceinline__ void autoreset_table(Tab<P> &T, const KArena &A, int t, Deal &pool, uint8_t *scr,
-                                                StepOut &o, bool &pool_dirty) {
-    pool_dirty |= flip_to_pool<P>(T, A, t, pool, scr, o.flags);
+                                                uint32_t *mtx, StepOut &o, bool &pool_dirty) {
+    pool_dirty |= flip_to_pool<P>(T, A, t, pool, scr, mtx, o.flags);
     o.flags |= SPL_F_RESET;
     o.mask = kFreshDealMask;
 }
@@ -1432,7 +1462,9 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     wave_lds_sync();
     STAMP(1);
 
-    StepOut o = step_rules(T, action, pre, valid, L, Tb);
+    // LDS for a token-return continuation (LaneMT): the observation rows past the deal scratch
+    uint32_t *const mtx = reinterpret_cast<uint32_t *>(&L.rows[64 * kScratchStride]);
+    StepOut o = step_rules(T, action, pre, valid, L, Tb, mtx);
     // autoreset 2: a table terminal on entry is re-dealt without a move (dual-step opponent phase)
     const bool entry_reset = valid && S.autoreset == 2 && (o.flags & SPL_F_AFTER_TERMINAL);
     if (entry_reset) o.flags = 0u;
@@ -1450,7 +1482,7 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     STAMP(5);
     bool pool_dirty = false;
     if (ended && S.autoreset && !abl(ABL_RESET))
-        autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], o, pool_dirty);
+        autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], mtx, o, pool_dirty);
     STAMP(6);
     wave_lds_sync();  // deal scratch (rows) free again
 
@@ -1533,6 +1565,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
     __shared__ BlockLDS L;
     const RefillSlots rs = refill_slots(K, S.autoreset ? refill : 0);
     const int lane = lane_id();
+    uint32_t *const deal_mtx = reinterpret_cast<uint32_t *>(&L.rows[64 * kScratchStride]);  // LaneMT continuation
     const int t0 = blockIdx.x * 64;
     const int t = t0 + lane;
     const bool valid = t < A.n;
@@ -1566,14 +1599,16 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
         const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
         wave_lds_sync();  // previous step's LDS reads done (rows, mask, frows)
         RSTAMP(0, k);
-        StepOut o = step_rules(T, action, pre, valid, L, Tb, k > 0, cur_mask);
+        // token-return continuation (LaneMT) in frows: rows still hold the last step's obs tail
+        StepOut o = step_rules(T, action, pre, valid, L, Tb, reinterpret_cast<uint32_t *>(L.frows), k > 0, cur_mask);
         RSTAMP(1, k);
         if (obs_tail) store_obs_range(L.rows, obs_tail, kObsSplit, kObsBlockWords);
         obs_tail = nullptr;
         if (rs.due(k)) {  // fused pool refill (wave-uniform)
             wave_lds_sync();  // the tail's LDS reads are done: the rows serve as deal scratch
             if (valid && pend_of(T.sw[SW_MISC]) > 0)
-                T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], &L.rows[lane * kScratchStride], pool, pool_dirty);
+                T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], &L.rows[lane * kScratchStride], deal_mtx, pool,
+                                                pool_dirty);
         }
         RSTAMP(2, k);
         const int8_t wnr = (int8_t)get_winner(T.sw);
@@ -1584,7 +1619,8 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
             if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], final_reward_p0(T));
             if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
         }
-        if (valid && o.term && S.autoreset) autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], o, pool_dirty);
+        if (valid && o.term && S.autoreset)
+            autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], deal_mtx, o, pool_dirty);
         wave_lds_sync();
         if (!abl(ABL_ENCODE)) encode_row(T, L.rows, L);
         L.mask[lane] = o.mask;
@@ -1665,7 +1701,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
 template <int P>
 struct __align__(16) WsLDS : Consts {
     static constexpr int kW = SW_COUNT + 4 * P;  // state words per table
-    static constexpr int kTerm = P == 3 ? 8 : 16;  // terminal states listed per step
+    static constexpr int kTerm = P == 3 ? 8 : (P == 4 ? 15 : 16);  // terminal states listed per step
     static constexpr int kScrStride = P == 2 ? kScratchStride : 100;
     static constexpr bool kScrInSlot = P == 4;
     static_assert(!kScrInSlot || kW * 64 * 4 >= 64 * kScrStride, "scratch must fit the state slot");
@@ -1677,9 +1713,12 @@ struct __align__(16) WsLDS : Consts {
     uint32_t mbits[96];
     uint8_t rows[64 * kObsDim];
     uint8_t scr[kScrInSlot ? 16 : 64 * kScrStride];  // the rules wave's deal scratch (P < 4)
+    uint32_t mtx[kScrInSlot ? 624 : 0];               // deal continuation (LaneMT) at P = 4 (none below)
     __device__ __forceinline__ uint8_t *scratch(int b, int lane) {
         return kScrInSlot ? reinterpret_cast<uint8_t *>(&st[b][0][0]) + lane * kScrStride : &scr[lane * kScrStride];
     }
+    // LDS for a deal's LaneMT continuation: this step's free state slot, unless it holds the scratch
+    __device__ __forceinline__ uint32_t *deal_mtx(int b) { return kScrInSlot ? mtx : &st[b][0][0]; }
 };
 static_assert(sizeof(WsLDS<2>) <= 40960 && sizeof(WsLDS<3>) <= 40960 && sizeof(WsLDS<4>) <= 40960,
               "k_rollout_ws needs four workgroups per CU");
@@ -1772,10 +1811,11 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
             const int b = k & 1;
             const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
             WSSTAMP(0, k);
-            StepOut o = step_rules(T, action, pre, valid, L, Tb, k > 0, cur_mask);
+            // token-return continuation (LaneMT) in this step's free state slot
+            StepOut o = step_rules(T, action, pre, valid, L, Tb, &L.st[b][0][0], k > 0, cur_mask);
             WSSTAMP(1, k);
             if (rs.due(k) && valid && pend_of(T.sw[SW_MISC]) > 0)  // fused pool refill
-                T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], L.scratch(b, lane), pool, pool_dirty);
+                T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], L.scratch(b, lane), L.deal_mtx(b), pool, pool_dirty);
             const int8_t wnr = (int8_t)get_winner(T.sw);
             const bool fin_me = valid && o.term && want_final;
             const uint64_t fin_all = __ballot(fin_me);
@@ -1789,7 +1829,8 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
                 }
             }
             const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;  // per termination, as k_step
-            if (valid && o.term && S.autoreset) autoreset_table(T, A, t, pool, L.scratch(b, lane), o, pool_dirty);
+            if (valid && o.term && S.autoreset)
+                autoreset_table(T, A, t, pool, L.scratch(b, lane), L.deal_mtx(b), o, pool_dirty);
             L.small[b][lane] = pack_small(valid, o, wnr, valid && o.term, ep_add);  // stored by the output wave
             action = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
             cur_mask = o.mask;
@@ -1915,10 +1956,11 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
     wave_lds_sync();
     const bool doit = valid && (mask_in == nullptr || mask_in[t] != 0);
     uint8_t *scr = &L.rows[lane * kScratchStride];
+    uint32_t *const mtx = reinterpret_cast<uint32_t *>(&L.rows[64 * kScratchStride]);  // LaneMT continuation
     if (doit) {
         if (eseed_in) {  // engine/state.py:181-211 initial_state(P, seed) from an explicit engine seed
             Deal d0;     // no pool: a later reset() without a seed deals inline
-            deal_into(eseed_in[t], P, slot_rec(A, t, 0), scr, d0);
+            deal_into(eseed_in[t], P, slot_rec(A, t, 0), scr, d0, mtx);
             fresh_state(T, ring_bits(0, kSlotRecords - 1), d0);
         } else if (pcg_in) {  // reset(seed=...): restart this table's np_random stream, deal every record
             Pcg64 g;
@@ -1931,9 +1973,9 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
             // record 0 = this episode, records 1.. = the next episodes in stream order: the ring
             // starts full, so refills (one deal per table per call) only have to keep pace
             Deal d0, d;
-            deal_into(g.engine_seed(), P, slot_rec(A, t, 0), scr, d0);
+            deal_into(g.engine_seed(), P, slot_rec(A, t, 0), scr, d0, mtx);
             for (int r = 1; r < kSlotRecords; ++r) {
-                deal_into(g.engine_seed(), P, slot_rec(A, t, r), scr, d);
+                deal_into(g.engine_seed(), P, slot_rec(A, t, r), scr, d, mtx);
                 if (r == 1) store_pool(A, t, d);
             }
             store_pcg(A, t, g);
@@ -1941,7 +1983,7 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
         } else {       // reset() without a seed: continue the stream (pool deal)
             Deal d = pend_of(T.sw[SW_MISC]) < kSlotRecords - 1 ? load_pool(A, t) : empty_deal();
             uint32_t fl = 0;
-            if (flip_to_pool<P>(T, A, t, d, scr, fl)) store_pool(A, t, d);
+            if (flip_to_pool<P>(T, A, t, d, scr, mtx, fl)) store_pool(A, t, d);
         }
     }
     wave_lds_sync();
@@ -1972,7 +2014,8 @@ __global__ __launch_bounds__(64) void k_refill(KArena A) {
     if (pend_of(misc) == 0) return;
     Deal pool;
     bool pool_dirty = false;
-    A.planes[mi] = refill_table<P>(A, t, misc, &scr_all[lane_id() * kScratchStride], pool, pool_dirty);
+    A.planes[mi] = refill_table<P>(A, t, misc, &scr_all[lane_id() * kScratchStride],
+                                   reinterpret_cast<uint32_t *>(&scr_all[64 * kScratchStride]), pool, pool_dirty);
     if (pool_dirty) store_pool(A, t, pool);  // it was the next pool: words to the pool planes
 }
 
@@ -2227,6 +2270,12 @@ int spl_debug_set_rollout_stamps(void *buf) {
     return SPL_OK;
 }
 #endif
+
+int spl_debug_set_stream_limit(int outputs) {
+    if (outputs < 1 || outputs > MTStream::kMaxOut) return fail(SPL_E_ARG, "stream limit must be 1..454");
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stream_limit), &outputs, sizeof(outputs)));
+    return SPL_OK;
+}
 
 const char *spl_last_error(void) { return g_err.c_str(); }
 

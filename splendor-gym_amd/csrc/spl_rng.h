@@ -125,6 +125,65 @@ struct MTStream {
     }
 };
 
+// One lane's full CPython MT19937 state (624 words) in a caller-provided LDS region: the
+// continuation path of a lane that needs more outputs than MTStream streams (kMaxOut).  Run by ONE
+// lane at a time (the caller loops over the lanes that need it), so the region is shared by the
+// wave and no cross-lane operation is involved.  init() is a serial pass over the state; never
+// taken by natural play: crafted states with hundreds of tokens to return.
+struct LaneMT {
+    uint32_t *m;  // >= 624 words of LDS owned by the calling lane for the duration
+    int idx;
+
+    // random.seed(seed) for 0 <= seed < 2^64: init_genrand(19650218), then init_by_array with a
+    // key of 1 or 2 32-bit words (Modules/_randommodule.c)
+    __device__ void init(uint64_t seed) {
+        const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+        const int keylen = key[1] ? 2 : 1;
+        m[0] = 19650218u;
+        for (int i = 1; i < 624; ++i) m[i] = 1812433253u * (m[i - 1] ^ (m[i - 1] >> 30)) + (uint32_t)i;
+        int i = 1, j = 0;
+        for (int k = 624; k; --k) {
+            m[i] = (m[i] ^ ((m[i - 1] ^ (m[i - 1] >> 30)) * 1664525u)) + key[j] + (uint32_t)j;
+            ++i;
+            ++j;
+            if (i >= 624) {
+                m[0] = m[623];
+                i = 1;
+            }
+            if (j >= keylen) j = 0;
+        }
+        for (int k = 623; k; --k) {
+            m[i] = (m[i] ^ ((m[i - 1] ^ (m[i - 1] >> 30)) * 1566083941u)) - (uint32_t)i;
+            ++i;
+            if (i >= 624) {
+                m[0] = m[623];
+                i = 1;
+            }
+        }
+        m[0] = 0x80000000u;
+        idx = 624;
+    }
+
+    __device__ void twist() {
+        int k = 0;
+        for (; k < 624 - 397; ++k) m[k] = m[k + 397] ^ mt_tw(m[k], m[k + 1]);
+        for (; k < 623; ++k) m[k] = m[k - 227] ^ mt_tw(m[k], m[k + 1]);
+        m[623] = m[396] ^ mt_tw(m[623], m[0]);
+        idx = 0;
+    }
+
+    // continue the stream at output `j` (< 624) of the first block
+    __device__ void start_at(int j) {
+        twist();
+        idx = j;
+    }
+
+    __device__ uint32_t next() {
+        if (idx >= 624) twist();
+        return mt_temper(m[idx++]);
+    }
+};
+
 __device__ __forceinline__ int bit_length(uint32_t n) { return n ? 32 - __clz((int)n) : 0; }
 
 // ---- numpy PCG64 ------------------------------------------------------------------------

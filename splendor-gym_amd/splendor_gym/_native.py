@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 LIB_NAME = "libsplendor_amd.so"
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # per-table flag bits (include/splendor_amd.h)
 POLICY_UNIFORM, POLICY_GREEDY_V1, POLICY_BASIC_PRIORITY = 0, 1, 2  # SPL_POLICY_* (device next_actions)
@@ -90,6 +90,7 @@ SIGNATURES = {
     "spl_arena_init": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p], c_int32),
     "spl_reset": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
                   c_int32),
+    "spl_debug_set_stream_limit": ([c_int32], c_int32),
     "spl_deal": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
     "spl_step": ([c_void_p, ctypes.POINTER(ArenaDesc), ctypes.POINTER(StepArgs), c_void_p], c_int32),
     "spl_rollout": ([c_void_p, ctypes.POINTER(ArenaDesc), ctypes.POINTER(StepArgs), c_int32, c_int32, c_void_p],

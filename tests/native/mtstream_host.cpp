@@ -4,6 +4,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <initializer_list>
 #define __device__
 #define __host__
 #define __constant__ static constexpr
@@ -31,6 +32,26 @@ int main(int argc, char** argv) {
     for (int j = 0; j < spl::MTStream::kMaxOut; ++j) {
       uint32_t a = ms.next(j), b = orc_mt_next(&ref);
       if (a != b) { printf("seed %llu out %d: %u != %u\n", (unsigned long long)seed, j, a, b); bad++; break; }
+    }
+    // the full-state continuation (LaneMT) picks up at output kMaxOut and runs through later twists
+    static uint32_t region[624];
+    spl::LaneMT lm{region, 0};
+    lm.init(seed);
+    lm.start_at(spl::MTStream::kMaxOut);
+    for (int j = spl::MTStream::kMaxOut; j < 2600; ++j) {
+      uint32_t a = lm.next(), b = orc_mt_next(&ref);
+      if (a != b) { printf("LaneMT seed %llu out %d: %u != %u\n", (unsigned long long)seed, j, a, b); bad++; break; }
+    }
+    for (int start : {1, 3, 40, 227, 300}) {  // the test hook's lower limits: continue at any output
+      orc_mt_t r2; orc_mt_seed(&r2, seed);
+      for (int j = 0; j < start; ++j) orc_mt_next(&r2);
+      spl::LaneMT l2{region, 0};
+      l2.init(seed);
+      l2.start_at(start);
+      for (int j = start; j < 1300; ++j) {
+        uint32_t a = l2.next(), b = orc_mt_next(&r2);
+        if (a != b) { printf("LaneMT start %d seed %llu out %d\n", start, (unsigned long long)seed, j); bad++; break; }
+      }
     }
   }
   printf(bad ? "FAIL %d\n" : "OK\n", bad);

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_native.SIGNATURES), declared ^ set(_native.SIGNATURES)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.spl_abi_version() == _native.ABI_VERSION == 2
+    assert lib.spl_abi_version() == _native.ABI_VERSION == 3
 
 
 def test_abi_host_side_errors():
@@ -218,3 +218,21 @@ def test_fresh_deal_mask_constant():
     for P in (2, 3, 4):
         for s in range(0, 200000, 1999):
             assert o.legal(o.initial_state(P, s)) == want, (P, s)
+
+
+def test_oracle_under_address_and_undefined_sanitizers(tmp_path):
+    """the CPU restatement under ASan + UBSan (gcc -fsanitize=address,undefined,
+    no recovery): deals, long random rollouts and crafted extreme steps (tests/native/oracle_sanitize.c)."""
+    import numpy as np
+    from oracle.oracle import load_tables
+    cards, nobles = load_tables()
+    tables = tmp_path / "tables.bin"
+    tables.write_bytes(np.concatenate([cards.reshape(-1), nobles.reshape(-1)]).astype(np.int32).tobytes())
+    exe = tmp_path / "oracle_san"
+    subprocess.run(["gcc", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-fno-omit-frame-pointer", "-o", str(exe), os.path.join(REPO, "tests", "native", "oracle_sanitize.c"),
+                    os.path.join(REPO, "oracle", "splendor_oracle.c")], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([str(exe), str(tables)], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout[-2000:] + r.stderr[-4000:]
