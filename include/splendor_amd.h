@@ -184,6 +184,12 @@ int spl_table_upload(spl_ctx_t *ctx, spl_arena_t *arena, int32_t first, int32_t 
  * to drive every deal and token return through the continuation. */
 int spl_debug_set_stream_limit(int outputs);
 
+/* TEST HOOK of the bounds-check build (libsplendor_amd_checked.so, -DSPL_BOUNDS_CHECK): the OR of the
+ * invariant violations the kernels recorded (table / slot / deck / token-table / deal-scratch index,
+ * byte-packed counts out of range), cleared when `clear`.  Synchronises the device.  The product
+ * build returns SPL_E_ARG. */
+int spl_debug_bounds_flags(uint32_t *flags, int clear);
+
 /* Copy of the token-return RNG table (spl_ctx_create builds it on device), for tests.
  * Returns the number of uint32 words (4 per entry) when out == NULL. */
 int64_t spl_ctx_token_lut(spl_ctx_t *ctx, uint32_t *out, int64_t words);

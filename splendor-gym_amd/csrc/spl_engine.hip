@@ -76,6 +76,25 @@ constexpr int ABL_LEGAL_PRE = 1, ABL_APPLY = 2, ABL_LEGAL_POST = 4, ABL_FINAL = 
               ABL_LOAD = 2048, ABL_TOKLIM = 4096, ABL_NOBLE = 8192, ABL_DECK_GATHER = 16384, ABL_LUT_GATHER = 32768;
 __device__ __forceinline__ bool abl(int bit) { return (SPL_ABL & bit) != 0; }
 
+// Bounds-check build (-DSPL_BOUNDS_CHECK; libsplendor_amd_checked.so, tests/test_gpu_bounds_check.py):
+// index and range invariants are tested at run time and violations recorded as bits of
+// g_bounds_flags (an atomic OR: a checked run never faults, it reports).  The product build
+// compiles every check out.
+#ifdef SPL_BOUNDS_CHECK
+__device__ uint32_t g_bounds_flags;
+#define SPL_CHECK(cond, bit)                                              \
+    do {                                                                  \
+        if (!(cond)) atomicOr(&g_bounds_flags, (uint32_t)(bit));          \
+    } while (0)
+#else
+#define SPL_CHECK(cond, bit) \
+    do {                     \
+    } while (0)
+#endif
+enum : uint32_t {
+    BC_TABLE = 1, BC_SLOT = 2, BC_DECK = 4, BC_LUT = 8, BC_SCRATCH = 16, BC_BYTE = 32, BC_ROWS = 64, BC_CARD = 128
+};
+
 // Phase stamps for the diagnostic build only (-DSPL_STAMPS, tools/stamps.py): lane 0 of every
 // wave records s_memrealtime (100 MHz) at phase boundaries of k_step.  Never in the product build.
 #ifdef SPL_STAMPS
@@ -214,6 +233,11 @@ __device__ __forceinline__ Pl unpack_pl(const uint32_t w[4]) {
 }
 
 __device__ __forceinline__ void pack_pl(const Pl &p, uint32_t w[4]) {
+#ifdef SPL_BOUNDS_CHECK
+    for (int c = 0; c < 6; ++c) SPL_CHECK(p.tok[c] >= 0 && p.tok[c] <= 255, BC_BYTE);
+    for (int c = 0; c < 5; ++c) SPL_CHECK(p.bon[c] >= 0 && p.bon[c] <= 255, BC_BYTE);
+    SPL_CHECK(p.pres >= 0 && p.pres <= 255 && p.nres >= 0 && p.nres <= 3, BC_BYTE);
+#endif
     w[0] = (uint32_t)p.tok[0] | ((uint32_t)p.tok[1] << 8) | ((uint32_t)p.tok[2] << 16) | ((uint32_t)p.tok[3] << 24);
     w[1] = (uint32_t)p.tok[4] | ((uint32_t)p.tok[5] << 8) | ((uint32_t)p.bon[0] << 16) | ((uint32_t)p.bon[1] << 24);
     w[2] = (uint32_t)p.bon[2] | ((uint32_t)p.bon[3] << 8) | ((uint32_t)p.bon[4] << 16) | ((uint32_t)p.pres << 24);
@@ -248,6 +272,9 @@ __device__ __forceinline__ void get_bank(const uint32_t *sw, int bank[6]) {
 }
 
 __device__ __forceinline__ void put_bank(uint32_t *sw, const int bank[6]) {
+#ifdef SPL_BOUNDS_CHECK
+    for (int c = 0; c < 6; ++c) SPL_CHECK(bank[c] >= 0 && bank[c] <= 255, BC_BYTE);
+#endif
     sw[SW_BANK0] = (uint32_t)bank[0] | ((uint32_t)bank[1] << 8) | ((uint32_t)bank[2] << 16) | ((uint32_t)bank[3] << 24);
     sw[SW_BANK1] = (sw[SW_BANK1] & 0xFFFF0000u) | (uint32_t)bank[4] | ((uint32_t)bank[5] << 8);
 }
@@ -394,6 +421,8 @@ __device__ __forceinline__ void pay_for_card(Pl &p, int bank[6], uint4 rec) {
 }
 
 __device__ __forceinline__ uint8_t *slot_rec(const KArena &A, int t, int slot) {
+    SPL_CHECK(t >= 0 && t < A.n, BC_TABLE);
+    SPL_CHECK(slot >= 0 && slot < kSlotRecords, BC_SLOT);
     return A.slots + ((size_t)t * kSlotRecords + slot) * kSlotBytes;
 }
 // slot-record ring status (spl_layout.h)
@@ -584,6 +613,7 @@ __device__ __forceinline__ void enforce_token_limit(Pl &p, int bank[6], int turn
     const bool in_lut = key >= 0;
     bool need_mt = !in_lut;
     if (in_lut) {
+        SPL_CHECK(key < kLutEntries, BC_LUT);
         const uint4 e = key == pre_key ? pre_e : lut[key];
         Pl p2 = p;
         int bank2[6];
@@ -1003,6 +1033,7 @@ __device__ __forceinline__ uint32_t deal_into(uint32_t seed, int P, uint8_t *rec
         const int r = (int)(y >> (32 - bit_length((uint32_t)n)));
         const bool acc = on && d < 4 && r < n;
         const int ai = base + i, ar = base + (acc ? r : i);
+        SPL_CHECK(ai >= 0 && ai < 100 && ar >= 0 && ar < 100, BC_SCRATCH);
         const uint8_t xi = scr[ai], xr = scr[ar];
         between();
         scr[ai] = xr;
@@ -1111,6 +1142,7 @@ __device__ __forceinline__ void store_pcg(const KArena &A, int t, const Pcg64 &g
 }
 
 __device__ __forceinline__ Deal load_pool(const KArena &A, int t) {
+    SPL_CHECK(t >= 0 && t < A.n, BC_TABLE);
     Deal d;
 #pragma unroll
     for (int k = 0; k < 3; ++k) d.board[k] = A.pool[(size_t)(PL_BOARD + k) * A.n + t];
@@ -1119,6 +1151,7 @@ __device__ __forceinline__ Deal load_pool(const KArena &A, int t) {
     return d;
 }
 __device__ __forceinline__ void store_pool(const KArena &A, int t, const Deal &d) {
+    SPL_CHECK(t >= 0 && t < A.n, BC_TABLE);
 #pragma unroll
     for (int k = 0; k < 3; ++k) A.pool[(size_t)(PL_BOARD + k) * A.n + t] = d.board[k];
     A.pool[(size_t)PL_NOB0 * A.n + t] = d.nob0;
@@ -1142,6 +1175,7 @@ __device__ __forceinline__ uint32_t deal_next(const KArena &A, int t, int slot, 
 
 template <int P>
 __device__ __forceinline__ void load_tab(Tab<P> &T, const KArena &A, int t) {
+    SPL_CHECK(t >= 0 && t < A.n, BC_TABLE);
 #pragma unroll
     for (int w = 0; w < SW_COUNT; ++w) T.sw[w] = A.planes[(size_t)w * A.n + t];
 #pragma unroll
@@ -1152,6 +1186,7 @@ __device__ __forceinline__ void load_tab(Tab<P> &T, const KArena &A, int t) {
 
 template <int P>
 __device__ __forceinline__ void store_tab(const Tab<P> &T, const KArena &A, int t) {
+    SPL_CHECK(t >= 0 && t < A.n, BC_TABLE);
 #pragma unroll
     for (int w = 0; w < SW_COUNT; ++w) A.planes[(size_t)w * A.n + t] = T.sw[w];
 #pragma unroll
@@ -1283,6 +1318,7 @@ __device__ __forceinline__ StepPre step_prefetch(const Tab<P> &T, int action, bo
     if (live_tab && ptier >= 0) {
         const int len = (int)bget(T.sw[SW_DECK], ptier);
         const uint8_t *live = live_rec(A, t, T.sw[SW_MISC]);
+        SPL_CHECK(len <= tier_size(ptier), BC_DECK);
         if (len > 0) pre.top = abl(ABL_DECK_GATHER) ? (uint32_t)(len + 3 * ptier) : live[tier_base(ptier) + len - 1];
     }
     if (live_tab && action >= 0 && action < SPL_NUM_ACTIONS) {
@@ -1292,6 +1328,7 @@ __device__ __forceinline__ StepPre step_prefetch(const Tab<P> &T, int action, bo
         int bank[6];
         get_bank(T.sw, bank);
         pre.key = predict_lut_key(unpack_pl(pw4), bank, action, get_turn(T.sw), tp);
+        SPL_CHECK(pre.key < kLutEntries, BC_LUT);
         if (pre.key >= 0) pre.e = abl(ABL_LUT_GATHER) ? make_uint4(0x12345678u, 0x9abcdef0u, 0x0fedcba9u, (uint32_t)pre.key) : Tb.lut[pre.key];
     }
     return pre;
@@ -2270,6 +2307,23 @@ int spl_debug_set_rollout_stamps(void *buf) {
     return SPL_OK;
 }
 #endif
+
+int spl_debug_bounds_flags(uint32_t *flags, int clear) {
+#ifdef SPL_BOUNDS_CHECK
+    if (!flags) return fail(SPL_E_ARG, "null flags");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(flags, HIP_SYMBOL(g_bounds_flags), sizeof(uint32_t)));
+    if (clear) {
+        const uint32_t z = 0;
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_bounds_flags), &z, sizeof(z)));
+    }
+    return SPL_OK;
+#else
+    (void)flags;
+    (void)clear;
+    return fail(SPL_E_ARG, "not a bounds-check build (-DSPL_BOUNDS_CHECK)");
+#endif
+}
 
 int spl_debug_set_stream_limit(int outputs) {
     if (outputs < 1 || outputs > MTStream::kMaxOut) return fail(SPL_E_ARG, "stream limit must be 1..454");

@@ -91,6 +91,7 @@ SIGNATURES = {
     "spl_reset": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
                   c_int32),
     "spl_debug_set_stream_limit": ([c_int32], c_int32),
+    "spl_debug_bounds_flags": ([c_void_p, c_int32], c_int32),
     "spl_deal": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
     "spl_step": ([c_void_p, ctypes.POINTER(ArenaDesc), ctypes.POINTER(StepArgs), c_void_p], c_int32),
     "spl_rollout": ([c_void_p, ctypes.POINTER(ArenaDesc), ctypes.POINTER(StepArgs), c_int32, c_int32, c_void_p],

@@ -236,3 +236,13 @@ def test_oracle_under_address_and_undefined_sanitizers(tmp_path):
     env.pop("LD_PRELOAD", None)
     r = subprocess.run([str(exe), str(tables)], capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def test_bounds_check_hook_absent_from_product_build():
+    import ctypes
+    from splendor_gym import _native
+    lib = _native.load_library()
+    v = ctypes.c_uint32()
+    assert lib.spl_debug_bounds_flags(ctypes.byref(v), 0) == -1  # product library: not a checked build
+    assert b"bounds-check" in lib.spl_last_error()
+    assert lib.spl_debug_set_stream_limit(0) == -1 and lib.spl_debug_set_stream_limit(455) == -1
