@@ -361,12 +361,18 @@ def main():
                              "algo_bytes_note": algo_note},
                 "launch": rec["how"], "plan": plan}
 
+    def with_traffic(s):
+        """The variant's summary with the committed PMC HBM bytes per launch of its kernel."""
+        pmc_key = {"step": "k_step", "rollout_store": "k_rollout_store", "rollout_inplace": "k_rollout"}[s["variant"]]
+        traffic, traffic_src = load_pmc_traffic(P, T, pmc_key, s["plan"]["per"])
+        s["roofline"].update(traffic=traffic, traffic_source=traffic_src,
+                             traffic_over_algo=None if traffic is None
+                             else round(traffic / s["roofline"]["algo_bytes_per_launch"], 4))
+        return s
+
     if rank == 0:
-        main_s = summary(recs[headline])
-        pmc_key = {"step": "k_step", "rollout_store": "k_rollout_store", "rollout_inplace": "k_rollout"}[headline]
-        traffic, traffic_src = load_pmc_traffic(P, T, pmc_key, main_s["plan"]["per"])
-        roof = dict(main_s["roofline"], traffic=traffic, traffic_source=traffic_src,
-                    traffic_over_algo=None if traffic is None else round(traffic / main_s["roofline"]["algo_bytes_per_launch"], 4))
+        main_s = with_traffic(summary(recs[headline]))
+        roof = main_s["roofline"]
         plan = main_s["plan"]
         out = {
             "metric": f"env-steps/sec (whole node), {P}p {T} tables/GPU",
@@ -397,7 +403,7 @@ def main():
             "error_flags": bad,
         }
         for v in variants[1:]:
-            s = summary(recs[v])
+            s = with_traffic(summary(recs[v]))
             s.pop("plan")
             out["in_place_l3" if v == "rollout_inplace" else ("other_mode" if v == "step" else v)] = s
         print(json.dumps(out))

@@ -102,7 +102,7 @@ __device__ uint64_t *g_stamps;
 #define STAMP(i)                                                                                 \
     do {                                                                                         \
         __builtin_amdgcn_sched_barrier(0);                                                       \
-        if (threadIdx.x == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if ((threadIdx.x & 63) == 0 && g_stamps) g_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
         __builtin_amdgcn_sched_barrier(0);                                                       \
     } while (0)
 // k_rollout keeps its stamps in registers (lane k holds step k's) so that stamping never waits
@@ -165,11 +165,18 @@ struct __align__(16) Consts {
     uint2 nobles[10];
 };
 
-struct __align__(16) BlockLDS : Consts {
+// one wave's output staging
+struct __align__(16) WaveBuf {
     uint64_t mask[64];
     uint32_t mbits[96];  // the wave's 64 x 45 mask bits as one stream (store_mask_block)
     uint8_t rows[64 * kObsDim];   // observation staging; also the deal scratch (64 x 112 B)
     uint8_t frows[64 * kObsDim];  // terminal observations (k_step): stored with everything else at the end
+};
+struct __align__(16) BlockLDS : Consts, WaveBuf {};
+// k_step with W waves (64 tables each) per workgroup: one copy of the constant tables
+template <int W>
+struct __align__(16) StepLDS : Consts {
+    WaveBuf w[W];
 };
 
 // ------------------------------------------------------------------------------------------
@@ -1334,6 +1341,8 @@ __device__ __forceinline__ StepPre step_prefetch(const Tab<P> &T, int action, bo
     return pre;
 }
 
+constexpr uint64_t kMaskDeferred = 1ull << 63;  // step_rules(defer_mask): legal mask still to evaluate
+
 struct StepOut {
     uint32_t flags;
     float reward;
@@ -1347,7 +1356,7 @@ struct StepOut {
 template <int P>
 __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepPre &pre, bool valid, const Consts &L,
                                               const KTables &Tb, uint32_t *mtx, bool known = false,
-                                              uint64_t known_mask = 0ull) {
+                                              uint64_t known_mask = 0ull, bool defer_mask = false) {
     StepOut o{0u, 0.0f, false, 0ull};
     bool want_mask = false;
     if (valid) {
@@ -1397,8 +1406,11 @@ __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepP
             }
         }
     }
-    // one legal_moves evaluation per lane (a single call site keeps one copy in the code)
-    if (want_mask) o.mask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);
+    // one legal_moves evaluation per lane (a single call site keeps one copy in the code).
+    // defer_mask: left to the caller (kMaskDeferred marks the lanes that need it; k_step_ws
+    // evaluates it after handing the state to its output wave)
+    if (defer_mask) o.mask = want_mask ? kMaskDeferred : 0ull;
+    else if (want_mask) o.mask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);
     return o;
 }
 
@@ -1474,16 +1486,27 @@ __device__ __forceinline__ void store_final_rows(const uint8_t *rows_lds, uint64
 // any wave has started its stores; from there to the block stores at the end the wave touches
 // only registers and LDS.  A load issued later would queue behind the other waves' observation
 // writes (tens of MB in flight) and its wave would become the kernel's tail.
-template <int P>
-__global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
-    __shared__ BlockLDS L;
+//
+// W waves per workgroup (64 tables each, independent except for the shared constant tables):
+// fewer, larger workgroups reach the whole chip sooner than 64-thread ones.
+template <int P, int W>
+__global__ __launch_bounds__(64 * W) void k_step(KArena A, KTables Tb, KStep S) {
+    __shared__ StepLDS<W> SL;
+    Consts &L = SL;
+    const int wave = W == 1 ? 0 : (int)(threadIdx.x >> 6);
+    WaveBuf &B = SL.w[wave];
     const int lane = lane_id();
-    const int t0 = blockIdx.x * 64;
+    const int t0 = (blockIdx.x * W + wave) * 64;
     const int t = t0 + lane;
     const bool valid = t < A.n;
-    const int rows = min(64, A.n - t0);
+    const int rows = max(0, min(64, A.n - t0));
     STAMP(0);
-    load_tables_lds(L, Tb);
+    if (W == 1) {
+        load_tables_lds(L, Tb);
+    } else {
+        for (int i = threadIdx.x; i < 90; i += 64 * W) L.cards[i] = Tb.cards[i];
+        if (threadIdx.x < 10) L.nobles[threadIdx.x] = Tb.nobles[threadIdx.x];
+    }
 
     Tab<P> T;
     int action = 0;
@@ -1495,12 +1518,13 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     } else {
         fresh_state(T, 0u, empty_deal());
     }
+    if (W == 1) wave_lds_sync();
+    else __syncthreads();  // the constant tables (nothing stored yet: no store drain to wait for)
     const StepPre pre = step_prefetch(T, action, valid, A, t, Tb);
-    wave_lds_sync();
     STAMP(1);
 
     // LDS for a token-return continuation (LaneMT): the observation rows past the deal scratch
-    uint32_t *const mtx = reinterpret_cast<uint32_t *>(&L.rows[64 * kScratchStride]);
+    uint32_t *const mtx = reinterpret_cast<uint32_t *>(&B.rows[64 * kScratchStride]);
     StepOut o = step_rules(T, action, pre, valid, L, Tb, mtx);
     // autoreset 2: a table terminal on entry is re-dealt without a move (dual-step opponent phase)
     const bool entry_reset = valid && S.autoreset == 2 && (o.flags & SPL_F_AFTER_TERMINAL);
@@ -1513,28 +1537,28 @@ __global__ __launch_bounds__(64) void k_step(KArena A, KTables Tb, KStep S) {
     // with everything else at the end
     const bool want_final = S.autoreset && S.final_obs != nullptr && !abl(ABL_FINAL);
     const uint64_t fin = __ballot(ended && want_final);
-    if (__any(ended && want_final)) encode_row(T, L.frows, L);  // rows of other lanes are not stored
+    if (__any(ended && want_final)) encode_row(T, B.frows, L);  // rows of other lanes are not stored
     const int fin_moves = get_moves(T.sw);
     const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;
     STAMP(5);
     bool pool_dirty = false;
     if (ended && S.autoreset && !abl(ABL_RESET))
-        autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], mtx, o, pool_dirty);
+        autoreset_table(T, A, t, pool, &B.rows[lane * kScratchStride], mtx, o, pool_dirty);
     STAMP(6);
     wave_lds_sync();  // deal scratch (rows) free again
 
     // observation + mask of the current state, block stores
-    if (!abl(ABL_ENCODE)) encode_row(T, L.rows, L);
-    L.mask[lane] = o.mask;
+    if (!abl(ABL_ENCODE)) encode_row(T, B.rows, L);
+    B.mask[lane] = o.mask;
     STAMP(7);
     wave_lds_sync();
     STAMP(8);
     if (!abl(ABL_STORE)) {
-        if (!abl(ABL_OBS_STORE)) store_obs_block(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
+        if (!abl(ABL_OBS_STORE)) store_obs_block(B.rows, rows, S.obs + (size_t)t0 * kObsDim);
         STAMP(9);
-        if (!abl(ABL_MASK_STORE)) store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+        if (!abl(ABL_MASK_STORE)) store_mask_block(B.mask, B.mbits, rows, S.mask + (size_t)t0 * 45);
     }
-    store_final_rows(L.frows, fin, S.final_obs, t0);
+    store_final_rows(B.frows, fin, S.final_obs, t0);
     STAMP(10);
     if (valid && o.term) {  // no-return atomics: nothing to wait for
         if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_add);
@@ -1801,13 +1825,141 @@ __device__ __forceinline__ void ws_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
+// SplendorEnv.step for every table with the rules / output split of k_rollout_ws, for ONE step:
+// 128-thread workgroups of 64 tables.  The RULES wave loads, steps and autoresets its tables and
+// hands the new state words (and the pre-reset words of tables that just ended) to the OUTPUT
+// wave through LDS; the output wave encodes and stores the observation rows (terminal rows first)
+// while the rules wave evaluates the legal mask of the new state (engine legal_moves,
+// envs/splendor_env.py:81) and the next action; a second hand-off passes the masks and the small
+// outputs.  The output wave also stages the constant tables while the rules wave's state loads
+// are in flight.  (Terminal rows written per lane by the rules wave instead: 27.5 -> 29.0 us.)  Same outputs, bit for bit, as k_step (the GPU parity suite runs through it).
+template <int P>
+struct __align__(16) StepWsLDS : Consts {
+    static constexpr int kW = SW_COUNT + 4 * P;  // state words per table
+    uint32_t st[kW][64];   // state after the step (and autoreset)
+    uint32_t fst[kW][64];  // pre-reset state of the tables that ended (final_observation)
+    uint32_t small[64];    // pack_small
+    uint64_t mask[64];
+    uint64_t fin;          // lanes with a terminal row
+    uint32_t mbits[96];
+    uint8_t rows[64 * kObsDim];  // observation staging; before hand-off 1 the rules wave's deal scratch + LaneMT
+};
+static_assert(sizeof(StepWsLDS<4>) <= 40960, "k_step_ws needs four workgroups per CU");
+
+template <int P>
+__global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) {
+    __shared__ StepWsLDS<P> L;
+    constexpr int kW = StepWsLDS<P>::kW;
+    const int lane = lane_id();
+    const bool rules_wave = threadIdx.x < 64;
+    const int t0 = blockIdx.x * 64;
+    const int t = t0 + lane;
+    const bool valid = t < A.n;
+    const int rows = min(64, A.n - t0);
+    const bool want_final = S.autoreset && S.final_obs != nullptr;
+    if (rules_wave) {
+        Tab<P> T;
+        int action = 0;
+        Deal pool = empty_deal();
+        if (valid) {
+            load_tab(T, A, t);
+            action = S.actions[t];
+            if (S.autoreset) pool = load_pool(A, t);
+        } else {
+            fresh_state(T, 0u, empty_deal());
+        }
+        const StepPre pre = step_prefetch(T, action, valid, A, t, Tb);
+        ws_sync();  // hand-off 0: the output wave staged the constant tables
+        uint32_t *const mtx = reinterpret_cast<uint32_t *>(&L.rows[64 * kScratchStride]);
+        StepOut o = step_rules(T, action, pre, valid, L, Tb, mtx, false, 0ull, true);
+        // autoreset 2: a table terminal on entry is re-dealt without a move (dual-step opponent phase)
+        const bool entry_reset = valid && S.autoreset == 2 && (o.flags & SPL_F_AFTER_TERMINAL);
+        if (entry_reset) o.flags = 0u;
+        const bool ended = valid && (o.term || entry_reset);
+        const int8_t wnr = (int8_t)get_winner(T.sw);
+        const bool fin_me = ended && want_final;
+        if (fin_me) {
+#pragma unroll
+            for (int w = 0; w < kW; ++w) L.fst[w][lane] = tab_word(T, w);
+        }
+        const uint64_t fin = __ballot(fin_me);
+        if (lane == 0) L.fin = fin;
+        const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;
+        bool pool_dirty = false;
+        if (ended && S.autoreset)
+            autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], mtx, o, pool_dirty);
+#pragma unroll
+        for (int w = 0; w < kW; ++w) L.st[w][lane] = tab_word(T, w);
+        ws_sync();  // hand-off 1: state words (deal scratch in `rows` free again)
+        if (o.mask & kMaskDeferred) o.mask = legal_of(T, L);
+        L.mask[lane] = o.mask;
+        L.small[lane] = pack_small(valid, o, wnr, valid && o.term, ep_add);
+        ws_sync();  // hand-off 2: masks and small outputs
+        if (valid) {
+            if (S.next_actions) {
+                const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
+                S.next_actions[t] = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply);
+            }
+            store_tab(T, A, t);
+            if (pool_dirty) store_pool(A, t, pool);
+        }
+    } else {
+        load_tables_lds(L, Tb);
+        ws_sync();  // hand-off 0
+        ws_sync();  // hand-off 1
+        Tab<P> T;
+#pragma unroll
+        for (int w = 0; w < kW; ++w) set_tab_word(T, w, L.st[w][lane]);
+        const uint64_t fin = L.fin;
+        if (fin) {  // terminal rows (info["final_observation"]) first, through the same staging rows
+            const bool mine = (fin >> lane) & 1ull;
+            Tab<P> F = T;
+            if (mine) {
+#pragma unroll
+                for (int w = 0; w < kW; ++w) set_tab_word(F, w, L.fst[w][lane]);
+            }
+            encode_row(F, L.rows, L);
+            wave_lds_sync();
+            store_final_rows(L.rows, fin, S.final_obs, t0);
+            if (__any(mine && get_moves(F.sw) > 255)) {  // move_count > 255: crafted states only
+                __builtin_amdgcn_s_waitcnt(0);
+                if (mine && get_moves(F.sw) > 255) S.final_obs[(size_t)t * kObsDim + 295] = get_moves(F.sw);
+            }
+            wave_lds_sync();  // the terminal rows' LDS reads are done
+        }
+        encode_row(T, L.rows, L);
+        wave_lds_sync();
+        store_obs_block(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
+        ws_sync();  // hand-off 2
+        store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+        const uint32_t sm = L.small[lane];
+        if (sm & (1u << 9)) {  // valid lane: reward / terminated / flags / winner, episode statistics
+            S.reward[t] = reward_of_code((sm >> 13) & 7u);
+            S.terminated[t] = (uint8_t)((sm >> 8) & 1u);
+            S.flags[t] = (uint8_t)(sm & 0xFFu);
+            if (S.winner) S.winner[t] = (int8_t)((int)((sm >> 10) & 7u) - 1);
+            if (sm & (1u << 18)) {
+                if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_of_code((sm >> 16) & 3u));
+                if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
+            }
+        }
+        if (__any(valid && get_moves(T.sw) > 255)) {  // patch after this wave's block stores of the same dwords
+            __builtin_amdgcn_s_waitcnt(0);
+            if (valid && get_moves(T.sw) > 255) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
+        }
+    }
+}
+
 // TPW = tables per workgroup: 64, or 32 for grids too small to give every SIMD a wave (e.g. the
 // 32 768-table share of a 4-player 8-GPU run): twice the workgroups, lanes 32-63 idle.  The rules
 // work is latency-bound at one wave per SIMD, so half-populated waves on every SIMD finish a step
 // in about the time full ones take on half of them.
-template <int P, int TPW>
-__global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep S, int K, int per_step, int refill) {
+// kStore: per-step outputs (a [K][n][...] rollout store) or every step into the same [n][...] block;
+// a template argument so that the two variants are separate kernels in a profile.
+template <int P, int TPW, bool kStore>
+__global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep S, int K, int refill) {
     static_assert(TPW == 64 || TPW == 32, "64 or 32 tables per workgroup");
+    constexpr bool per_step = kStore;
     __shared__ WsLDS<P> L;
     constexpr int kW = WsLDS<P>::kW;
     const int lane = lane_id();
@@ -2280,6 +2432,14 @@ static int launch_check() {
 }
 
 static inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 63) / 64); }
+#ifndef SPL_STEP_WAVES
+#define SPL_STEP_WAVES 1
+#endif
+constexpr int kStepWaves = SPL_STEP_WAVES;  // k_step waves per workgroup
+#ifndef SPL_STEP_WS
+#define SPL_STEP_WS 1
+#endif
+constexpr bool kStepWs = SPL_STEP_WS != 0;  // spl_step: two-wave k_step_ws (else k_step)
 
 extern "C" {
 
@@ -2377,9 +2537,9 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         int occ[5] = {0, 0, 0, 0, 0};
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], k_rollout_ws<2, 64>, 128, 0));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[3], k_rollout_ws<3, 64>, 128, 0));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[4], k_rollout_ws<4, 64>, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], k_rollout_ws<2, 64, true>, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[3], k_rollout_ws<3, 64, true>, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[4], k_rollout_ws<4, 64, true>, 128, 0));
         for (int q = 0; q < 5; ++q) ws_resident[q] = occ[q] * cus;
     }
     spl_ctx_t *c = new spl_ctx_t();
@@ -2542,8 +2702,14 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     const KStep S = kstep(a);
     const KArena A = karena(arena);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    DISPATCH_P(arena->players,
-               hipLaunchKernelGGL(k_step<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A, ktables(ctx), S));
+    if (kStepWs) {
+        DISPATCH_P(arena->players, hipLaunchKernelGGL(k_step_ws<PP>, dim3(blocks_for(arena->n)), dim3(128), 0, s, A,
+                                                      ktables(ctx), S));
+    } else {
+        DISPATCH_P(arena->players,
+                   hipLaunchKernelGGL((k_step<PP, kStepWaves>), dim3((unsigned)((arena->n + 64 * kStepWaves - 1) / (64 * kStepWaves))),
+                                      dim3(64 * kStepWaves), 0, s, A, ktables(ctx), S));
+    }
     if (int r = launch_check()) return r;
     arena->steps += 1;
     if (a->autoreset && ctx->refill_period > 0 && arena->steps % ctx->refill_period == 0)
@@ -2576,19 +2742,24 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     if (ctx->pipeline == 2) tpw = 64;
     else if (ctx->pipeline == 3) tpw = 32;
     else if (ctx->pipeline == 1) tpw = 2 * (int64_t)blocks_for(arena->n) <= resident ? 32 : 64;
-    const int p_out = per_step_outputs != 0;
+    const bool p_out = per_step_outputs != 0;
+#define SPL_LAUNCH_WS(TPW, BLOCKS)                                                                           \
+    DISPATCH_P(arena->players, if (p_out) {                                                                  \
+        hipLaunchKernelGGL((k_rollout_ws<PP, TPW, true>), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
+                           (int)steps, fused);                                                               \
+    } else {                                                                                                 \
+        hipLaunchKernelGGL((k_rollout_ws<PP, TPW, false>), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
+                           (int)steps, fused);                                                               \
+    })
     if (tpw == 64) {
-        DISPATCH_P(arena->players,
-                   hipLaunchKernelGGL((k_rollout_ws<PP, 64>), dim3(blocks_for(arena->n)), dim3(128), 0, s, A,
-                                      ktables(ctx), S, (int)steps, p_out, fused));
+        SPL_LAUNCH_WS(64, blocks_for(arena->n));
     } else if (tpw == 32) {
-        DISPATCH_P(arena->players,
-                   hipLaunchKernelGGL((k_rollout_ws<PP, 32>), dim3((unsigned)((arena->n + 31) / 32)), dim3(128), 0, s,
-                                      A, ktables(ctx), S, (int)steps, p_out, fused));
+        SPL_LAUNCH_WS(32, (unsigned)((arena->n + 31) / 32));
     } else {
         DISPATCH_P(arena->players, hipLaunchKernelGGL(k_rollout<PP>, dim3(blocks_for(arena->n)), dim3(64), 0, s, A,
                                                       ktables(ctx), S, (int)steps, (int)(per_step_outputs != 0), fused));
     }
+#undef SPL_LAUNCH_WS
     if (int r = launch_check()) return r;
     arena->steps += steps;
     if (fused) arena->epoch += fused;

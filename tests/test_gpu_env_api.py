@@ -99,9 +99,16 @@ def mask_from_state(env):  # reference tests/utils.py:15-16
 
 
 def test_no_legal_move_draw():  # test_draw_rule.py:7-24, in-place edits of env.state (no set_state)
+    """The reference resets from entropy (SplendorEnv(seed=0) does not seed reset) and reserves the
+    first three tier-1 deck cards: when one of them costs white only, 10 white tokens buy it and its
+    assertion fails (a flaky case of the reference test).  Here the reset is seeded with the first
+    seed whose three cards are not all-white, which is the situation the test means."""
     from splendor_gym.envs import SplendorEnv
     env = SplendorEnv(seed=0)
-    obs, info = env.reset()
+    for seed in range(100):
+        obs, info = env.reset(seed=seed)
+        if not any(set(c for c, v in card.cost.items() if v) <= {"white"} for card in env.state.decks[1][:3]):
+            break
     env.state.bank[:] = [0, 0, 0, 0, 0, 0]
     p = env.state.players[env.state.to_play]
     p.tokens[:] = [10, 0, 0, 0, 0, 0]

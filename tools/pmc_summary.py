@@ -45,9 +45,18 @@ def main():
     ap.add_argument("--rollout-key", default="k_rollout_store",
                     help="name under which the rollout kernel's traffic is recorded: k_rollout_store (bench "
                          "--outputs store, per-step blocks) or k_rollout (--outputs inplace)")
+    ap.add_argument("--merge", action="store_true",
+                    help="update the kernels of this run in an existing summary instead of replacing it")
     a = ap.parse_args()
     per, dur = load(a.pmc_dir)
-    summary = {"tables": a.tables, "players": a.players, "source": a.pmc_dir, "kernels": {}}
+    summary = {"tables": a.tables, "players": a.players, "kernels": {}, "hbm_bytes_per_launch": {},
+               "steps_per_launch": {}, "sources": {}}
+    if a.merge and os.path.exists(a.out):
+        with open(a.out) as f:
+            old = json.load(f)
+        assert old.get("tables") == a.tables and old.get("players") == a.players, "merge: other workload"
+        for key in ("kernels", "hbm_bytes_per_launch", "steps_per_launch", "sources"):
+            summary[key].update(old.get(key, {}))
     for k, cs in per.items():
         mean = {c: sum(v) / len(v) for c, v in cs.items()}
         d = {"counters_mean_per_dispatch": mean, "dispatches_per_pass": max(len(v) for v in cs.values())}
@@ -77,13 +86,12 @@ def main():
         if "TCC_EA0_RDREQ" in mean:
             d["rdreq_bytes_64B"] = mean["TCC_EA0_RDREQ"] * 64
             d["wrreq_bytes_64B"] = mean.get("TCC_EA0_WRREQ", 0) * 64
-        summary["kernels"][k] = d
-    summary["hbm_bytes_per_launch"] = {}
-    for k, name in (("k_step", "k_step"), ("k_rollout", a.rollout_key)):
-        st = summary["kernels"].get(k, {})
-        if "fetch_bytes" in st and "write_bytes" in st:
-            summary["hbm_bytes_per_launch"][name] = round(st["fetch_bytes"] + st["write_bytes"])
-    summary["steps_per_launch"] = {"k_step": 1, a.rollout_key: a.rollout_steps}
+        name = a.rollout_key if k == "k_rollout" else k
+        summary["kernels"][name] = d
+        summary["sources"][name] = a.pmc_dir
+        if name in ("k_step", a.rollout_key) and "fetch_bytes" in d and "write_bytes" in d:
+            summary["hbm_bytes_per_launch"][name] = round(d["fetch_bytes"] + d["write_bytes"])
+            summary["steps_per_launch"][name] = 1 if name == "k_step" else a.rollout_steps
     summary["hbm_bytes_note"] = ("FETCH_SIZE + WRITE_SIZE (KiB x 1024) per launch, uncorrected: the kernels' reads "
                                  "are 4-byte-per-lane planes and gathers, outside the guide's 16 B/lane calibration")
     os.makedirs(os.path.dirname(a.out), exist_ok=True)

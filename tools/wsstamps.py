@@ -125,6 +125,15 @@ def main():
     print("rules waves per SIMD (of each WG's rules wave): " + "; ".join(
         f"{c} -> {int((nr == c).sum())} WGs, mean end {e_last[nr == c].mean():.0f}" for c in sorted(set(nr.tolist()))))
     print("first 8 WGs hwid:", [(int(xcc[i, 0] & 15), int(se[i, 0]), int(cu[i, 0]), int(simd[i, 0]), int(simd[i, 1])) for i in range(8)])
+    # per XCC (blockIdx % 8 is the XCC, checked above): where the rules wave's time goes
+    rs = us(R[..., 4:63, 1] - R[..., 4:63, 0])  # [run, wg, step]
+    tl = us(R[..., 4:63, 2] - R[..., 4:63, 1])
+    enc = us(O[..., 4:63, 1] - O[..., 4:63, 0])
+    ost = us(O[..., 4:63, 2] - O[..., 4:63, 1])
+    for name, v in (("rules", rs), ("tail", tl), ("out encode", enc), ("out obs st", ost)):
+        print(f"per-step {name:10s} by XCC mean/p90/p99: " + " | ".join(
+            f"{v[:, xcd == x].mean():.2f}/{np.percentile(v[:, xcd == x], 90):.1f}/{np.percentile(v[:, xcd == x], 99):.1f}"
+            for x in range(8)))
     # per-workgroup: total rules-wave busy time vs barrier waits; slowest 1% vs median
     busy = us((R[..., :, 2] - R[..., :, 0]).sum(axis=-1))
     slow = end >= np.percentile(end, 99)
