@@ -1830,15 +1830,14 @@ __device__ __forceinline__ void ws_sync() {
 // hands the new state words (and the pre-reset words of tables that just ended) to the OUTPUT
 // wave through LDS; the output wave encodes and stores the observation rows (terminal rows first)
 // while the rules wave evaluates the legal mask of the new state (engine legal_moves,
-// envs/splendor_env.py:81) and the next action; a second hand-off passes the masks and the small
-// outputs.  The output wave also stages the constant tables while the rules wave's state loads
+// envs/splendor_env.py:81) and stores the masks, small outputs, next action and state.  The
+// output wave also stages the constant tables while the rules wave's state loads
 // are in flight.  (Terminal rows written per lane by the rules wave instead: 27.5 -> 29.0 us.)  Same outputs, bit for bit, as k_step (the GPU parity suite runs through it).
 template <int P>
 struct __align__(16) StepWsLDS : Consts {
     static constexpr int kW = SW_COUNT + 4 * P;  // state words per table
     uint32_t st[kW][64];   // state after the step (and autoreset)
     uint32_t fst[kW][64];  // pre-reset state of the tables that ended (final_observation)
-    uint32_t small[64];    // pack_small
     uint64_t mask[64];
     uint64_t fin;          // lanes with a terminal row
     uint32_t mbits[96];
@@ -1857,6 +1856,7 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
     const bool valid = t < A.n;
     const int rows = min(64, A.n - t0);
     const bool want_final = S.autoreset && S.final_obs != nullptr;
+    STAMP(0);
     if (rules_wave) {
         Tab<P> T;
         int action = 0;
@@ -1870,6 +1870,7 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
         }
         const StepPre pre = step_prefetch(T, action, valid, A, t, Tb);
         ws_sync();  // hand-off 0: the output wave staged the constant tables
+        STAMP(1);
         uint32_t *const mtx = reinterpret_cast<uint32_t *>(&L.rows[64 * kScratchStride]);
         StepOut o = step_rules(T, action, pre, valid, L, Tb, mtx, false, 0ull, true);
         // autoreset 2: a table terminal on entry is re-dealt without a move (dual-step opponent phase)
@@ -1877,6 +1878,7 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
         if (entry_reset) o.flags = 0u;
         const bool ended = valid && (o.term || entry_reset);
         const int8_t wnr = (int8_t)get_winner(T.sw);
+        STAMP(2);
         const bool fin_me = ended && want_final;
         if (fin_me) {
 #pragma unroll
@@ -1890,12 +1892,24 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
             autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], mtx, o, pool_dirty);
 #pragma unroll
         for (int w = 0; w < kW; ++w) L.st[w][lane] = tab_word(T, w);
+        STAMP(3);
         ws_sync();  // hand-off 1: state words (deal scratch in `rows` free again)
+        STAMP(4);
         if (o.mask & kMaskDeferred) o.mask = legal_of(T, L);
+        STAMP(5);
+        // masks and small outputs leave from this wave while the output wave streams the rows
         L.mask[lane] = o.mask;
-        L.small[lane] = pack_small(valid, o, wnr, valid && o.term, ep_add);
-        ws_sync();  // hand-off 2: masks and small outputs
+        wave_lds_sync();
+        store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
         if (valid) {
+            S.reward[t] = o.reward;
+            S.terminated[t] = o.term ? 1 : 0;
+            S.flags[t] = (uint8_t)o.flags;
+            if (S.winner) S.winner[t] = wnr;
+            if (o.term) {
+                if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_add);
+                if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
+            }
             if (S.next_actions) {
                 const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
                 S.next_actions[t] = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply);
@@ -1903,10 +1917,14 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
             store_tab(T, A, t);
             if (pool_dirty) store_pool(A, t, pool);
         }
+        STAMP(6);
     } else {
         load_tables_lds(L, Tb);
+        STAMP(1);
         ws_sync();  // hand-off 0
+        STAMP(2);
         ws_sync();  // hand-off 1
+        STAMP(3);
         Tab<P> T;
 #pragma unroll
         for (int w = 0; w < kW; ++w) set_tab_word(T, w, L.st[w][lane]);
@@ -1927,26 +1945,17 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
             }
             wave_lds_sync();  // the terminal rows' LDS reads are done
         }
+        STAMP(4);
         encode_row(T, L.rows, L);
         wave_lds_sync();
+        STAMP(5);
         store_obs_block(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
-        ws_sync();  // hand-off 2
-        store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
-        const uint32_t sm = L.small[lane];
-        if (sm & (1u << 9)) {  // valid lane: reward / terminated / flags / winner, episode statistics
-            S.reward[t] = reward_of_code((sm >> 13) & 7u);
-            S.terminated[t] = (uint8_t)((sm >> 8) & 1u);
-            S.flags[t] = (uint8_t)(sm & 0xFFu);
-            if (S.winner) S.winner[t] = (int8_t)((int)((sm >> 10) & 7u) - 1);
-            if (sm & (1u << 18)) {
-                if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_of_code((sm >> 16) & 3u));
-                if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
-            }
-        }
+        STAMP(6);
         if (__any(valid && get_moves(T.sw) > 255)) {  // patch after this wave's block stores of the same dwords
             __builtin_amdgcn_s_waitcnt(0);
             if (valid && get_moves(T.sw) > 255) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
         }
+        STAMP(7);
     }
 }
 

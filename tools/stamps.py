@@ -14,6 +14,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.environ.get("STAMP_LIB", os.path.join(REPO, "splendor-gym_amd", "ablate", "lib_stamps.so"))
 NAMES = ["start", "loaded+prefetched", "pre-apply", "applied", "step logic", "final obs", "reset done",
          "encoded", "barrier", "obs stored", "mask+final stored", "end"]
+# k_step_ws (the default spl_step kernel): stamps per wave, wave 0 = rules, wave 1 = output
+WS_RULES = ["start", "past hand-off 0", "rules done", "state to LDS (reset done)", "past hand-off 1", "legal mask",
+            "end (mask, small outputs, state stored)"]
+WS_OUT = ["start", "tables staged", "past hand-off 0", "past hand-off 1", "final rows done", "encoded",
+          "obs stores issued", "end"]
 
 CHILD = r'''
 import sys, os, ctypes, json
@@ -27,7 +32,7 @@ e.lib.spl_debug_set_stamps.argtypes = [ctypes.c_void_p]
 e.reset(seeds=range(T))
 buf = [torch.zeros(T, dtype=torch.int32, device=e.device) for _ in range(2)]
 e.sample_uniform(out=buf[0], seed=1, ply=0)
-st = torch.zeros((T // 64) * 16, dtype=torch.int64, device=e.device)
+st = torch.zeros((T // 64) * 2 * 16, dtype=torch.int64, device=e.device)
 _native.check(e.lib, e.lib.spl_debug_set_stamps(st.data_ptr()))
 out = []
 for k in range(96):
@@ -36,6 +41,7 @@ for k in range(96):
     if k >= 80:
         torch.cuda.synchronize()
         out.append(st.view(-1, 16).cpu().tolist())
+        st.zero_()
 print(json.dumps(out))
 '''
 
@@ -57,16 +63,23 @@ def main():
         return 1
     runs = json.loads(r.stdout.strip().splitlines()[-1])
     import numpy as np
+    a = np.array(runs, dtype=np.int64)  # [run, wave slot, 16]
+    ws = (a[0, :, 0] != 0).sum() > a.shape[1] // 2  # k_step_ws stamps two waves per 64 tables
+    if not ws:
+        a = a[:, : a.shape[1] // 2]
     rows = []
-    for run in runs:
-        a = np.array(run, dtype=np.int64)[:, :len(NAMES)]
-        t0 = a[:, 0].min()
-        rows.append(a - t0)
-    a = np.concatenate(rows).astype(np.float64) * 0.01  # 100 MHz ticks -> microseconds
-    print(f"{'phase':22s} {'median us':>10s} {'p90 us':>8s} {'max us':>8s}   (since kernel start, {len(a)} wave-samples)")
-    for i, nm in enumerate(NAMES):
-        col = a[:, i][a[:, i] >= 0]
-        print(f"{i:2d} {nm:19s} {np.median(col):10.2f} {np.percentile(col, 90):8.2f} {col.max():8.2f}")
+    for run in a:
+        t0 = run[run[:, 0] > 0, 0].min()
+        rows.append(np.where(run > 0, run - t0, -1))
+    a = np.stack(rows).astype(np.float64)
+    a = np.where(a >= 0, a * 0.01, np.nan)  # 100 MHz ticks -> microseconds since the kernel's first stamp
+    groups = [("k_step", NAMES, a.reshape(-1, 16))] if not ws else [
+        ("k_step_ws rules wave", WS_RULES, a[:, 0::2].reshape(-1, 16)), ("k_step_ws output wave", WS_OUT, a[:, 1::2].reshape(-1, 16))]
+    for title, names, m in groups:
+        print(f"{title}: {'phase':26s} {'median us':>10s} {'p90 us':>8s} {'max us':>8s}   ({len(m)} wave-samples)")
+        for i, nm in enumerate(names):
+            col = m[:, i][~np.isnan(m[:, i])]
+            print(f"{i:2d} {nm:26s} {np.median(col):10.2f} {np.percentile(col, 90):8.2f} {col.max():8.2f}")
     return 0
 
 
