@@ -139,6 +139,15 @@ class SplendorEnv(Env):
             self._view_rec = self._view.to_record().tobytes()
         return self._view
 
+    def cached_to_play(self) -> Optional[int]:
+        """state.to_play without a device download (None before reset): from an outstanding
+        write-through view if one was handed out, else from the last observation (obs[294])."""
+        if self._eng is None:
+            return None
+        if self._view is not None:
+            return int(self._view.to_play)
+        return int(self.current_player)
+
     def _flush_view(self):
         """Upload host edits of the view handed out by `state` (no-op when unchanged)."""
         if self._view is None:
@@ -152,6 +161,7 @@ class SplendorEnv(Env):
         """Replace the device table by `state` (also what in-place edits of .state do implicitly)."""
         self._engine().upload(state.to_record())
         self._view = None
+        self.current_player = int(state.to_play)
 
     def legal_mask(self) -> np.ndarray:
         """engine legal_moves(self.state) as int8[45], computed on the device (rules.py:40-93)."""

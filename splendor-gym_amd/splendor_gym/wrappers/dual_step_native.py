@@ -21,6 +21,17 @@ class DualStepNativeWrapper(Wrapper):
         self.total_agent_steps = 0
         self.total_opponent_steps = 0
 
+    def _to_play(self):
+        """Player to move, or None before reset.  The reference reads env.state.to_play
+        (dual_step_native.py:94-97, 130); the GPU env answers from its last observation (or from
+        an outstanding write-through view) instead of downloading the table, so a dual step costs
+        two env steps and no state downloads."""
+        cached = getattr(self.env, "cached_to_play", None)
+        if cached is not None:
+            return cached()
+        state = getattr(self.env, "state", None)
+        return None if state is None else state.to_play
+
     def _count_opponent(self):
         self.total_opponent_steps += 1
 
@@ -39,9 +50,9 @@ class DualStepNativeWrapper(Wrapper):
         """(agent_obs, agent_reward, opponent_obs, opponent_reward, done, info) after the agent's
         move and, unless that ended the game, the opponent's reply (dual_step_native.py:90-193).
         Both observation slots hold the same array: the encoding is from the side to play."""
-        if getattr(self.env, "state", None) is None:
+        if self._to_play() is None:
             raise RuntimeError("Cannot call dual_step() before reset()")
-        if self.env.state.to_play != 0:
+        if self._to_play() != 0:
             raise ValueError("dual_step() requires agent (player 0) to move first")
         self.turn_count += 1
         self.total_agent_steps += 1
@@ -55,7 +66,7 @@ class DualStepNativeWrapper(Wrapper):
             info.update({"opponent_action": None, "opponent_reward": opp_reward, "turn_complete": True,
                          "game_ended_on": "agent_move"})
             return obs_a, rew_a, obs_a, opp_reward, True, info
-        to_play = self.env.state.to_play
+        to_play = self._to_play()
         if to_play != 1:
             raise ValueError(f"Expected opponent (player 1) to move after agent, got to_play={to_play}")
         opp_action = self._opp_policy(obs_a, info_a)
