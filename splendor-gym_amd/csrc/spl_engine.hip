@@ -259,9 +259,14 @@ template <int P>
 __device__ __forceinline__ void get_player(const Tab<P> &T, int p, uint32_t w[4]) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        uint32_t v = opaque(T.pw[0][k]);
+        // launder every player's word first: an asm inside the select would be executed
+        // conditionally, i.e. compiled into one branch per word
+        uint32_t o[P];
 #pragma unroll
-        for (int q = 1; q < P; ++q) v = (p == q) ? opaque(T.pw[q][k]) : v;
+        for (int q = 0; q < P; ++q) o[q] = opaque(T.pw[q][k]);
+        uint32_t v = o[0];
+#pragma unroll
+        for (int q = 1; q < P; ++q) v = (p == q) ? o[q] : v;
         w[k] = v;
     }
 }
@@ -360,18 +365,29 @@ __device__ __forceinline__ uint64_t legal_mask(const uint32_t *sw, const Pl &p, 
     for (int c = 0; c < 5; ++c) m |= (uint64_t)(bank[c] >= 4) << (10 + c);  // :61-63
     const bool can_res = p.nres < 3;
     const Have h = have_of(p);
+    // every card record is read unconditionally (missing cards read record 0) and combined with
+    // bitwise ops: `present && afford(card_rec(...))` compiled into 15 branches, each an LDS read
+    // followed by its own lgkmcnt(0) wait — 15 serial LDS round trips per legal mask
+    uint4 rec[15];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) rec[k] = card_rec(L, (int)bget(sw[SW_BOARD + k / 4], k % 4));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) rec[12 + i] = card_rec(L, p.res[i]);
 #pragma unroll
     for (int k = 0; k < 12; ++k) {  // :66-80
-        const int id = (int)bget(sw[SW_BOARD + k / 4], k % 4);
-        const bool present = id != 0xFF;
-        m |= (uint64_t)(present && afford(h, card_rec(L, id))) << (15 + k);
-        m |= (uint64_t)(present && can_res) << (27 + k);
+        const uint32_t present = bget(sw[SW_BOARD + k / 4], k % 4) != 0xFFu ? 1u : 0u;
+        const uint32_t aff = afford(h, rec[k]) ? 1u : 0u;
+        m |= (uint64_t)(present & aff) << (15 + k);
+        m |= (uint64_t)(present & (can_res ? 1u : 0u)) << (27 + k);
     }
 #pragma unroll
     for (int t = 0; t < 3; ++t) m |= (uint64_t)(can_res && bget(sw[SW_DECK], t) > 0) << (39 + t);  // :83-86
 #pragma unroll
-    for (int i = 0; i < 3; ++i)  // :89-91
-        m |= (uint64_t)(i < p.nres && afford(h, card_rec(L, p.res[i]))) << (42 + i);
+    for (int i = 0; i < 3; ++i) {  // :89-91
+        const uint32_t held = i < p.nres ? 1u : 0u;
+        const uint32_t aff = afford(h, rec[12 + i]) ? 1u : 0u;
+        m |= (uint64_t)(held & aff) << (42 + i);
+    }
     return m;
 }
 

@@ -16,14 +16,27 @@ OUTD = os.path.join(REPO, "splendor-gym_amd", "ablate")
 SRCS = [os.path.join(CSRC, f) for f in ("spl_engine.hip", "spl_policy.hip", "spl_policy32.hip", "spl_dual.hip")]
 
 
+def sources_at(rev):
+    """The engine sources as of git revision `rev` (exported to a temporary tree)."""
+    import tempfile
+    d = tempfile.mkdtemp(prefix="spl_rev_")
+    arc = subprocess.run(["git", "-C", REPO, "archive", rev, "splendor-gym_amd/csrc", "include"], check=True,
+                         capture_output=True).stdout
+    subprocess.run(["tar", "-x", "-C", d], input=arc, check=True)
+    return [os.path.join(d, "splendor-gym_amd", "csrc", os.path.basename(f)) for f in SRCS]
+
+
 def build(specs):
+    """name=-DFLAG,... builds the working tree; name@REV=-DFLAG,... builds git revision REV."""
     os.makedirs(OUTD, exist_ok=True)
     procs = []
     for spec in specs:
         name, _, flags = spec.partition("=")
+        name, _, rev = name.partition("@")
+        srcs = sources_at(rev) if rev else SRCS
         out = os.path.join(OUTD, f"lib_{name}.so")
         cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-w",
-               *[f for f in flags.split(",") if f], "-shared", "-o", out, *SRCS]
+               *[f for f in flags.split(",") if f], "-shared", "-o", out, *srcs]
         procs.append((name, subprocess.Popen(cmd)))
     for name, p in procs:
         if p.wait() != 0:
