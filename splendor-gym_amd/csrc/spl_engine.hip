@@ -119,7 +119,7 @@ __device__ uint64_t *g_rstamps;
     } while (0)
 // k_rollout_ws: both waves keep kWsStamps stamps per step in registers (lane k = step k, K <= 64),
 // written to g_wsstamps[workgroup][wave][step][kWsStamps] at the end.
-constexpr int kWsStamps = 4;
+constexpr int kWsStamps = 8;  // 0-3 per step; 4-7 sub-phases of the rules wave
 __device__ uint64_t *g_wsstamps;
 __device__ uint32_t *g_wshwid;  // [workgroup][wave][2]: HW_ID (SIMD, CU, SE) and XCC_ID of each wave
 __device__ uint64_t *g_wsclk;   // [workgroup][4]: s_memtime / s_memrealtime at the rules wave's start and end
@@ -1372,10 +1372,16 @@ struct StepOut {
 // envs/splendor_env.py:51-90 on the table in registers.  `known` (k_rollout after its first
 // step): `known_mask` is legal_moves of the table's current state, computed by the previous step,
 // so "any legal move?" and mask[action] need no re-evaluation.
-template <int P>
+// sub-phase stamp hook of step_rules (diagnostic builds pass a stamping lambda)
+struct NoStamp {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+
+template <int P, class Stamp = NoStamp>
 __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepPre &pre, bool valid, const Consts &L,
                                               const KTables &Tb, uint32_t *mtx, bool known = false,
-                                              uint64_t known_mask = 0ull, bool defer_mask = false) {
+                                              uint64_t known_mask = 0ull, bool defer_mask = false,
+                                              Stamp stamp = Stamp()) {
     StepOut o{0u, 0.0f, false, 0ull};
     bool want_mask = false;
     if (valid) {
@@ -1411,8 +1417,10 @@ __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepP
                 want_mask = true;
             } else {
                 STAMP(2);
+                stamp(4);
                 if (!abl(ABL_APPLY)) apply_action(T, action, pre.top, L, Tb.lut, pre.key, pre.e, mtx);  // :68
                 STAMP(3);
+                stamp(5);
                 o.term = is_terminal(T.sw);                       // :70
                 if (o.term) {                                     // :71-80
                     const int w = get_winner(T.sw);
@@ -1425,6 +1433,7 @@ __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepP
             }
         }
     }
+    stamp(6);
     // one legal_moves evaluation per lane (a single call site keeps one copy in the code).
     // defer_mask: left to the caller (kMaskDeferred marks the lanes that need it; k_step_ws
     // evaluates it after handing the state to its output wave)
@@ -2033,7 +2042,12 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
             const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
             WSSTAMP(0, k);
             // token-return continuation (LaneMT) in this step's free state slot
+#ifdef SPL_STAMPS
+            auto sub = [&](int i) { WSSTAMP(i, k); };
+            StepOut o = step_rules(T, action, pre, valid, L, Tb, &L.st[b][0][0], k > 0, cur_mask, false, sub);
+#else
             StepOut o = step_rules(T, action, pre, valid, L, Tb, &L.st[b][0][0], k > 0, cur_mask);
+#endif
             WSSTAMP(1, k);
             if (rs.due(k) && valid && pend_of(T.sw[SW_MISC]) > 0)  // fused pool refill
                 T.sw[SW_MISC] = refill_table<P>(A, t, T.sw[SW_MISC], L.scratch(b, lane), L.deal_mtx(b), pool, pool_dirty);
@@ -2052,6 +2066,7 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
             const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;  // per termination, as k_step
             if (valid && o.term && S.autoreset)
                 autoreset_table(T, A, t, pool, L.scratch(b, lane), L.deal_mtx(b), o, pool_dirty);
+            WSSTAMP(7, k);
             L.small[b][lane] = pack_small(valid, o, wnr, valid && o.term, ep_add);  // stored by the output wave
             action = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
             cur_mask = o.mask;

@@ -33,7 +33,7 @@ _native.check(e.lib, e.lib.spl_debug_set_ws_hwid(hw.data_ptr()))
 e.lib.spl_debug_set_ws_clk.argtypes = [ctypes.c_void_p]
 clk = torch.zeros((T // 64) * 4, dtype=torch.int64, device=e.device)
 _native.check(e.lib, e.lib.spl_debug_set_ws_clk(clk.data_ptr()))
-st = torch.zeros((T // 64) * 2 * 64 * 4, dtype=torch.int64, device=e.device)
+st = torch.zeros((T // 64) * 2 * 64 * 8, dtype=torch.int64, device=e.device)
 _native.check(e.lib, e.lib.spl_debug_set_ws_stamps(st.data_ptr()))
 store = None if inplace else dict(
     obs=torch.empty((K, T, 297), dtype=torch.int32, device=e.device),
@@ -48,7 +48,7 @@ for it in range(6):
     e.rollout(K, actions=buf[it & 1], next_actions=buf[(it & 1) ^ 1], policy_seed=1, ply=1 + K * it, out=store)
     if it >= 3:
         torch.cuda.synchronize()
-        out.append(st.view(-1, 2, 64, 4).cpu().numpy().tolist())
+        out.append(st.view(-1, 2, 64, 8).cpu().numpy().tolist())
         hws = hw.view(-1, 2, 2).cpu().numpy().tolist()
         clks = clk.view(-1, 4).cpu().numpy().tolist()
 print(json.dumps(clks))
@@ -62,9 +62,10 @@ def main():
     if "--lib" in sys.argv:
         lib = sys.argv[sys.argv.index("--lib") + 1]
     if "--run" not in sys.argv:
-        os.makedirs(os.path.dirname(LIB), exist_ok=True)
+        os.makedirs(os.path.dirname(lib), exist_ok=True)
+        extra = os.environ.get("STAMP_DEFS", "").split()  # e.g. STAMP_DEFS=-DSPL_ABL=49152
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-DSPL_STAMPS", "-w",
-                        "-shared", "-o", LIB, *[os.path.join(REPO, "splendor-gym_amd", "csrc", f)
+                        *extra, "-shared", "-o", lib, *[os.path.join(REPO, "splendor-gym_amd", "csrc", f)
                                                   for f in ("spl_engine.hip", "spl_policy.hip", "spl_policy32.hip", "spl_dual.hip")]],
                        check=True)
         if "--build-only" in sys.argv:
@@ -125,6 +126,14 @@ def main():
     print("rules waves per SIMD (of each WG's rules wave): " + "; ".join(
         f"{c} -> {int((nr == c).sum())} WGs, mean end {e_last[nr == c].mean():.0f}" for c in sorted(set(nr.tolist()))))
     print("first 8 WGs hwid:", [(int(xcc[i, 0] & 15), int(se[i, 0]), int(cu[i, 0]), int(simd[i, 0]), int(simd[i, 1])) for i in range(8)])
+    # rules-wave sub-phases (stamps 4-7; 4/5 only on lanes' steps that apply an action, so a
+    # missing stamp reads as 0 and those steps are skipped)
+    ok = (R[..., 4:63, 4] > 0) & (R[..., 4:63, 5] > 0) & (R[..., 4:63, 6] > 0)
+    sub = {"pre (to apply)": (R[..., 4:63, 4] - R[..., 4:63, 0]), "apply": (R[..., 4:63, 5] - R[..., 4:63, 4]),
+           "post (term/reward)": (R[..., 4:63, 6] - R[..., 4:63, 5]), "legal mask": (R[..., 4:63, 1] - R[..., 4:63, 6]),
+           "refill/final/autoreset": (R[..., 4:63, 7] - R[..., 4:63, 1]), "policy+prefetch+LDS": (R[..., 4:63, 2] - R[..., 4:63, 7])}
+    print("rules-wave sub-phases, steps 4..62, median/mean us: " + "; ".join(
+        f"{k} {np.median(us(v[ok])):.2f}/{us(v[ok]).mean():.2f}" for k, v in sub.items()))
     # per XCC (blockIdx % 8 is the XCC, checked above): where the rules wave's time goes
     rs = us(R[..., 4:63, 1] - R[..., 4:63, 0])  # [run, wg, step]
     tl = us(R[..., 4:63, 2] - R[..., 4:63, 1])
