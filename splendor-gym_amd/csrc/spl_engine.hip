@@ -119,7 +119,7 @@ __device__ uint64_t *g_rstamps;
     } while (0)
 // k_rollout_ws: both waves keep kWsStamps stamps per step in registers (lane k = step k, K <= 64),
 // written to g_wsstamps[workgroup][wave][step][kWsStamps] at the end.
-constexpr int kWsStamps = 8;  // 0-3 per step; 4-7 sub-phases of the rules wave
+constexpr int kWsStamps = 11;  // 0-3 per step; 4-10 sub-phases of the rules wave
 __device__ uint64_t *g_wsstamps;
 __device__ uint32_t *g_wshwid;  // [workgroup][wave][2]: HW_ID (SIMD, CU, SE) and XCC_ID of each wave
 __device__ uint64_t *g_wsclk;   // [workgroup][4]: s_memtime / s_memrealtime at the rules wave's start and end
@@ -578,44 +578,48 @@ __device__ __forceinline__ int predict_lut_key(const Pl &p, const int bank[6], i
 // exit is wave-uniform and the body predicated, so divergent rejection counts cost no nested
 // control flow.  Returns false if the lane needs more than the table's 40 outputs.
 __device__ __forceinline__ bool token_return_lut(Pl &p, int bank[6], int remaining, uint4 e) {
-    // the five non-gold counts as bytes of one 64-bit word each (player, bank)
-    uint64_t tk = 0, bk = 0;
+    // On this path the mover holds 11..13 tokens, so every count fits a nibble: `tk` holds the
+    // five non-gold counts, `list` the held colours in ascending order (CPython's `choices`
+    // list, rebuilt after every draw in the reference) and `n` its length.  A draw reads the
+    // r-th entry of the list; a colour that runs out is cut out of it.  All 32-bit ops.
+    uint32_t tk = 0, list = 0;
+    int n = 0;
 #pragma unroll
     for (int c = 0; c < 5; ++c) {
-        tk |= (uint64_t)(uint32_t)p.tok[c] << (8 * c);
-        bk |= (uint64_t)(uint32_t)bank[c] << (8 * c);
+        tk |= (uint32_t)p.tok[c] << (4 * c);
+        const bool has = p.tok[c] > 0;
+        list |= has ? (uint32_t)c << (4 * n) : 0u;
+        n += has ? 1 : 0;
     }
-    uint32_t held = 0;  // non-gold colours the player holds
+    bool active = remaining > 0 && n > 0;
+    // every lane draws at the same position, so the output word and bit offset are uniform
 #pragma unroll
-    for (int c = 0; c < 5; ++c) held |= (p.tok[c] > 0 ? 1u : 0u) << c;
-    int pos = 0;
-    bool active = remaining > 0 && held != 0u;
-    for (;;) {
-        active = active && pos < kLutOutputs;
-        if (!__any(active)) break;
-        const int nch = __popc(held);
-        const int kb = nch >= 4 ? 3 : (nch >= 2 ? 2 : 1);
-        const int q = (pos >= 10 ? 1 : 0) + (pos >= 20 ? 1 : 0) + (pos >= 30 ? 1 : 0);
+    for (int q = 0; q < 4; ++q) {
         const uint32_t w = q == 0 ? e.x : (q == 1 ? e.y : (q == 2 ? e.z : e.w));
-        const int r = (int)(__builtin_amdgcn_ubfe(w, 3u * (uint32_t)(pos - 10 * q), 3u) >> (3 - kb));
-        ++pos;
-        const bool acc = active && r < nch;
-        uint32_t h = held;  // drop the r lowest held colours: the r-th is the lowest left
-#pragma unroll
-        for (int i = 0; i < 4; ++i) h = i < r ? (h & (h - 1u)) : h;
-        const uint32_t c8 = 8u * (uint32_t)__builtin_ctz(h | 0x20u);
-        const uint64_t one = acc ? (1ull << c8) : 0ull;
-        tk -= one;
-        bk += one;
-        held &= (acc && ((tk >> c8) & 0xFFull) == 0ull) ? ~(1u << (c8 >> 3)) : 0xFFFFFFFFu;
-        remaining -= acc ? 1 : 0;
-        active = active && remaining > 0 && held != 0u;
+#pragma unroll 1
+        for (int j = 0; j < 10; ++j) {
+            if (!__any(active)) goto drawn;
+            // _randbelow(n): top bit_length(n) of the 3 stored bits; shift 3 - bit_length(n)
+            // for n = 1..5 is 2, 1, 1, 0, 0 (nibbles of 0x1120)
+            const uint32_t r = __builtin_amdgcn_ubfe(w, 3u * (uint32_t)j, 3u) >> ((0x1120u >> (4 * n)) & 15u);
+            const bool acc = active && (int)r < n;
+            const uint32_t c4 = 4u * __builtin_amdgcn_ubfe(list, 4u * r, 4u);  // nibble of the colour in tk
+            tk -= acc ? (1u << c4) : 0u;
+            const bool out = acc && ((tk >> c4) & 15u) == 0u;
+            const uint32_t low = (1u << (4u * r)) - 1u;  // cut entry r out of the list
+            list = out ? ((list & low) | ((list >> ((4u * r + 4u) & 31u)) << (4u * r))) : list;
+            n -= out ? 1 : 0;
+            remaining -= acc ? 1 : 0;
+            active = active && remaining > 0 && n > 0;
+        }
     }
-    if (remaining > 0 && held != 0u) return false;  // table outputs exhausted
+drawn:
+    if (remaining > 0 && n > 0) return false;  // table outputs exhausted
 #pragma unroll
     for (int c = 0; c < 5; ++c) {
-        p.tok[c] = (int)((tk >> (8 * c)) & 0xFFull);
-        bank[c] = (int)((bk >> (8 * c)) & 0xFFull);
+        const int now = (int)((tk >> (4 * c)) & 15u);
+        bank[c] += p.tok[c] - now;
+        p.tok[c] = now;
     }
     if (remaining > 0 && p.tok[5] > 0) {              // :179-184 then gold
         const int give = min(remaining, p.tok[5]);
@@ -719,10 +723,15 @@ __device__ __forceinline__ bool is_terminal(const uint32_t *sw) {
     return (sw[SW_MISC] & ST_GAME_OVER) && get_to_play(sw) == 0;
 }
 
+// sub-phase stamp hook of step_rules (diagnostic builds pass a stamping lambda)
+struct NoStamp {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+
 // engine/rules.py:196-287 apply_action on the current player (action known legal)
-template <int P>
+template <int P, class Stamp>
 __device__ __forceinline__ void apply_action(Tab<P> &T, int a, uint32_t top, const Consts &L, const uint4 *lut,
-                                             int pre_key, uint4 pre_e, uint32_t *mtx) {
+                                             int pre_key, uint4 pre_e, uint32_t *mtx, Stamp stamp) {
     uint32_t *sw = T.sw;
     const int tp = get_to_play(sw);
     uint32_t w[4];
@@ -779,8 +788,11 @@ __device__ __forceinline__ void apply_action(Tab<P> &T, int a, uint32_t top, con
         p.nres -= 1;
         pay_for_card(p, bank, card_rec(L, card));
     }
+    stamp(8);
     if (!abl(ABL_NOBLE)) grant_noble(sw, p, tp, L);                         // :260
+    stamp(9);
     if (!abl(ABL_TOKLIM)) enforce_token_limit(p, bank, get_turn(sw), tp, lut, pre_key, pre_e, mtx);  // :261
+    stamp(10);
     uint32_t misc = sw[SW_MISC];
     if (p.pres >= 15) misc |= ST_GAME_OVER;                                 // :264-265
     pack_pl(p, w);
@@ -1372,11 +1384,6 @@ struct StepOut {
 // envs/splendor_env.py:51-90 on the table in registers.  `known` (k_rollout after its first
 // step): `known_mask` is legal_moves of the table's current state, computed by the previous step,
 // so "any legal move?" and mask[action] need no re-evaluation.
-// sub-phase stamp hook of step_rules (diagnostic builds pass a stamping lambda)
-struct NoStamp {
-    __device__ __forceinline__ void operator()(int) const {}
-};
-
 template <int P, class Stamp = NoStamp>
 __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepPre &pre, bool valid, const Consts &L,
                                               const KTables &Tb, uint32_t *mtx, bool known = false,
@@ -1418,7 +1425,7 @@ __device__ __forceinline__ StepOut step_rules(Tab<P> &T, int action, const StepP
             } else {
                 STAMP(2);
                 stamp(4);
-                if (!abl(ABL_APPLY)) apply_action(T, action, pre.top, L, Tb.lut, pre.key, pre.e, mtx);  // :68
+                if (!abl(ABL_APPLY)) apply_action(T, action, pre.top, L, Tb.lut, pre.key, pre.e, mtx, stamp);  // :68
                 STAMP(3);
                 stamp(5);
                 o.term = is_terminal(T.sw);                       // :70

@@ -33,7 +33,7 @@ _native.check(e.lib, e.lib.spl_debug_set_ws_hwid(hw.data_ptr()))
 e.lib.spl_debug_set_ws_clk.argtypes = [ctypes.c_void_p]
 clk = torch.zeros((T // 64) * 4, dtype=torch.int64, device=e.device)
 _native.check(e.lib, e.lib.spl_debug_set_ws_clk(clk.data_ptr()))
-st = torch.zeros((T // 64) * 2 * 64 * 8, dtype=torch.int64, device=e.device)
+st = torch.zeros((T // 64) * 2 * 64 * 11, dtype=torch.int64, device=e.device)
 _native.check(e.lib, e.lib.spl_debug_set_ws_stamps(st.data_ptr()))
 store = None if inplace else dict(
     obs=torch.empty((K, T, 297), dtype=torch.int32, device=e.device),
@@ -48,7 +48,7 @@ for it in range(6):
     e.rollout(K, actions=buf[it & 1], next_actions=buf[(it & 1) ^ 1], policy_seed=1, ply=1 + K * it, out=store)
     if it >= 3:
         torch.cuda.synchronize()
-        out.append(st.view(-1, 2, 64, 8).cpu().numpy().tolist())
+        out.append(st.view(-1, 2, 64, 11).cpu().numpy().tolist())
         hws = hw.view(-1, 2, 2).cpu().numpy().tolist()
         clks = clk.view(-1, 4).cpu().numpy().tolist()
 print(json.dumps(clks))
@@ -129,7 +129,10 @@ def main():
     # rules-wave sub-phases (stamps 4-7; 4/5 only on lanes' steps that apply an action, so a
     # missing stamp reads as 0 and those steps are skipped)
     ok = (R[..., 4:63, 4] > 0) & (R[..., 4:63, 5] > 0) & (R[..., 4:63, 6] > 0)
+    ok = ok & (R[..., 4:63, 8] > 0) & (R[..., 4:63, 9] > 0) & (R[..., 4:63, 10] > 0)
     sub = {"pre (to apply)": (R[..., 4:63, 4] - R[..., 4:63, 0]), "apply": (R[..., 4:63, 5] - R[..., 4:63, 4]),
+           "  action": (R[..., 4:63, 8] - R[..., 4:63, 4]), "  noble": (R[..., 4:63, 9] - R[..., 4:63, 8]),
+           "  token limit": (R[..., 4:63, 10] - R[..., 4:63, 9]), "  end of turn": (R[..., 4:63, 5] - R[..., 4:63, 10]),
            "post (term/reward)": (R[..., 4:63, 6] - R[..., 4:63, 5]), "legal mask": (R[..., 4:63, 1] - R[..., 4:63, 6]),
            "refill/final/autoreset": (R[..., 4:63, 7] - R[..., 4:63, 1]), "policy+prefetch+LDS": (R[..., 4:63, 2] - R[..., 4:63, 7])}
     print("rules-wave sub-phases, steps 4..62, median/mean us: " + "; ".join(
