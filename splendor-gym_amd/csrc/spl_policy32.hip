@@ -4,7 +4,7 @@
 // critic Linear(297,256)-Tanh-Linear(256,256)-Tanh-Linear(256,{45|1}); masked_categorical sample,
 // log_prob, entropy, critic value; or the greedy masked argmax of training_utils.py:263-276), but
 // every product is an exact fp32 FMA: v_mfma_f32_16x16x4_f32 (fp32 in, fp32 accumulate — the chip's
-// fp32 matrix peak, bitwise an fmaf chain), tanh as the correctly rounded-to-2-ulp tanhf.  Logits and
+// fp32 matrix peak, bitwise an fmaf chain), tanh to a few ulp (tanh_f32).  Logits and
 // values therefore agree with torch's fp32 nn.Linear stack to summation-order rounding.
 //
 //   * a wave = 16 tables = the 16 columns of every 16x16x4 tile; a workgroup = 8 waves = 128 tables
@@ -22,6 +22,10 @@
 #include <stdint.h>
 
 #include <string>
+
+#ifndef SPL_TANH_LIBM
+#define SPL_TANH_LIBM 0
+#endif
 
 #include "../../include/splendor_amd.h"
 #include "../../include/splendor_policy.h"
@@ -118,6 +122,30 @@ struct ActArgs {
     int64_t image_stride;
 };
 
+// tanh in fp32 without branches (SPL_TANH_LIBM=1 restores libm tanhf).  |x| < 0.625:
+// x + x^3 P(x^2), a degree-4 fit in x^2 (<= 0.9 ulp in fp32 Horner, checked over [0, 0.625]);
+// otherwise 1 - 2 / (exp(2|x|) + 1) on v_exp_f32 / v_rcp_f32 (~1.5 ulp with correctly rounded
+// exp2 and rcp, a few ulp on the hardware's).  Both halves are evaluated and selected, so a
+// tile's 64 lanes never diverge and the VALU work stays in one block the scheduler can place
+// beside the next tile's MFMAs; libm tanhf is about twice the instructions and branches.
+__device__ __forceinline__ float tanh_f32(float x) {
+#if SPL_TANH_LIBM
+    return tanhf(x);
+#else
+    const float ax = __builtin_fabsf(x);
+    const float z = ax * ax;
+    float p = -0.005718891508877277f;
+    p = __builtin_fmaf(p, z, 0.02065306343138218f);
+    p = __builtin_fmaf(p, z, -0.053744640201330185f);
+    p = __builtin_fmaf(p, z, 0.13331513106822968f);
+    p = __builtin_fmaf(p, z, -0.3333328664302826f);
+    const float small = __builtin_fmaf(ax * z, p, ax);
+    const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);  // exp(2|x|)
+    const float big = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
+    return __builtin_copysignf(ax < 0.625f ? small : big, x);
+#endif
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
@@ -165,7 +193,7 @@ __device__ __forceinline__ void layer_tanh(Enter &enter, const float (&B)[NB], f
     for (int t = 0; t < kTiles; ++t) {
         const f32x4 acc = tile_mma<KS>(enter(), B, lane);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) H[4 * t + i] = tanhf(acc[i]);
+        for (int i = 0; i < 4; ++i) H[4 * t + i] = tanh_f32(acc[i]);
     }
 }
 
@@ -241,10 +269,10 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         for (int t = 0; t < kTiles; ++t) {
             const f32x4 acc = tile_mma<kKs2>(enter(), H1, lane);
             const float4 w = *reinterpret_cast<const float4 *>(a.critic_out + 16 * t + 4 * g);
-            value = __builtin_fmaf(w.x, tanhf(acc[0]), value);
-            value = __builtin_fmaf(w.y, tanhf(acc[1]), value);
-            value = __builtin_fmaf(w.z, tanhf(acc[2]), value);
-            value = __builtin_fmaf(w.w, tanhf(acc[3]), value);
+            value = __builtin_fmaf(w.x, tanh_f32(acc[0]), value);
+            value = __builtin_fmaf(w.y, tanh_f32(acc[1]), value);
+            value = __builtin_fmaf(w.z, tanh_f32(acc[2]), value);
+            value = __builtin_fmaf(w.w, tanh_f32(acc[3]), value);
         }
         value += __shfl_xor(value, 16);  // the other lane groups' units, then the bias
         value += __shfl_xor(value, 32);

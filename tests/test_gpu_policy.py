@@ -3,7 +3,7 @@
 
 fp32 kernel (the default, the reference's precision; exact fp32 products on v_mfma_f32_16x16x4_f32):
   * |logit - ref| <= 1e-5 * (|ref| + 1) and |value - ref| <= 1e-5 * (|ref| + 1) against the plain
-    fp32 module (what is left is summation order and tanhf vs torch's tanh, ~1e-7);
+    fp32 module (what is left is summation order and the kernel's few-ulp tanh vs torch's, ~1e-7);
   * greedy actions EQUAL torch's argmax on every row whose top two legal logits are more than
     1e-5 apart (closer pairs are ties at fp32 rounding: each side's sums round differently).
 

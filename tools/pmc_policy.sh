@@ -7,3 +7,19 @@ for grp in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_C
   timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $grp --kernel-include-regex "k_act" --output-format csv -d $O/p$i -o run -- python3 tools/bench_policy.py --fused-only --iters 5 > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
 done
 echo done
+python3 - <<'PY'
+import csv, glob, collections
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in sorted(glob.glob("gpurun_out/pmc_pol/p*/run_counter_collection.csv")):
+    per = collections.defaultdict(float)
+    for r in csv.DictReader(open(f)):
+        per[(r["Kernel_Name"].split("(")[0][-40:], r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+    for (k, d, c), v in per.items():
+        acc[k][c].append(v)
+for k, cs in acc.items():
+    m = {c: sum(v) / len(v) for c, v in cs.items()}
+    out = {c: round(v) for c, v in m.items()}
+    if m.get("GRBM_GUI_ACTIVE"):
+        out["mfma_busy_frac"] = round(m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (m["GRBM_GUI_ACTIVE"] / 8 * 256 * 4), 3) if "SQ_VALU_MFMA_BUSY_CYCLES" in m else None
+    print(k, out)
+PY
