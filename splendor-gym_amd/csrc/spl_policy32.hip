@@ -23,6 +23,9 @@
 
 #include <string>
 
+#ifndef SPL_AF_AHEAD
+#define SPL_AF_AHEAD 2
+#endif
 #ifndef SPL_TANH_LIBM
 #define SPL_TANH_LIBM 0
 #endif
@@ -174,16 +177,21 @@ __device__ __forceinline__ f32x4 tile_mma(const uint8_t *slot, const float (&B)[
     const float *bias = reinterpret_cast<const float *>(slot + kBiasOff) + 4 * (lane >> 4);
     f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
     const f32x4 *A = reinterpret_cast<const f32x4 *>(slot) + lane;
-    f32x4 af[2];
-    af[0] = A[0];
+    // A fragments SPL_AF_AHEAD groups ahead (a group's four MFMAs take ~128 cycles, about one LDS
+    // round trip with eight waves reading the ring)
+    constexpr int D = SPL_AF_AHEAD, NR = D + 1;
+    f32x4 af[NR];
+#pragma unroll
+    for (int q = 0; q < D; ++q) af[q] = A[q * 64];
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
-        if (q + 1 < NG) af[(q + 1) & 1] = A[(q + 1) * 64];
+        if (q + D < NG) af[(q + D) % NR] = A[(q + D) * 64];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[q & 1][j], B[4 * q + j], acc, 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[q % NR][j], B[4 * q + j], acc, 0, 0, 0);
         if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
+
 }
 
 // a hidden layer: 16 tiles, each tile's tanh is the next layer's B fragments 4t..4t+3
