@@ -191,7 +191,6 @@ __device__ __forceinline__ f32x4 tile_mma(const uint8_t *slot, const float (&B)[
         if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
-
 }
 
 // a hidden layer: 16 tiles, each tile's tanh is the next layer's B fragments 4t..4t+3
