@@ -417,12 +417,23 @@ __global__ __launch_bounds__(64) void k_group_scan(int G, int32_t *counts, int32
     gtab[2 * G + 1] = pos;
 }
 
+// Tables into their group's range of `order` (order within a group is irrelevant).  Ranks are
+// taken in LDS and each workgroup reserves its span of every group with ONE global atomic: one
+// global atomic per table on a dozen hot addresses serialises in L2 (about 0.3 ms for 65 536
+// tables over 13 groups).
 __global__ __launch_bounds__(256) void k_group_scatter(int n, int G, const int32_t *group_of, int32_t *cursor,
                                                        int32_t *order) {
+    __shared__ int32_t cnt[64], base[64];
+    if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+    __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int g = group_of[i];
-    if (g >= 0 && g < G) order[atomicAdd(&cursor[g], 1)] = i;  // order within a group is irrelevant
+    const int g = i < n ? group_of[i] : -1;
+    const bool in = g >= 0 && g < G;
+    const int rank = in ? atomicAdd(&cnt[g], 1) : 0;
+    __syncthreads();
+    if (threadIdx.x < G && cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
+    __syncthreads();
+    if (in) order[base[g] + rank] = i;
 }
 
 constexpr int kMaxGroups = 64;
