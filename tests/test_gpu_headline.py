@@ -6,7 +6,8 @@
     and a 256-table subset of the chain is replayed through the CPU oracle;
   * 4-player sharding invariance (two shards == one engine);
   * BASELINE config 5: batched self-play with the fused fp32 ActorCritic as agent AND opponent
-    (DualStepVectorEnv) equals the same loop driven by the torch fp32 module, table by table.
+    (DualStepVectorEnv) equals the same loop driven by the torch fp32 module, table by table —
+    with random-init networks and with the reference's trained checkpoint.
 Reference: scripts/random_rollout.py:13-28, envs/splendor_env.py:51-90, ppo_splendor.py:219-297."""
 import numpy as np
 import pytest
@@ -110,7 +111,8 @@ def test_sharded_equals_whole_4p():
     assert whole.download().tobytes() == np.concatenate([p.download() for p in parts]).tobytes()
 
 
-def test_selfplay_fused_fp32_actor_matches_torch():
+@pytest.mark.parametrize("weights", ["random", "trained"])
+def test_selfplay_fused_fp32_actor_matches_torch(weights):
     """Config 5 (ppo_splendor.py:219-297 with the frozen-opponent dual step): 4096 tables x 120
     dual steps, agent = greedy fused fp32 actor, opponent = greedy fused fp32 frozen actor, against
     the same loop with the torch fp32 modules.  Every table must match step for step (obs, masks,
@@ -125,6 +127,12 @@ def test_selfplay_fused_fp32_actor_matches_torch():
     torch.manual_seed(7)
     agent = ActorCritic().cuda().eval()
     opp = ActorCritic().cuda().eval()
+    if weights == "trained":  # the reference's checkpoint for both sides
+        import os
+        from safetensors.torch import load_file
+        sd = load_file(os.path.join(os.path.dirname(__file__), "golden", "ppo_splendor_latest.safetensors"), device="cuda")
+        agent.load_state_dict(sd)
+        opp.load_state_dict(sd)
     fa = FusedActorCritic(agent, with_critic=True)   # precision fp32
     fo = FusedActorCritic(opp, with_critic=False)
     rec = {}

@@ -36,10 +36,43 @@ def states(n, seed=5, plies=12):
 
 
 def model(seed=0, device="cuda"):
+    """Random-init ActorCritic, or (seed="trained") the reference's trained checkpoint
+    runs/ppo_splendor/ppo_splendor_latest.pt (tests/golden/ppo_splendor_latest.safetensors)."""
     import torch
     from splendor_gym.policy import ActorCritic
+    if seed == "trained":
+        import os
+        from safetensors.torch import load_file
+        m = ActorCritic().to(device).eval()
+        m.load_state_dict(load_file(os.path.join(os.path.dirname(__file__), "golden", "ppo_splendor_latest.safetensors"),
+                                    device=device))
+        return m
     torch.manual_seed(seed)
     return ActorCritic().to(device).eval()
+
+
+@pytest.mark.parametrize("n", [33, 4096])
+def test_trained_checkpoint_matches_torch_fp32(n):
+    """The reference's trained weights (config 5's actor): logits and values within the fp32
+    tolerance of the torch module, greedy actions equal wherever the top two legal logits are more
+    than 1e-5 apart, sampled actions legal."""
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic
+    _, obs, mask = states(max(n, 64), seed=13, plies=20)
+    obs, mask = obs[:n].contiguous(), mask[:n].contiguous()
+    m = model("trained")
+    full = FusedActorCritic(m, with_critic=True)
+    act, logits = full.greedy(obs, mask, want_logits=True)
+    with torch.no_grad():
+        ref = m.actor(obs.float())
+        vref = m.critic(obs.float())
+    assert fp32_close(logits, ref), (logits - ref).abs().max().item()
+    want, clear = greedy_clear(ref, mask, 1e-5)
+    assert torch.equal(act[clear], want[clear])
+    a, _, _, value = full.act(obs, mask, seed=2, ply=3)
+    assert fp32_close(value, vref), (value - vref).abs().max().item()
+    legal_any = mask.sum(dim=1) > 0
+    assert (mask[legal_any].gather(1, a[legal_any].long()[:, None]) != 0).all()
 
 
 def bf16_ref(seq, x):

@@ -37,6 +37,10 @@ def main():
                     help="pool: the reference's opponent_supplier (current policy p=0.25, else one of 12 frozen "
                          "snapshots, drawn per episode; fused fp32 grouped kernel); frozen: one frozen greedy actor")
     ap.add_argument("--pool-size", type=int, default=12)
+    ap.add_argument("--weights", choices=["trained", "random"], default="trained",
+                    help="trained: the reference's runs/ppo_splendor/ppo_splendor_latest.pt (committed as "
+                         "tests/golden/ppo_splendor_latest.safetensors) for agent, opponent and pool snapshots; "
+                         "random: random-init networks")
     args = ap.parse_args()
 
     import torch
@@ -50,8 +54,17 @@ def main():
     torch.cuda.set_device(dev)
     torch.manual_seed(1234 + rank)
     N = args.tables
-    agent = ActorCritic().to(dev).eval()
-    opp_model = ActorCritic().to(dev).eval()
+    ckpt = os.path.join(REPO, "tests", "golden", "ppo_splendor_latest.safetensors")
+
+    def net():
+        m = ActorCritic().to(dev).eval()
+        if args.weights == "trained":
+            from safetensors.torch import load_file
+            m.load_state_dict(load_file(ckpt, device=str(dev)))
+        return m
+
+    agent = net()
+    opp_model = net()
     fused = args.actor == "fused"
     if fused:
         prec = "bf16" if args.bf16 else "fp32"
@@ -60,8 +73,8 @@ def main():
             if args.bf16:
                 raise SystemExit("--opponent pool is fp32 (the grouped kernel); use --opponent frozen with --bf16")
             opponent = OpponentPool(agent, pool_size=args.pool_size, p_current=0.25, seed=99)
-            for _ in range(args.pool_size):  # distinct random-init snapshots stand in for trained ones
-                opponent.add_snapshot(ActorCritic().to(dev).eval())
+            for _ in range(args.pool_size):  # one snapshot image per slot (the one checkpoint, or random init)
+                opponent.add_snapshot(net())
         else:
             opponent = FusedActorCritic(opp_model, with_critic=False, precision=prec).opponent()
     else:
@@ -122,13 +135,15 @@ def main():
             "metric": f"env-steps/sec (whole node), 2p self-play with on-device ActorCritic actor, {N} tables/GPU",
             "value": round(steps / full, 1), "unit": "env-steps/s", "n_gpus": world, "iters": args.iters,
             "ms_per_dual_step": round(full / args.iters * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-            "dtype": "bf16" if args.bf16 else "fp32", "data": "synthetic: seeded deals, random-init ActorCritic",
+            "dtype": "bf16" if args.bf16 else "fp32", "data": ("synthetic: seeded deals; ActorCritic weights from the reference checkpoint "
+                     "runs/ppo_splendor/ppo_splendor_latest.pt (agent, opponent, every pool snapshot)"
+                     if args.weights == "trained" else "synthetic: seeded deals, random-init ActorCritic"),
             "config": {"workload": "PPO rollout step: ActorCritic.get_action_and_value + DualStepVectorEnv.dual_step "
                                    + ("(opponent pool: current policy p=0.25 else one of "
                                       f"{args.pool_size} frozen snapshots per episode, greedy; reset after done)"
                                       if fused and args.opponent == "pool" else
                                       "(greedy frozen-ActorCritic opponent, reset after done)"),
-                       "tables_per_gpu": N, "players": 2, "launch": "hipGraph replay" if graph is not None else "eager",
+                       "weights": args.weights, "tables_per_gpu": N, "players": 2, "launch": "hipGraph replay" if graph is not None else "eager",
                        "actor": (f"spl_policy_act (fused, {'bf16' if args.bf16 else 'fp32'} MFMA)" if fused
                                  else "torch nn.Module" + (" (bf16 autocast)" if args.bf16 else ""))},
             "env_only": {"value": round(steps / env_only, 1), "ms_per_dual_step": round(env_only / args.iters * 1e3, 4),

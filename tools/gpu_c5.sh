@@ -1,13 +1,11 @@
-#!/bin/bash
-# GPU session: full parity suite, then the config-5 self-play bench (fused actor) + kernel stats.
+# config 5 with the reference's trained checkpoint: tests + self-play bench (frozen and pool opponents)
 set -o pipefail
-TAG=${1:-c5}
-O=gpurun_out
-mkdir -p $O
-export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > $O/pytest_gpu_$TAG.log 2>&1 || { echo "tests failed"; tail -40 $O/pytest_gpu_$TAG.log; exit 1; }
-tail -1 $O/pytest_gpu_$TAG.log
-timeout -k 10 300 python tools/bench_selfplay.py > $O/sp_$TAG.json 2> $O/sp_$TAG.err || { tail -20 $O/sp_$TAG.err; exit 1; }
-cat $O/sp_$TAG.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof_sp_$TAG -o run -- python3 tools/bench_selfplay.py --iters 32 > $O/sp_prof_$TAG.json 2> $O/sp_prof_$TAG.err
-echo rc $?
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_policy.py tests/test_gpu_headline.py -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/c5_tests.log 2>&1 || { tail -30 gpurun_out/c5_tests.log; exit 1; }
+tail -1 gpurun_out/c5_tests.log
+for opp in frozen pool; do
+  timeout -k 10 300 python tools/bench_selfplay.py --opponent $opp > gpurun_out/sp_trained_$opp.json 2> gpurun_out/sp_err.txt || { tail -20 gpurun_out/sp_err.txt; exit 1; }
+  cut -c1-300 gpurun_out/sp_trained_$opp.json
+done
+timeout -k 10 300 python tools/bench_selfplay.py --opponent frozen --weights random > gpurun_out/sp_random_frozen.json 2> gpurun_out/sp_err.txt || { tail -20 gpurun_out/sp_err.txt; exit 1; }
+cut -c1-300 gpurun_out/sp_random_frozen.json
