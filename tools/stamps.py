@@ -80,6 +80,12 @@ def main():
         for i, nm in enumerate(names):
             col = m[:, i][~np.isnan(m[:, i])]
             print(f"{i:2d} {nm:26s} {np.median(col):10.2f} {np.percentile(col, 90):8.2f} {col.max():8.2f}")
+    if ws:  # per XCC (workgroup i runs on XCC i % 8): the rules wave's hand-off 1 and the output wave's end
+        wg = np.arange(a.shape[1] // 2) % 8
+        for title, idx, ph in (("rules: past hand-off 1", 0, 4), ("output: end", 1, len(WS_OUT) - 1)):
+            v = a[:, idx::2, ph]
+            print(f"{title} by XCC median/p99: " + " | ".join(
+                f"{np.nanmedian(v[:, wg == x]):.1f}/{np.nanpercentile(v[:, wg == x], 99):.1f}" for x in range(8)))
     return 0
 
 
