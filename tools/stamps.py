@@ -18,7 +18,7 @@ NAMES = ["start", "loaded+prefetched", "pre-apply", "applied", "step logic", "fi
 WS_RULES = ["start", "past hand-off 0", "rules done", "state to LDS (reset done)", "past hand-off 1", "legal mask",
             "end (mask, small outputs, state stored)"]
 WS_OUT = ["start", "tables staged", "past hand-off 0", "past hand-off 1", "final rows done", "encoded",
-          "obs stores issued", "end"]
+          "obs stores issued", "end", "early board stores issued"]
 
 CHILD = r'''
 import sys, os, ctypes, json
@@ -79,6 +79,8 @@ def main():
         print(f"{title}: {'phase':26s} {'median us':>10s} {'p90 us':>8s} {'max us':>8s}   ({len(m)} wave-samples)")
         for i, nm in enumerate(names):
             col = m[:, i][~np.isnan(m[:, i])]
+            if col.size == 0:
+                continue
             print(f"{i:2d} {nm:26s} {np.median(col):10.2f} {np.percentile(col, 90):8.2f} {col.max():8.2f}")
     if ws:  # per XCC (workgroup i runs on XCC i % 8): the rules wave's hand-off 1 and the output wave's end
         wg = np.arange(a.shape[1] // 2) % 8
