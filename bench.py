@@ -288,9 +288,11 @@ def main():
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         if graph is not None:
-            for _ in range(K // G):
+            ev = events(K // G)  # recorded on the replay stream around each replay, not as graph nodes
+            for i in range(K // G):
+                ev[0][i].record()
                 graph.replay()
-            ev = None
+                ev[1][i].record()
         else:
             ev = events(K // per)
             ply_base.fill_(k_base + W)
@@ -301,21 +303,26 @@ def main():
         terminations = int(ep_cnt.sum().item()) - eps0
         kt = "HIP events around each launch in the timed region"
         k_next = k_base + W + K + 1
-        if ev is None:
+        eager_s = None
+        if graph is not None:
             # ROCm rejects timing events as graph nodes ("External events are disallowed"), so the
-            # kernel duration comes from HIP events around each launch of an eager window of the
-            # same loop, run right after the timed replays on the same stream and state.
+            # per-launch time is each replay's event interval over its G launches (the graph's
+            # inter-kernel gaps included); HIP events around each launch of an eager window of the
+            # same loop, right after the timed replays, are reported beside it (they also bracket
+            # the host dispatch latency of a ~20 us kernel).
+            launch_s = sum(ev[0][i].elapsed_time(ev[1][i]) for i in range(len(ev[0]))) / (K // per) / 1e3
+            kt = f"HIP events around each of {K // G} hipGraph replays ({G // per} launches each) in the timed region"
             nwin = plan["unit"] * max(1, -(-64 // plan["unit"]))
             ev = events(nwin // per)
             ply_base.fill_(k_next)
             run(variant, 0, nwin, stream, ev)
             torch.cuda.synchronize(dev)
-            kt = f"HIP events around each of {nwin // per} eager launches right after the timed replays"
+            eager_s = sum(ev[0][i].elapsed_time(ev[1][i]) for i in range(len(ev[0]))) / len(ev[0]) / 1e3
             k_next += nwin + 1
-        nev = len(ev[0])
-        launch_s = sum(ev[0][i].elapsed_time(ev[1][i]) for i in range(nev)) / nev / 1e3
+        else:
+            launch_s = sum(ev[0][i].elapsed_time(ev[1][i]) for i in range(len(ev[0]))) / len(ev[0]) / 1e3
         return {"variant": variant, "plan": plan, "elapsed": elapsed, "launch_s": launch_s, "how": how,
-                "kernel_timing": kt, "terminations": terminations, "k_next": k_next}
+                "kernel_timing": kt, "terminations": terminations, "k_next": k_next, "eager_s": eager_s}
 
     headline = "step" if args.mode == "step" else ("rollout_store" if args.outputs == "store" else "rollout_inplace")
     variants = [headline]
@@ -357,7 +364,10 @@ def main():
                              "frac": round(achieved / HBM_PEAK_GBS, 4),
                              "frac_of_achievable": round(achieved / HBM_ACHIEVABLE_GBS, 4),
                              "kernel": kernel_name(v), "kernel_avg_us": round(rec["launch_s"] * 1e6, 2),
-                             "kernel_timing": rec["kernel_timing"], "algo_bytes_per_launch": round(algo),
+                             "kernel_timing": rec["kernel_timing"],
+                             **({} if rec["eager_s"] is None else
+                                {"eager_launch_us": round(rec["eager_s"] * 1e6, 2)}),
+                             "algo_bytes_per_launch": round(algo),
                              "algo_bytes_note": algo_note},
                 "launch": rec["how"], "plan": plan}
 
