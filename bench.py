@@ -173,6 +173,9 @@ def main():
     ap.add_argument("--pipeline", choices=("auto", "always", "half", "off"), default="auto",
                     help="rollout mode: two-wave pipelined kernel (auto: 32 or 64 tables per workgroup by grid "
                          "size; always: 64; half: 32) vs one wave per 64 tables (off)")
+    ap.add_argument("--delegation", type=int, default=None,
+                    help="rollout store: every n-th step the odd-XCC workgroups' rows are stored by their "
+                         "even-XCC partners (default: the library's, 6; 0 = off)")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,7 +201,7 @@ def main():
     table0 = rank * T
     pipe = {"auto": True, "always": "always", "half": "half", "off": False}[args.pipeline]
     eng = Engine(T, P, device=dev, refill_period=R, table0=table0, refill_fused=args.refill == "fused",
-                 pipeline=pipe)
+                 pipeline=pipe, delegation=args.delegation)
     eng.reset(seeds=range(table0, table0 + T))
     lib = eng.lib
     buf = [torch.zeros(T, dtype=torch.int32, device=dev) for _ in range(2)]
@@ -403,6 +406,7 @@ def main():
                        "tables_per_gpu": T, "players": P, "parallelism": f"table-sharded x{world}",
                        "refill_every": R, "refill": args.refill if headline != "step" else "separate",
                        "pipeline": args.pipeline, "rollout_steps_per_launch": RK, "variant": headline,
+                       "delegation": 6 if args.delegation is None else args.delegation,
                        "launch": main_s["launch"], "requested_steps": plan["requested_steps"],
                        "requested_warmup": plan["requested_warmup"],
                        "step_rounding": f"steps/warmup rounded up to whole units of {plan['unit']} (step_plan)"},

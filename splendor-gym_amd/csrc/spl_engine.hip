@@ -37,6 +37,8 @@ struct KArena {
     uint8_t *slots;    // [n][2][128] deck records
     uint8_t *pcg;      // [n][64] engine-seed streams
     int n;
+    uint8_t *deleg;    // [n/128][kDelegTasks][64 x 297] staged observation blocks (rollout-store delegation)
+    uint32_t *dflags;  // [n/128][kDelegFlagWords] its flags
 };
 
 struct KTables {
@@ -123,6 +125,7 @@ constexpr int kWsStamps = 11;  // 0-3 per step; 4-10 sub-phases of the rules wav
 __device__ uint64_t *g_wsstamps;
 __device__ uint32_t *g_wshwid;  // [workgroup][wave][2]: HW_ID (SIMD, CU, SE) and XCC_ID of each wave
 __device__ uint64_t *g_wsclk;   // [workgroup][4]: s_memtime / s_memrealtime at the rules wave's start and end
+__device__ uint64_t *g_wsend;   // [workgroup][2]: s_memrealtime at the output wave's last step and at its end
 #define WSHWID(wave)                                                                             \
     do {                                                                                         \
         if (g_wshwid && lane_id() == 0) {                                                        \
@@ -156,6 +159,9 @@ __device__ int g_stream_limit = MTStream::kMaxOut;
 #define SPL_SCRATCH_STRIDE 116
 #endif
 constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
+#ifndef SPL_DELEG_EVERY
+#define SPL_DELEG_EVERY 6  // rollout-store delegation period (spl_ctx_set_rollout_delegation)
+#endif
 #ifndef SPL_WS_PRIO
 #define SPL_WS_PRIO 1
 #endif
@@ -1995,6 +2001,63 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
     }
 }
 
+// Rollout-store delegation (k_rollout_ws<P, 64, true>, spl_ctx_set_rollout_delegation).  The
+// XCCs of an MI355X do not drain stores equally fast: with the rollout store's own write pattern
+// and nothing else running (tools/microbench_store_xcc.hip), workgroups on odd XCCs (odd blockIdx)
+// finish ~20 % after those on even XCCs, whichever addresses they write; in the kernel the slowest
+// XCC sets the launch time.  So workgroups pair up (2q on an even XCC, 2q+1 on the odd one next to
+// it), and on every `every`-th step the odd one stages its 64 encoded rows as bytes (19 KB, a
+// quarter of the 76 KB it would store) and its even partner, done with its own steps first,
+// expands and stores them into the rollout store.  Cross-XCC hand-off (the guide's valid form):
+// payload stored sc1 (write-through), the ready flag stored sc1 only after the payload has
+// completed, the consumer polls sc1 and loads the payload sc1 behind an agent-scope acquire.
+// Nothing waits unboundedly: a consumer that does not see a task within its time limit gives up,
+// and the producer stores every task whose `taken` flag it does not see itself (a row stored
+// twice is the same row).  Launch epochs live in the arena (each side counts its own launches),
+// so flags from earlier launches, graph replays included, never match.
+struct Deleg {
+    bool on, producer;
+    int pair, every;
+    uint32_t epoch;
+};
+__device__ __forceinline__ bool deleg_step(int k, int K, int every) {
+    return every > 0 && k % every == every / 2 - 1 && k + 2 < K && k / every < kDelegTasks;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7FFFFFF0, 0x00020000);
+}
+constexpr int kSc1 = 16;  // buffer-op aux bit: sc1 (write-through store / L1-bypassing load)
+__device__ __forceinline__ uint32_t flag_load(const uint32_t *f) {
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc_of(f), 0, 0, kSc1);
+}
+__device__ __forceinline__ void flag_store(uint32_t *f, uint32_t v) {  // lane 0 only
+    if (lane_id() == 0) __builtin_amdgcn_raw_buffer_store_b32(v, rsrc_of(f), 0, 0, kSc1);
+}
+// the wave's 64 staged rows (LDS bytes) -> a delegation slot, 16-byte sc1 stores
+__device__ __forceinline__ void stage_rows(const uint8_t *rows_lds, uint8_t *slot) {
+    const v4i *src = reinterpret_cast<const v4i *>(rows_lds);
+    const __amdgpu_buffer_rsrc_t r = rsrc_of(slot);
+    for (int q = lane_id(); q < kDelegPayload / 16; q += 64)
+        __builtin_amdgcn_raw_buffer_store_b128(src[q], r, q * 16, 0, kSc1);
+}
+// a delegation slot -> LDS rows (sc1 loads)
+__device__ __forceinline__ void unstage_rows(const uint8_t *slot, uint8_t *rows_lds) {
+    v4i *dst = reinterpret_cast<v4i *>(rows_lds);
+    const __amdgpu_buffer_rsrc_t r = rsrc_of(slot);
+    constexpr int kQ = kDelegPayload / 16;  // 1188
+    v4i v[(kQ + 63) / 64];
+#pragma unroll
+    for (int i = 0; i < (kQ + 63) / 64; ++i) {
+        const int q = lane_id() + 64 * i;
+        if (q < kQ) v[i] = __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r, q * 16, 0, kSc1));
+    }
+#pragma unroll
+    for (int i = 0; i < (kQ + 63) / 64; ++i) {
+        const int q = lane_id() + 64 * i;
+        if (q < kQ) dst[q] = v[i];
+    }
+}
+
 // TPW = tables per workgroup: 64, or 32 for grids too small to give every SIMD a wave (e.g. the
 // 32 768-table share of a 4-player 8-GPU run): twice the workgroups, lanes 32-63 idle.  The rules
 // work is latency-bound at one wave per SIMD, so half-populated waves on every SIMD finish a step
@@ -2002,7 +2065,7 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
 // kStore: per-step outputs (a [K][n][...] rollout store) or every step into the same [n][...] block;
 // a template argument so that the two variants are separate kernels in a profile.
 template <int P, int TPW, bool kStore>
-__global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep S, int K, int refill) {
+__global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep S, int K, int refill, int deleg_every) {
     static_assert(TPW == 64 || TPW == 32, "64 or 32 tables per workgroup");
     constexpr bool per_step = kStore;
     __shared__ WsLDS<P> L;
@@ -2112,6 +2175,21 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
 #ifdef SPL_STAMPS
         int rst_lo[kWsStamps] = {0}, rst_hi[kWsStamps] = {0};
 #endif
+        // delegation: both workgroups of a full pair take part (the same test on both sides)
+        Deleg dl{false, false, (int)(blockIdx.x >> 1), deleg_every, 0u};
+        if (TPW == 64 && kStore && deleg_every >= 4 && (int)(blockIdx.x | 1u) * 64 + 64 <= A.n) {
+            dl.on = true;
+            dl.producer = (blockIdx.x & 1u) != 0;
+            uint32_t *ep = A.dflags + (size_t)dl.pair * kDelegFlagWords + (dl.producer ? DF_PROD_EPOCH : DF_CONS_EPOCH) * kFlagLine;
+            dl.epoch = __builtin_amdgcn_readfirstlane(flag_load(ep)) + 1u;
+            flag_store(ep, dl.epoch);
+        }
+        uint32_t *const dflags = A.dflags + (size_t)dl.pair * kDelegFlagWords;
+        auto ready_flag = [&](int j) { return dflags + (DF_TASKS + 2 * j) * kFlagLine; };
+        auto taken_flag = [&](int j) { return dflags + (DF_TASKS + 2 * j + 1) * kFlagLine; };
+        auto slot_of = [&](int j) { return A.deleg + ((size_t)dl.pair * kDelegTasks + j) * kDelegPayload; };
+        int pend = -1, pend_k = -1;  // producer: task staged at step pend_k, ready flag not yet set
+        uint32_t staged = 0u;        // producer: tasks staged (not stored here)
         for (int k = 0; k < K; ++k) {
             ws_sync();  // hand-off of step k
             WSSTAMP(0, k);
@@ -2143,7 +2221,19 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
             wave_lds_sync();
             WSSTAMP(1, k);
             int32_t *obs = S.obs + blk * kObsDim;
-            if (abl(ABL_OBS_STORE)) {
+            const bool big_moves = __any(valid && get_moves(T.sw) > 255);
+            if (dl.producer && deleg_step(k, K, dl.every)) {
+                const int j = k / dl.every;
+                if (big_moves) {  // a patched row: stored here, the partner skips the task
+                    store_obs_block<TPW, true>(L.rows, rows, obs + (size_t)t0 * kObsDim);
+                    flag_store(ready_flag(j), dl.epoch << 1 | 1u);
+                } else {
+                    stage_rows(L.rows, slot_of(j));
+                    staged |= 1u << j;
+                    pend = j;
+                    pend_k = k;
+                }
+            } else if (abl(ABL_OBS_STORE)) {
             } else if (per_step) {
                 store_obs_block<TPW, true>(L.rows, rows, obs + (size_t)t0 * kObsDim);
             } else {
@@ -2167,12 +2257,65 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
                     if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
                 }
             }
-            if (__any(valid && get_moves(T.sw) > 255)) {
+            if (big_moves) {
                 __builtin_amdgcn_s_waitcnt(0);
                 if (valid && get_moves(T.sw) > 255) obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
             }
+            if (pend >= 0 && k == pend_k + 2) {
+                // two steps of block stores (> 63 vector-memory instructions, the counter's
+                // limit) were issued after the staged rows, so they have completed; the wait
+                // states it for the ready flag's sake
+                asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+                flag_store(ready_flag(pend), dl.epoch << 1);
+                pend = -1;
+            }
             WSSTAMP(3, k);
         }
+#ifdef SPL_STAMPS
+        if (g_wsend && lane == 0) g_wsend[blockIdx.x * 2 + 0] = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (dl.on && !dl.producer) {
+            // consumer: the partner's staged blocks, each as soon as its ready flag shows
+            const int64_t pt0 = (int64_t)(blockIdx.x + 1) * 64;
+            const uint64_t limit = 200000;  // 2 ms of s_memrealtime (100 MHz) per task at most
+            for (int k = 0; k < K; ++k) {
+                if (!deleg_step(k, K, dl.every)) continue;
+                const int j = k / dl.every;
+                uint32_t f = 0;
+                const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    f = __builtin_amdgcn_readfirstlane(flag_load(ready_flag(j)));
+                    if ((f >> 1) == dl.epoch || __builtin_amdgcn_s_memrealtime() - t_start > limit) break;
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                if ((f >> 1) != dl.epoch) break;  // not seen in time: the producer stores the rest
+                if (f & 1u) continue;              // the producer stored it
+                flag_store(taken_flag(j), dl.epoch);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                unstage_rows(slot_of(j), L.rows);
+                wave_lds_sync();
+                store_obs_block<TPW, true>(L.rows, 64, S.obs + ((size_t)k * (size_t)A.n + pt0) * kObsDim);
+                wave_lds_sync();  // the block's LDS reads are done before the next task's rows land
+            }
+        }
+        if (dl.producer && staged) {
+            // producer: every staged block whose taken flag is not visible is stored here
+            for (int j = 0; j < kDelegTasks; ++j) {
+                if (!((staged >> j) & 1u)) continue;
+                const int k = j * dl.every + dl.every / 2 - 1;
+                if (__builtin_amdgcn_readfirstlane(flag_load(taken_flag(j))) == dl.epoch) continue;
+                unstage_rows(slot_of(j), L.rows);
+                wave_lds_sync();
+                store_obs_block<TPW, true>(L.rows, 64, S.obs + ((size_t)k * (size_t)A.n + t0) * kObsDim);
+                wave_lds_sync();
+            }
+        }
+#ifdef SPL_STAMPS
+        if (g_wsend) {
+            __builtin_amdgcn_s_waitcnt(0);  // this wave's stores have completed
+            if (lane == 0) g_wsend[blockIdx.x * 2 + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
 #ifdef SPL_STAMPS
         if (g_wsstamps && lane < K)
             for (int i = 0; i < kWsStamps; ++i)
@@ -2441,6 +2584,7 @@ struct spl_ctx_s {
     int refill_fused;  // spl_rollout: refill inside the rollout launch (default) or as a k_refill launch after it
     int pipeline;      // spl_rollout: 0 one wave per 64 tables, 1 two-wave (auto tables per workgroup), 2 / 3 two-wave at 64 / 32
     int ws_resident[5];  // k_rollout_ws<P>: workgroups resident per device (occupancy x CUs), index P
+    int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
     void *stage;
     size_t stage_bytes;
 };
@@ -2476,7 +2620,7 @@ static KArena karena(const spl_arena_t *a) {
     const ArenaLayout L = arena_layout(a->n, a->players);
     uint8_t *b = static_cast<uint8_t *>(a->base);
     return KArena{reinterpret_cast<uint32_t *>(b + L.planes), reinterpret_cast<uint32_t *>(b + L.pool), b + L.slots,
-                  b + L.pcg, a->n};
+                  b + L.pcg, a->n, b + L.deleg, reinterpret_cast<uint32_t *>(b + L.dflags)};
 }
 
 static int launch_check() {
@@ -2506,6 +2650,10 @@ int spl_debug_set_stamps(void *buf) {
 }
 int spl_debug_set_ws_clk(void *buf) {
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wsclk), &buf, sizeof(buf)));
+    return SPL_OK;
+}
+int spl_debug_set_ws_end(void *buf) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_wsend), &buf, sizeof(buf)));
     return SPL_OK;
 }
 int spl_debug_set_ws_hwid(void *buf) {
@@ -2600,6 +2748,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     c->device = device;
     c->refill_period = 64;
     c->refill_fused = 1;
+    c->deleg_every = SPL_DELEG_EVERY;
     c->pipeline = 1;
     memcpy(c->ws_resident, ws_resident, sizeof(ws_resident));
     if (hipMalloc(&c->cards, sizeof(uint4) * 90) != hipSuccess || hipMalloc(&c->nobles, sizeof(uint2) * 10) != hipSuccess ||
@@ -2639,6 +2788,12 @@ int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on) {
     if (!ctx) return fail(SPL_E_ARG, "null ctx");
     if (on < 0 || on > 3) return fail(SPL_E_ARG, "rollout pipeline must be 0..3");
     ctx->pipeline = on;
+    return SPL_OK;
+}
+
+int spl_ctx_set_rollout_delegation(spl_ctx_t *ctx, int every) {
+    if (!ctx || every < 0 || (every > 0 && every < 4)) return fail(SPL_E_ARG, "delegation period must be 0 or >= 4");
+    ctx->deleg_every = every;
     return SPL_OK;
 }
 
@@ -2800,10 +2955,10 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
 #define SPL_LAUNCH_WS(TPW, BLOCKS)                                                                           \
     DISPATCH_P(arena->players, if (p_out) {                                                                  \
         hipLaunchKernelGGL((k_rollout_ws<PP, TPW, true>), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
-                           (int)steps, fused);                                                               \
+                           (int)steps, fused, ctx->deleg_every);                                             \
     } else {                                                                                                 \
         hipLaunchKernelGGL((k_rollout_ws<PP, TPW, false>), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
-                           (int)steps, fused);                                                               \
+                           (int)steps, fused, 0);                                                            \
     })
     if (tpw == 64) {
         SPL_LAUNCH_WS(64, blocks_for(arena->n));

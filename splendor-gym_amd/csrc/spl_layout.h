@@ -71,8 +71,18 @@ constexpr int kLutTc = 128, kLutTp = 4, kLutSt = 3, kLutSb = 16;
 constexpr int kLutEntries = kLutTc * kLutTp * kLutSt * kLutSb;
 constexpr int kLutOutputs = 40;  // top 3 bits of the first 40 MT outputs, 10 per word
 
+// Rollout-store delegation (k_rollout_ws at 64 tables per workgroup with per-step outputs; see
+// the kernel): per pair of workgroups (2q, 2q+1), kDelegTasks staged 64-row observation blocks
+// (the odd workgroup's LDS bytes, 64 x 297 B) and the flags, one 128-byte line each: the two
+// workgroups' launch counters, then ready and taken per task.
+constexpr int kDelegTasks = 16;
+constexpr int kDelegPayload = 64 * 297;  // 19 008 B
+constexpr int kFlagLine = 32;            // u32 words per flag
+enum : int { DF_PROD_EPOCH = 0, DF_CONS_EPOCH = 1, DF_TASKS = 2 };  // + 2 * task + {0 ready, 1 taken}
+constexpr int kDelegFlagWords = (DF_TASKS + 2 * kDelegTasks) * kFlagLine;
+
 struct ArenaLayout {
-    int64_t planes, pool, slots, pcg, total;
+    int64_t planes, pool, slots, pcg, deleg, dflags, total;
 };
 
 __host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
@@ -83,7 +93,9 @@ __host__ __device__ inline ArenaLayout arena_layout(int64_t n, int P) {
     L.pool = align256(L.planes + (int64_t)num_words(P) * n * 4);
     L.slots = align256(L.pool + (int64_t)PL_COUNT * n * 4);
     L.pcg = align256(L.slots + n * kSlotRecords * kSlotBytes);
-    L.total = align256(L.pcg + n * kPcgBytes);
+    L.deleg = align256(L.pcg + n * kPcgBytes);
+    L.dflags = align256(L.deleg + (n / 128) * kDelegTasks * (int64_t)kDelegPayload);
+    L.total = align256(L.dflags + (n / 128) * kDelegFlagWords * 4);
     return L;
 }
 

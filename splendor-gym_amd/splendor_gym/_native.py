@@ -85,6 +85,7 @@ SIGNATURES = {
     "spl_ctx_set_refill_period": ([c_void_p, c_int32], c_int32),
     "spl_ctx_set_refill_fused": ([c_void_p, c_int32], c_int32),
     "spl_ctx_set_rollout_pipeline": ([c_void_p, c_int32], c_int32),
+    "spl_ctx_set_rollout_delegation": ([c_void_p, c_int32], c_int32),
     "spl_ctx_token_lut": ([c_void_p, c_void_p, c_int64], c_int64),
     "spl_arena_bytes": ([c_int32, c_int32], c_int64),
     "spl_arena_init": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p], c_int32),

@@ -31,7 +31,7 @@ class Engine:
     DEFAULT_REFILL = {2: 64, 3: 32, 4: 16}
 
     def __init__(self, num_tables, num_players=2, device=None, refill_period=None, table0=0, refill_fused=True,
-                 pipeline=True):
+                 pipeline=True, delegation=None):
         torch = _native.require_gpu()
         self.torch = torch
         self.lib = _native.load_library()
@@ -57,6 +57,10 @@ class Engine:
         # rollout(): two-wave pipelined kernel or one wave per 64 tables; same results
         pipe = {"always": 2, "half": 3}.get(pipeline, 1 if pipeline else 0)
         check(self.lib, self.lib.spl_ctx_set_rollout_pipeline(self.ctx, pipe))
+        # rollout() into a per-step store: every n-th step the odd-XCC workgroups' rows are stored by
+        # their even-XCC partners (None = the library default, 0 = off); same results
+        if delegation is not None:
+            check(self.lib, self.lib.spl_ctx_set_rollout_delegation(self.ctx, int(delegation)))
         nbytes = int(self.lib.spl_arena_bytes(self.n, self.P))
         dev = self.device
         self._arena_raw = torch.zeros(nbytes + 256, dtype=torch.uint8, device=dev)

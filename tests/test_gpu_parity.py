@@ -328,6 +328,74 @@ def test_rollout_mass_termination_and_long_games(pipeline):
     assert chain.download().tobytes() == roll.download().tobytes()
 
 
+def test_rollout_store_delegation_equals_undelegated():
+    """Rollout-store delegation (the odd workgroup of each pair hands every 4th step's rows to its
+    even partner; spl_ctx_set_rollout_delegation) changes nothing: 11 workgroups (five pairs and an
+    unpaired last one), crafted tables with move_count > 255 (their delegated steps are stored by
+    the producer itself), several eager launches, then hipGraph replays of one captured launch
+    (launch epochs counted on the device), against the same rollouts without delegation."""
+    import torch
+    n, K, seed, R = 64 * 11, 24, 3, 8
+    ref = engine(n, 2, refill_period=R, pipeline="always", delegation=0)
+    dlg = engine(n, 2, refill_period=R, pipeline="always", delegation=4)
+    ref.reset(seeds=range(n))
+    dlg.reset(seeds=range(n))
+    recs = ref.download()
+    big = np.arange(n) % 5 == 0
+    recs["move_count"] = np.where(big, 300 + 2 * (recs["move_count"] % 2), recs["move_count"])
+    ref.upload(recs)
+    dlg.upload(recs)
+    dev = ref.device
+    a_r = torch.zeros(n, dtype=torch.int32, device=dev)
+    ref.sample_uniform(out=a_r, seed=seed, ply=0)
+    a_d = a_r.clone()
+
+    def outs():
+        return {"obs": torch.full((K, n, 297), -1, dtype=torch.int32, device=dev),
+                "mask": torch.empty((K, n, 45), dtype=torch.int8, device=dev),
+                "reward": torch.empty((K, n), dtype=torch.float32, device=dev),
+                "terminated": torch.empty((K, n), dtype=torch.uint8, device=dev),
+                "flags": torch.empty((K, n), dtype=torch.uint8, device=dev),
+                "winner": torch.empty((K, n), dtype=torch.int8, device=dev),
+                "final_obs": torch.zeros((K, n, 297), dtype=torch.int32, device=dev)}
+
+    def same(o_r, o_d, tag):
+        for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
+            assert torch.equal(o_r[name], o_d[name]), (tag, name)
+        term = o_r["terminated"].bool()
+        assert torch.equal(o_r["final_obs"][term], o_d["final_obs"][term]), tag
+
+    saw_big = False
+    for launch in range(3):
+        o_r, o_d = outs(), outs()
+        na_r, na_d = torch.empty_like(a_r), torch.empty_like(a_d)
+        ref.rollout(K, actions=a_r, next_actions=na_r, policy_seed=seed, ply=1 + K * launch, out=o_r)
+        dlg.rollout(K, actions=a_d, next_actions=na_d, policy_seed=seed, ply=1 + K * launch, out=o_d)
+        same(o_r, o_d, launch)
+        saw_big = saw_big or bool((o_r["obs"][:, :, 295] > 255).any())
+        assert torch.equal(na_r, na_d)
+        a_r, a_d = na_r, na_d
+    assert saw_big  # the producer's own-store path ran
+    assert ref.download().tobytes() == dlg.download().tobytes()
+    # graph replays of one captured launch: the kernel arguments repeat, the epochs do not
+    o_d, na_d = outs(), torch.empty_like(a_d)
+    torch.cuda.synchronize(dev)
+    side = torch.cuda.Stream(dev)
+    with torch.cuda.stream(side):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            dlg.rollout(K, actions=a_d, next_actions=na_d, policy_seed=seed, ply=500, out=o_d)
+    for rep in range(2):
+        o_d["obs"].fill_(-1)
+        g.replay()
+        o_r, na_r = outs(), torch.empty_like(a_r)
+        ref.rollout(K, actions=a_r, next_actions=na_r, policy_seed=seed, ply=500, out=o_r)
+        torch.cuda.synchronize(dev)
+        same(o_r, o_d, ("replay", rep))
+        a_r.copy_(na_r)
+        a_d.copy_(na_d)
+
+
 def test_dual_step_vector_env_matches_per_env_wrappers():
     """DualStepVectorEnv (fused device greedy_v1 opponent) == per-env DualStepNativeWrapper over
     SplendorEnv with the host greedy_opponent_v1, including the PPO loop's reset after done."""

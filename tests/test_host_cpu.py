@@ -82,9 +82,11 @@ def test_arena_layout_sizes():
         for P in (2, 3, 4):
             words = 9 + 4 * P
             b = int(lib.spl_arena_bytes(n, P))
-            # state planes + 5 pool planes + 4 deck slot records x 128 B + 64 B PCG record, 256-aligned
-            assert b >= (words + 5) * 4 * n + 512 * n + 64 * n
-            assert b % 256 == 0 and b <= (words + 5) * 4 * n + 576 * n + 4 * 256
+            # state planes + 5 pool planes + 4 deck slot records x 128 B + 64 B PCG record, then per pair
+            # of 64-table workgroups 8 staged 64-row blocks and 18 flag lines (rollout-store delegation)
+            deleg = (n // 128) * (16 * 64 * 297 + 34 * 128)
+            assert b >= (words + 5) * 4 * n + 512 * n + 64 * n + deleg
+            assert b % 256 == 0 and b <= (words + 5) * 4 * n + 576 * n + deleg + 6 * 256
 
 
 def test_table_dtype_matches_oracle_struct():

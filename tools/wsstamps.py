@@ -33,6 +33,12 @@ _native.check(e.lib, e.lib.spl_debug_set_ws_hwid(hw.data_ptr()))
 e.lib.spl_debug_set_ws_clk.argtypes = [ctypes.c_void_p]
 clk = torch.zeros((T // 64) * 4, dtype=torch.int64, device=e.device)
 _native.check(e.lib, e.lib.spl_debug_set_ws_clk(clk.data_ptr()))
+wend = torch.zeros((T // 64) * 2, dtype=torch.int64, device=e.device)
+e.lib.spl_debug_set_ws_end.argtypes = [ctypes.c_void_p]  # a 64-bit pointer, not a C int
+_native.check(e.lib, e.lib.spl_debug_set_ws_end(wend.data_ptr()))
+deleg = os.environ.get("WS_DELEG")
+if deleg is not None:
+    _native.check(e.lib, e.lib.spl_ctx_set_rollout_delegation(e.ctx, int(deleg)))
 st = torch.zeros((T // 64) * 2 * 64 * 11, dtype=torch.int64, device=e.device)
 _native.check(e.lib, e.lib.spl_debug_set_ws_stamps(st.data_ptr()))
 store = None if inplace else dict(
@@ -51,6 +57,8 @@ for it in range(6):
         out.append(st.view(-1, 2, 64, 11).cpu().numpy().tolist())
         hws = hw.view(-1, 2, 2).cpu().numpy().tolist()
         clks = clk.view(-1, 4).cpu().numpy().tolist()
+        ends = wend.view(-1, 2).cpu().numpy().tolist()
+print(json.dumps(ends))
 print(json.dumps(clks))
 print(json.dumps(hws))
 print(json.dumps(out))
@@ -80,6 +88,7 @@ def main():
     runs = np.array(json.loads(r.stdout.strip().splitlines()[-1]), dtype=np.int64)  # [run, wg, wave, step, 4]
     hws = np.array(json.loads(r.stdout.strip().splitlines()[-2]), dtype=np.int64)  # [wg, wave, 2] (last launch)
     clks = np.array(json.loads(r.stdout.strip().splitlines()[-3]), dtype=np.float64)  # [wg, 4]
+    ends = np.array(json.loads(r.stdout.strip().splitlines()[-4]), dtype=np.float64)  # [wg, 2] (last launch)
     ghz = (clks[:, 2] - clks[:, 0]) / ((clks[:, 3] - clks[:, 1]) * 10.0)  # s_memtime ticks per ns
     us = lambda x: x * 0.01  # 100 MHz ticks
     t0 = runs[:, :, 0, 0, 0].min(axis=1)[:, None, None]
@@ -155,6 +164,15 @@ def main():
     worst = np.argmax(np.array([us(R[..., k, 2] - R[..., k, 0])[slow].mean() for k in range(64)]))
     print(f"slowest-1% WGs: per-step rules busy at k={worst}: {us(R[..., worst, 2] - R[..., worst, 0])[slow].mean():.1f} us; "
           f"sum of per-step periods excluding the max step {np.sort(us(np.diff(R[..., :, 0], axis=-1))[slow], axis=-1)[:, :-1].sum(axis=-1).mean():.0f} us")
+    # output waves of the last launch: last step issued, and the wave's end (delegated blocks included,
+    # its stores completed)
+    e0 = runs[-1, :, 0, 0, 0].min()
+    le, fe = us(ends[:, 0] - e0), us(ends[:, 1] - e0)
+    wgx = np.arange(len(fe)) % 8
+    print("output wave, last launch: last step issued mean/max %.0f/%.0f us; wave end (stores done) mean/p99/max "
+          "%.0f/%.0f/%.0f us" % (le.mean(), le.max(), fe.mean(), np.percentile(fe, 99), fe.max()))
+    print("  wave end mean by blockIdx %% 8: " + " ".join(f"{fe[wgx == x].mean():.0f}" for x in range(8)))
+    print("  last step mean by blockIdx %% 8: " + " ".join(f"{le[wgx == x].mean():.0f}" for x in range(8)))
     return 0
 
 
