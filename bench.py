@@ -288,21 +288,29 @@ def main():
         torch.cuda.synchronize(dev)
         eps0 = int(ep_cnt.sum().item())
         barrier(dev)
+        ev = events(K // G) if graph is not None else events(K // per)
+        if graph is None:
+            ply_base.fill_(k_base + W)
+        for e in ev[0] + ev[1]:  # the HIP events are created on first record: outside the timed region
+            e.record()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         if graph is not None:
-            ev = events(K // G)  # recorded on the replay stream around each replay, not as graph nodes
+            # recorded on the replay stream around each replay, not as graph nodes
             for i in range(K // G):
                 ev[0][i].record()
                 graph.replay()
                 ev[1][i].record()
         else:
-            ev = events(K // per)
-            ply_base.fill_(k_base + W)
             run(variant, 0, K, stream, ev)
+        t_enq = time.perf_counter()
         torch.cuda.synchronize(dev)
+        t_sync = time.perf_counter()
         barrier(dev)
         elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
+        span = ev[0][0].elapsed_time(ev[1][-1]) / 1e3
+        print(f"[{variant}] timed region: wall {(t_sync - t0) * 1e3:.3f} ms (host enqueue "
+              f"{(t_enq - t0) * 1e3:.3f} ms), GPU span first->last event {span * 1e3:.3f} ms", file=sys.stderr)
         terminations = int(ep_cnt.sum().item()) - eps0
         kt = "HIP events around each launch in the timed region"
         k_next = k_base + W + K + 1
