@@ -29,6 +29,11 @@
 #ifndef SPL_TANH_LIBM
 #define SPL_TANH_LIBM 0
 #endif
+// timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
+// streaming, no per-tile barrier), 4 A fragments loaded once per tile (no per-group LDS reads)
+#ifndef SPL_POL_ABL
+#define SPL_POL_ABL 0
+#endif
 
 #include "../../include/splendor_amd.h"
 #include "../../include/splendor_policy.h"
@@ -132,7 +137,9 @@ struct ActArgs {
 // tile's 64 lanes never diverge and the VALU work stays in one block the scheduler can place
 // beside the next tile's MFMAs; libm tanhf is about twice the instructions and branches.
 __device__ __forceinline__ float tanh_f32(float x) {
-#if SPL_TANH_LIBM
+#if SPL_POL_ABL & 1
+    return x;
+#elif SPL_TANH_LIBM
     return tanhf(x);
 #else
     const float ax = __builtin_fabsf(x);
@@ -185,9 +192,9 @@ __device__ __forceinline__ f32x4 tile_mma(const uint8_t *slot, const float (&B)[
     for (int q = 0; q < D; ++q) af[q] = A[q * 64];
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
-        if (q + D < NG) af[(q + D) % NR] = A[(q + D) * 64];
+        if (!(SPL_POL_ABL & 4) && q + D < NG) af[(q + D) % NR] = A[(q + D) * 64];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[q % NR][j], B[4 * q + j], acc, 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[(SPL_POL_ABL & 4) ? q % D : q % NR][j], B[4 * q + j], acc, 0, 0, 0);
         if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
@@ -254,6 +261,13 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
 
     int c = 0;
     auto enter = [&]() -> const uint8_t * {
+#if SPL_POL_ABL & 2
+        if (c++ == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        return ring;
+#endif
         // this wave's part of chunk c landed (later chunks' loads may stay outstanding)
         if (wave < kChunkBlocks - 2 * kWaves) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
