@@ -124,7 +124,7 @@ int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused);
  * identical in every mode. */
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
 /* spl_rollout with per_step_outputs at 64 tables per workgroup only: rollout-store delegation.  On
- * every `every`-th step (every >= 4; default 8) each workgroup on an odd XCC hands its encoded rows
+ * every `every`-th step (every >= 4; default 6) each workgroup on an odd XCC hands its encoded rows
  * (19 KB of bytes instead of 76 KB of int32) to its partner on the neighbouring even XCC, which
  * stores them after its own steps: MI355X's odd XCCs drain stores ~20 % slower, and the slowest
  * sets the launch time.  0 disables it.  Results are identical either way. */
