@@ -2006,9 +2006,11 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
 // and nothing else running (tools/microbench_store_xcc.hip), workgroups on odd XCCs (odd blockIdx)
 // finish ~20 % after those on even XCCs, whichever addresses they write; in the kernel the slowest
 // XCC sets the launch time.  So workgroups pair up (2q on an even XCC, 2q+1 on the odd one next to
-// it), and on every `every`-th step the odd one stages its 64 encoded rows as bytes (19 KB, a
-// quarter of the 76 KB it would store) and its even partner, done with its own steps first,
-// expands and stores them into the rollout store.  Cross-XCC hand-off (the guide's valid form):
+// it), and on every `every`-th step the odd one stages its 64 tables' state words after the step
+// (4.3 KB at 2 players, against the 76 KB block it would store; it skips that step's encode) and
+// its even partner, done with its own steps first, encodes and stores the rows into the rollout
+// store (staging the encoded rows as bytes, 19 KB a block, measured ~1 % slower and moved 0.06 GB
+// more per launch).  Cross-XCC hand-off (the guide's valid form):
 // payload stored sc1 (write-through), the ready flag stored sc1 only after the payload has
 // completed, the consumer polls sc1 and loads the payload sc1 behind an agent-scope acquire.
 // Nothing waits unboundedly: a consumer that does not see a task within its time limit gives up,
@@ -2033,29 +2035,25 @@ __device__ __forceinline__ uint32_t flag_load(const uint32_t *f) {
 __device__ __forceinline__ void flag_store(uint32_t *f, uint32_t v) {  // lane 0 only
     if (lane_id() == 0) __builtin_amdgcn_raw_buffer_store_b32(v, rsrc_of(f), 0, 0, kSc1);
 }
-// the wave's 64 staged rows (LDS bytes) -> a delegation slot, 16-byte sc1 stores
-__device__ __forceinline__ void stage_rows(const uint8_t *rows_lds, uint8_t *slot) {
-    const v4i *src = reinterpret_cast<const v4i *>(rows_lds);
+// a delegated step: the wave's 64 tables' state words after the step -> a delegation slot
+// ([word][lane], 256 contiguous bytes per word), sc1 (write-through) dword stores
+template <int P>
+__device__ __forceinline__ void stage_state(const Tab<P> &T, uint8_t *slot) {
     const __amdgpu_buffer_rsrc_t r = rsrc_of(slot);
-    for (int q = lane_id(); q < kDelegPayload / 16; q += 64)
-        __builtin_amdgcn_raw_buffer_store_b128(src[q], r, q * 16, 0, kSc1);
+#pragma unroll
+    for (int w = 0; w < num_words(P); ++w)
+        __builtin_amdgcn_raw_buffer_store_b32(tab_word(T, w), r, (w * 64 + lane_id()) * 4, 0, kSc1);
 }
-// a delegation slot -> LDS rows (sc1 loads)
-__device__ __forceinline__ void unstage_rows(const uint8_t *slot, uint8_t *rows_lds) {
-    v4i *dst = reinterpret_cast<v4i *>(rows_lds);
+// a delegation slot -> the staged tables' state (sc1 loads)
+template <int P>
+__device__ __forceinline__ void unstage_state(const uint8_t *slot, Tab<P> &T) {
     const __amdgpu_buffer_rsrc_t r = rsrc_of(slot);
-    constexpr int kQ = kDelegPayload / 16;  // 1188
-    v4i v[(kQ + 63) / 64];
+    uint32_t v[num_words(P)];
 #pragma unroll
-    for (int i = 0; i < (kQ + 63) / 64; ++i) {
-        const int q = lane_id() + 64 * i;
-        if (q < kQ) v[i] = __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r, q * 16, 0, kSc1));
-    }
+    for (int w = 0; w < num_words(P); ++w)
+        v[w] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (w * 64 + lane_id()) * 4, 0, kSc1);
 #pragma unroll
-    for (int i = 0; i < (kQ + 63) / 64; ++i) {
-        const int q = lane_id() + 64 * i;
-        if (q < kQ) dst[q] = v[i];
-    }
+    for (int w = 0; w < num_words(P); ++w) set_tab_word(T, w, v[w]);
 }
 
 // TPW = tables per workgroup: 64, or 32 for grids too small to give every SIMD a wave (e.g. the
@@ -2217,18 +2215,21 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
                 }
                 wave_lds_sync();  // the final rows' LDS reads are done
             }
-            encode_row(T, L.rows, L);
-            wave_lds_sync();
+            const bool big_moves = __any(valid && get_moves(T.sw) > 255);
+            const bool deleg_now = dl.producer && deleg_step(k, K, dl.every);
+            if (!deleg_now || big_moves) {  // a delegated step's rows are encoded by the partner
+                encode_row(T, L.rows, L);
+                wave_lds_sync();
+            }
             WSSTAMP(1, k);
             int32_t *obs = S.obs + blk * kObsDim;
-            const bool big_moves = __any(valid && get_moves(T.sw) > 255);
-            if (dl.producer && deleg_step(k, K, dl.every)) {
+            if (deleg_now) {
                 const int j = k / dl.every;
                 if (big_moves) {  // a patched row: stored here, the partner skips the task
                     store_obs_block<TPW, true>(L.rows, rows, obs + (size_t)t0 * kObsDim);
                     flag_store(ready_flag(j), dl.epoch << 1 | 1u);
                 } else {
-                    stage_rows(L.rows, slot_of(j));
+                    stage_state(T, slot_of(j));
                     staged |= 1u << j;
                     pend = j;
                     pend_k = k;
@@ -2292,7 +2293,9 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
                 if (f & 1u) continue;              // the producer stored it
                 flag_store(taken_flag(j), dl.epoch);
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                unstage_rows(slot_of(j), L.rows);
+                Tab<P> T;
+                unstage_state(slot_of(j), T);
+                encode_row(T, L.rows, L);
                 wave_lds_sync();
                 store_obs_block<TPW, true>(L.rows, 64, S.obs + ((size_t)k * (size_t)A.n + pt0) * kObsDim);
                 wave_lds_sync();  // the block's LDS reads are done before the next task's rows land
@@ -2304,7 +2307,9 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
                 if (!((staged >> j) & 1u)) continue;
                 const int k = j * dl.every + dl.every / 2 - 1;
                 if (__builtin_amdgcn_readfirstlane(flag_load(taken_flag(j))) == dl.epoch) continue;
-                unstage_rows(slot_of(j), L.rows);
+                Tab<P> T;
+                unstage_state(slot_of(j), T);
+                encode_row(T, L.rows, L);
                 wave_lds_sync();
                 store_obs_block<TPW, true>(L.rows, 64, S.obs + ((size_t)k * (size_t)A.n + t0) * kObsDim);
                 wave_lds_sync();

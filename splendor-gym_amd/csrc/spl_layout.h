@@ -72,11 +72,11 @@ constexpr int kLutEntries = kLutTc * kLutTp * kLutSt * kLutSb;
 constexpr int kLutOutputs = 40;  // top 3 bits of the first 40 MT outputs, 10 per word
 
 // Rollout-store delegation (k_rollout_ws at 64 tables per workgroup with per-step outputs; see
-// the kernel): per pair of workgroups (2q, 2q+1), kDelegTasks staged 64-row observation blocks
-// (the odd workgroup's LDS bytes, 64 x 297 B) and the flags, one 128-byte line each: the two
-// workgroups' launch counters, then ready and taken per task.
+// the kernel): per pair of workgroups (2q, 2q+1), kDelegTasks staged steps (the odd workgroup's
+// 64 tables' state words after the step, [word][lane] u32, room for 4 players) and the flags, one
+// 128-byte line each: the two workgroups' launch counters, then ready and taken per task.
 constexpr int kDelegTasks = 16;
-constexpr int kDelegPayload = 64 * 297;  // 19 008 B
+constexpr int kDelegPayload = 64 * 4 * num_words(4);  // 6 400 B
 constexpr int kFlagLine = 32;            // u32 words per flag
 enum : int { DF_PROD_EPOCH = 0, DF_CONS_EPOCH = 1, DF_TASKS = 2 };  // + 2 * task + {0 ready, 1 taken}
 constexpr int kDelegFlagWords = (DF_TASKS + 2 * kDelegTasks) * kFlagLine;
