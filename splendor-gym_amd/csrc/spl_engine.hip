@@ -162,6 +162,9 @@ constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 #ifndef SPL_DELEG_EVERY
 #define SPL_DELEG_EVERY 6  // rollout-store delegation period (spl_ctx_set_rollout_delegation)
 #endif
+#ifndef SPL_STEP_OBS_NT
+#define SPL_STEP_OBS_NT false  // k_step_ws observation stores non-temporal (A/B switch)
+#endif
 #ifndef SPL_WS_PRIO
 #define SPL_WS_PRIO 1
 #endif
@@ -1991,7 +1994,7 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
         encode_row(T, L.rows, L);
         wave_lds_sync();
         STAMP(5);
-        store_obs_block(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
+        store_obs_block<64, SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
         STAMP(6);
         if (__any(valid && get_moves(T.sw) > 255)) {  // patch after this wave's block stores of the same dwords
             __builtin_amdgcn_s_waitcnt(0);
