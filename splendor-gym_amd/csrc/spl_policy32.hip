@@ -239,8 +239,10 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
 #pragma unroll
     for (int c = 0; c < kSlots - 1; ++c) issue_chunk(W, c, ring + c * kChunk, wave, lane);
 
+    // grouped rows: the wave's table ids, one load (lane i < valid holds row i's), then shuffles
+    const int32_t tid_own = (a.order && lane < valid) ? a.order[tbase + lane] : 0;
     // observation B fragments: lane (r, g), k-step s = obs[table r][4s + g] (exact in fp32)
-    const int64_t xt = valid > 0 ? table_of(r < valid ? r : 0) : 0;
+    const int64_t xt = valid > 0 ? (a.order ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : tbase + (r < valid ? r : 0)) : 0;
     const int32_t *xrow = a.obs + (size_t)xt * kObs;
     float X[kKs1];
 #pragma unroll
@@ -248,8 +250,22 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         const int k = 4 * s + g;
         X[s] = k < kObs ? (float)xrow[k < kObs ? k : 0] : 0.f;
     }
-    if (a.order) {  // gathered rows
-        for (int e = lane; e < valid * kAct; e += 64) ms[e] = (uint8_t)a.mask[table_of(e / kAct) * kAct + e % kAct];
+    if (a.order) {
+        // gathered rows: every mask byte of the wave's rows in one batch of independent loads (a
+        // loop reading order[] per byte was two dependent round trips per iteration, ~12 of them)
+        constexpr int kMI = (kMaskWave + 63) / 64;  // 12
+        uint32_t mv[kMI];
+#pragma unroll
+        for (int i = 0; i < kMI; ++i) {
+            const int e = lane + 64 * i, row = e / kAct;
+            const int32_t tt = __shfl(tid_own, row < kRowsPerWave ? row : 0);
+            mv[i] = e < valid * kAct ? (uint32_t)(uint8_t)a.mask[(int64_t)tt * kAct + e % kAct] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < kMI; ++i) {
+            const int e = lane + 64 * i;
+            if (e < valid * kAct) ms[e] = (uint8_t)mv[i];
+        }
     } else if (valid == kRowsPerWave) {
         constexpr int kMQ = kMaskWave / 4;  // 180 dwords
         const uint32_t *msrc = reinterpret_cast<const uint32_t *>(a.mask + tbase * kAct);
