@@ -396,6 +396,44 @@ def test_rollout_store_delegation_equals_undelegated():
         a_d.copy_(na_d)
 
 
+@pytest.mark.parametrize("players", [3, 4])
+def test_rollout_store_delegation_multiplayer(players):
+    """Delegation at 3 and 4 players (more state words staged per table): two launches of a
+    6-workgroup rollout store equal the undelegated ones, outputs and final state."""
+    import torch
+    n, K, seed, R = 64 * 6, 24, 5, 8
+    ref = engine(n, players, refill_period=R, pipeline="always", delegation=0)
+    dlg = engine(n, players, refill_period=R, pipeline="always", delegation=4)
+    ref.reset(seeds=range(n))
+    dlg.reset(seeds=range(n))
+    dev = ref.device
+    a_r = torch.zeros(n, dtype=torch.int32, device=dev)
+    ref.sample_uniform(out=a_r, seed=seed, ply=0)
+    a_d = a_r.clone()
+
+    def outs():
+        return {"obs": torch.full((K, n, 297), -1, dtype=torch.int32, device=dev),
+                "mask": torch.empty((K, n, 45), dtype=torch.int8, device=dev),
+                "reward": torch.empty((K, n), dtype=torch.float32, device=dev),
+                "terminated": torch.empty((K, n), dtype=torch.uint8, device=dev),
+                "flags": torch.empty((K, n), dtype=torch.uint8, device=dev),
+                "winner": torch.empty((K, n), dtype=torch.int8, device=dev),
+                "final_obs": torch.zeros((K, n, 297), dtype=torch.int32, device=dev)}
+
+    for launch in range(2):
+        o_r, o_d = outs(), outs()
+        na_r, na_d = torch.empty_like(a_r), torch.empty_like(a_d)
+        ref.rollout(K, actions=a_r, next_actions=na_r, policy_seed=seed, ply=1 + K * launch, out=o_r)
+        dlg.rollout(K, actions=a_d, next_actions=na_d, policy_seed=seed, ply=1 + K * launch, out=o_d)
+        for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
+            assert torch.equal(o_r[name], o_d[name]), (launch, name)
+        term = o_r["terminated"].bool()
+        assert torch.equal(o_r["final_obs"][term], o_d["final_obs"][term]), launch
+        assert torch.equal(na_r, na_d)
+        a_r, a_d = na_r, na_d
+    assert ref.download().tobytes() == dlg.download().tobytes()
+
+
 def test_dual_step_vector_env_matches_per_env_wrappers():
     """DualStepVectorEnv (fused device greedy_v1 opponent) == per-env DualStepNativeWrapper over
     SplendorEnv with the host greedy_opponent_v1, including the PPO loop's reset after done."""
