@@ -46,6 +46,8 @@ typedef struct {
 
 #define SPL_ACT_SAMPLE 0 /* masked categorical sample + log_prob + entropy (+ critic value)     */
 #define SPL_ACT_GREEDY 1 /* argmax of the actor logits with illegal actions at -inf (first max)  */
+#define SPL_ACT_VALUE 2  /* the critic alone (ActorCritic.get_value, ppo_splendor.py:51): fp32 images
+                          * with a critic; writes args->value only, mask and action may be NULL     */
 
 typedef struct {
     const int32_t *obs;  /* [n][297] int32, 16-byte aligned                                       */
@@ -53,7 +55,7 @@ typedef struct {
     int32_t *action;     /* [n] out                                                               */
     float *logprob;      /* [n] out (SAMPLE; may be NULL)                                         */
     float *entropy;      /* [n] out, per table (SAMPLE; may be NULL; the reference reports mean)  */
-    float *value;        /* [n] out: critic(x) (SAMPLE; NULL skips the critic network)            */
+    float *value;        /* [n] out: critic(x) (SAMPLE, VALUE; NULL in SAMPLE skips the critic)   */
     float *logits;       /* [n][45] out: raw actor logits before masking (may be NULL)            */
     uint64_t seed;       /* SAMPLE: Philox key; draw for table t at ply p = f(seed; table0+t, p)  */
     uint64_t ply;

@@ -517,6 +517,11 @@ int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const sp
         return spl_fail(SPL_E_ARG, "packed_bytes does not match the image described by args->image");
     if (n <= 0) return spl_fail(SPL_E_ARG, "n must be positive");
     if (!args->obs || ((uintptr_t)args->obs & 15u)) return spl_fail(SPL_E_ARG, "obs must be 16-byte aligned");
+    if (args->mode == SPL_ACT_VALUE) {  // ActorCritic.get_value (ppo_splendor.py:51): the critic alone
+        if (!has_critic || !args->value) return spl_fail(SPL_E_ARG, "VALUE needs an image with a critic and a value output");
+        if (precision != SPL_PREC_FP32) return spl_fail(SPL_E_ARG, "VALUE is implemented for fp32 images");
+        return splp32_act(static_cast<const uint8_t *>(packed), true, true, false, n, args, stream);
+    }
     if (!args->mask || ((uintptr_t)args->mask & 3u)) return spl_fail(SPL_E_ARG, "mask must be 4-byte aligned");
     if (!args->action) return spl_fail(SPL_E_ARG, "action output missing");
     if (args->mode != SPL_ACT_SAMPLE && args->mode != SPL_ACT_GREEDY) return spl_fail(SPL_E_ARG, "unknown mode");

@@ -211,10 +211,13 @@ __device__ __forceinline__ void layer_tanh(Enter &enter, const float (&B)[NB], f
     }
 }
 
+// <false, false> greedy actor, <false, true> sampling actor, <true, true> critic + sampling actor
+// (get_action_and_value), <true, false> critic only (ActorCritic.get_value, ppo_splendor.py:51)
 template <bool kCritic, bool kSample>
 __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, ActArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
-    constexpr int kTotal = kCritic ? kAllChunks : kActorChunks;
+    constexpr bool kActor = kSample || !kCritic;
+    constexpr int kTotal = kCritic ? (kActor ? kAllChunks : kCriticChunks) : kActorChunks;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
     // rows [rbase, rend) of this workgroup: tables rbase.. directly, or positions of the grouped
     // order (one network per workgroup: the group whose workgroup range holds blockIdx.x)
@@ -250,7 +253,9 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         const int k = 4 * s + g;
         X[s] = k < kObs ? (float)xrow[k < kObs ? k : 0] : 0.f;
     }
-    if (a.order) {
+    if constexpr (!kActor) {
+        // get_value: no mask
+    } else if (a.order) {
         // gathered rows: every mask byte of the wave's rows in one batch of independent loads (a
         // loop reading order[] per byte was two dependent round trips per iteration, ~12 of them)
         constexpr int kMI = (kMaskWave + 63) / 64;  // 12
@@ -314,6 +319,11 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         value += __shfl_xor(value, 16);  // the other lane groups' units, then the bias
         value += __shfl_xor(value, 32);
         value += a.critic_out[kHid];
+    }
+    if constexpr (!kActor) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing reloads land while the LDS is ours
+        if (g == 0 && r < valid) a.value[table_of(r)] = value;
+        return;
     }
     layer_tanh<kKs1>(enter, X, H1, lane);
     float H2[kKs2];
@@ -500,8 +510,10 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
     const hipStream_t s = (hipStream_t)stream;
     const uint8_t *W = img;
     if (has_critic && !critic) W += (size_t)kCriticChunks * kChunk;  // the actor part of a full image
-    if (critic)
+    if (critic && sample)
         hipLaunchKernelGGL((k_act32<true, true>), grid, block, 0, s, W, a);
+    else if (critic)  // get_value
+        hipLaunchKernelGGL((k_act32<true, false>), grid, block, 0, s, W, a);
     else if (sample)
         hipLaunchKernelGGL((k_act32<false, true>), grid, block, 0, s, W, a);
     else

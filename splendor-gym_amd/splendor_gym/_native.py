@@ -51,7 +51,7 @@ class ActArgs(ctypes.Structure):
                 ("ply", c_uint64), ("ply_base", c_void_p), ("table0", c_int64), ("mode", c_int32), ("image", c_int32)]
 
 
-ACT_SAMPLE, ACT_GREEDY = 0, 1  # SPL_ACT_*
+ACT_SAMPLE, ACT_GREEDY, ACT_VALUE = 0, 1, 2  # SPL_ACT_*
 PREC_FP32, PREC_BF16 = 0, 1    # SPL_PREC_*
 IMG_CRITIC = 1                 # SPL_IMG_CRITIC
 

@@ -11,6 +11,8 @@ tables in one HIP launch straight from the engine's int32 observations and int8 
     multinomial stream: same distribution, different samples.
   * ``greedy(obs, mask)`` = ``argmax(actor(obs).masked_fill(mask < 0.5, -inf))`` (first maximum;
     0 when nothing is legal) — the frozen-opponent policy of training_utils.py:263-276.
+  * ``get_value(obs)`` = ``model.get_value(obs.float())`` (ppo_splendor.py:51, the bootstrap value
+    of ppo_splendor.py:302): the critic alone, fp32.
 
 precision="fp32" (default, the reference's precision): exact fp32 products and accumulation on
 v_mfma_f32_16x16x4_f32 — logits and values equal the fp32 module's to summation-order rounding
@@ -21,7 +23,7 @@ after each PPO update).
 import ctypes
 
 from . import _native
-from ._native import (ACT_GREEDY, ACT_SAMPLE, IMG_CRITIC, NUM_ACTIONS, OBS_DIM, PREC_BF16, PREC_FP32, ActArgs, MlpDesc,
+from ._native import (ACT_GREEDY, ACT_SAMPLE, ACT_VALUE, IMG_CRITIC, NUM_ACTIONS, OBS_DIM, PREC_BF16, PREC_FP32, ActArgs, MlpDesc,
                       check, ptr)
 
 _PRECISIONS = {"fp32": PREC_FP32, "bf16": PREC_BF16}
@@ -94,8 +96,8 @@ class FusedActorCritic:
 
     def _run(self, obs, mask, mode, action, logprob=None, entropy=None, value=None, logits=None, seed=0, ply=0,
              table0=0, ply_base=None):
-        n = self._check_inputs(obs, mask)
-        a = ActArgs(obs=obs.data_ptr(), mask=mask.data_ptr(), action=action.data_ptr(), logprob=ptr(logprob),
+        n = self._check_inputs(obs, mask) if mask is not None else obs.shape[0]
+        a = ActArgs(obs=obs.data_ptr(), mask=ptr(mask), action=ptr(action), logprob=ptr(logprob),
                     entropy=ptr(entropy), value=ptr(value), logits=ptr(logits), seed=int(seed) & (2**64 - 1),
                     ply=int(ply) & (2**64 - 1), ply_base=ptr(ply_base), table0=int(table0), mode=mode, image=self._image_flags)
         with self.torch.cuda.device(self.device):
@@ -125,6 +127,19 @@ class FusedActorCritic:
         logits = t.empty(n, NUM_ACTIONS, dtype=t.float32, device=self.device) if want_logits else None
         self._run(obs, mask, ACT_GREEDY, action, logits=logits)
         return (action, logits) if want_logits else action
+
+    def get_value(self, obs, out=None):
+        """ActorCritic.get_value (ppo_splendor.py:51): the critic's value, f32 [n, 1].  Needs
+        with_critic and precision="fp32"."""
+        t = self.torch
+        if not self.with_critic or self.precision != "fp32":
+            raise ValueError("get_value needs an fp32 image with the critic")
+        if obs.dtype != t.int32 or obs.dim() != 2 or obs.shape[1] != OBS_DIM or not obs.is_contiguous() or \
+                obs.device != self.device:
+            raise ValueError("obs must be a contiguous int32 [n, 297] tensor on the policy's device")
+        value = out if out is not None else t.empty(obs.shape[0], 1, dtype=t.float32, device=self.device)
+        self._run(obs, None, ACT_VALUE, None, value=value)
+        return value
 
     def opponent(self):
         """A batched opponent for DualStepVectorEnv: (obs, mask) -> int32 actions."""

@@ -141,6 +141,28 @@ def test_greedy_logits_match_torch_bf16(n):
     assert (act[none] == 0).all()
 
 
+@pytest.mark.parametrize("weights", [2, "trained"])
+@pytest.mark.parametrize("n", [1, 33, 1000, 4096])
+def test_get_value_equals_sample_value(weights, n):
+    """SPL_ACT_VALUE (ActorCritic.get_value, ppo_splendor.py:51) runs the critic alone: bit-equal to
+    the value the SAMPLE launch returns (same instructions), within the fp32 tolerance of torch,
+    and it needs no mask; partial last waves and workgroups included."""
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic
+    _, obs, mask = states(max(n, 64), seed=13)
+    obs, mask = obs[:n].contiguous(), mask[:n].contiguous()
+    m = model(weights)
+    f = FusedActorCritic(m, with_critic=True)
+    v = f.get_value(obs)
+    _, _, _, v_sample = f.act(obs, mask, seed=1, ply=1)
+    assert v.shape == (n, 1) and torch.equal(v, v_sample)
+    with torch.no_grad():
+        vref = m.get_value(obs.float())
+    assert fp32_close(v, vref), (v - vref).abs().max().item()
+    with pytest.raises(Exception):
+        FusedActorCritic(m, with_critic=False).get_value(obs)
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("n", [1, 33, 1000, 4096])
 def test_full_image_serves_greedy_and_sample(precision, n):
