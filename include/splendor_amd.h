@@ -178,6 +178,13 @@ int spl_legal(spl_ctx_t *ctx, spl_arena_t *arena, int8_t *mask, void *stream);
 int spl_sample_uniform(spl_ctx_t *ctx, int32_t n, const int8_t *mask, int32_t *actions,
                        uint64_t seed, uint64_t ply, int64_t table0, void *stream);
 
+/* The flags of a step split for a gymnasium info dict (envs/splendor_env.py:70-90 info keys):
+ * info[0*n + t] = illegal_action, info[n + t] = draw, info[2n + t] = turn_limit (0/1 bytes), and
+ * *errors (8-byte aligned, device) += the number of tables whose flags carry SPL_F_OOB or
+ * SPL_F_AFTER_TERMINAL (the reference's ValueError / RuntimeError): a running count, compared with
+ * its previous value by the caller.  One launch, asynchronous on `stream`. */
+int spl_step_info(int32_t n, const uint8_t *flags, uint8_t *info, uint64_t *errors, void *stream);
+
 /* Host-view copies of `count` tables starting at `first` (synchronous on `stream`). */
 int spl_table_download(spl_ctx_t *ctx, spl_arena_t *arena, int32_t first, int32_t count,
                        spl_table_t *host, void *stream);

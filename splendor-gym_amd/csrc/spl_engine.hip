@@ -2449,6 +2449,22 @@ __global__ __launch_bounds__(64) void k_sample(int n, const int8_t *mask, int32_
     actions[t] = sample_uniform(m, seed, (uint64_t)(table0 + t), ply);
 }
 
+// spl_step_info: the per-table flags byte split into the gymnasium info planes (illegal_action,
+// draw, turn_limit as 0/1 bytes, [3][n]) and a running count of the tables whose flags carry an
+// error (out-of-range action, step after termination), one atomic per wave that has any
+__global__ __launch_bounds__(256) void k_step_info(int n, const uint8_t *flags, uint8_t *info,
+                                                   unsigned long long *errors) {
+    const int t = blockIdx.x * 256 + (int)threadIdx.x;
+    const uint32_t f = t < n ? flags[t] : 0u;
+    if (t < n) {
+        info[t] = (f & SPL_F_ILLEGAL) ? 1 : 0;
+        info[(size_t)n + t] = (f & SPL_F_DRAW) ? 1 : 0;
+        info[2 * (size_t)n + t] = (f & SPL_F_TURN_LIMIT) ? 1 : 0;
+    }
+    const uint64_t bad = __ballot((f & (SPL_F_OOB | SPL_F_AFTER_TERMINAL)) != 0);
+    if (bad && lane_id() == __ffsll((unsigned long long)bad) - 1) atomicAdd(errors, (unsigned long long)__popcll(bad));
+}
+
 // host view <-> arena (splendor_table.h)
 template <int P>
 __global__ __launch_bounds__(64) void k_download(KArena A, int first, int count, spl_table_t *out) {
@@ -3009,6 +3025,13 @@ int spl_sample_uniform(spl_ctx_t *ctx, int32_t n, const int8_t *mask, int32_t *a
     if (!ctx || n <= 0 || !mask || !actions) return fail(SPL_E_ARG, "bad sample arguments");
     hipLaunchKernelGGL(k_sample, dim3(blocks_for(n)), dim3(64), 0, static_cast<hipStream_t>(stream), n, mask, actions,
                        seed, ply, table0);
+    return launch_check();
+}
+
+int spl_step_info(int32_t n, const uint8_t *flags, uint8_t *info, uint64_t *errors, void *stream) {
+    if (n <= 0 || !flags || !info || !errors || ((uintptr_t)errors & 7u)) return fail(SPL_E_ARG, "bad step-info arguments");
+    hipLaunchKernelGGL(k_step_info, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, static_cast<hipStream_t>(stream), n,
+                       flags, info, reinterpret_cast<unsigned long long *>(errors));
     return launch_check();
 }
 

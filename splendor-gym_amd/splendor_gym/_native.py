@@ -100,6 +100,7 @@ SIGNATURES = {
     "spl_refill": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p], c_int32),
     "spl_encode": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p, c_void_p], c_int32),
     "spl_legal": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p, c_void_p], c_int32),
+    "spl_step_info": ([c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
     "spl_sample_uniform": ([c_void_p, c_int32, c_void_p, c_void_p, c_uint64, c_uint64, c_int64, c_void_p],
                            c_int32),
     "spl_table_download": ([c_void_p, ctypes.POINTER(ArenaDesc), c_int32, c_int32, c_void_p, c_void_p],

@@ -348,6 +348,40 @@ def test_vector_env_numpy_mode():
     assert done > 0
 
 
+def test_vector_env_action_errors():
+    """Out-of-range actions raise the reference's ValueError (envs/splendor_env.py:63-64): host
+    arrays are checked before the launch, device tensors by the step itself ("sync") or by the
+    next call ("deferred"); info's flag views follow the per-table flags."""
+    import torch
+    from splendor_gym import SplendorVectorEnv
+    from splendor_gym import _native
+    n = 64
+    for mode in ("sync", "deferred"):
+        vec = SplendorVectorEnv(n, device="cuda:0", check_actions=mode)
+        vec.reset(seed=7)
+        bad = np.zeros(n, np.int32)
+        bad[5] = 45
+        with pytest.raises(ValueError):
+            vec.step(bad)  # host actions: before any launch
+        acts = vec.sample_actions(seed=2, ply=0).clone()
+        obs, rew, term, trunc, info = vec.step(acts)
+        fl = vec.engine.flags
+        assert torch.equal(info["illegal_action"], (fl & _native.F_ILLEGAL) != 0)
+        assert torch.equal(info["draw"], (fl & _native.F_DRAW) != 0)
+        assert torch.equal(info["turn_limit"], (fl & _native.F_TURN_LIMIT) != 0)
+        assert term.dtype == torch.bool and not trunc.any()
+        dev_bad = vec.sample_actions(seed=2, ply=1).clone()
+        dev_bad[9] = -1
+        if mode == "sync":
+            with pytest.raises(ValueError, match="envs \\[9\\]"):
+                vec.step(dev_bad)
+        else:
+            vec.step(dev_bad)  # returns; the error comes back with the next call
+            with pytest.raises(ValueError, match="deferred"):
+                vec.step(vec.sample_actions(seed=2, ply=2).clone())
+        vec.close()
+
+
 @pytest.mark.slow
 def test_rollout_perf_smoke():  # test_gym_compat.py:135-157 (threshold 6000 SPS)
     env = make_env()
