@@ -238,13 +238,17 @@ def main():
     ctx, desc = eng.ctx, ctypes.byref(eng.desc)
     stream = eng.stream()
 
-    def run(variant, k0, k1, strm, ev=None):
+    def step_args(variant):
+        """The two alternating argument blocks of a variant (built outside any timed region)."""
+        bufs = get_store() if variant == "rollout_store" else eng_bufs
+        return [mkargs(buf[0], buf[1], bufs), mkargs(buf[1], buf[0], bufs)]
+
+    def run(variant, k0, k1, strm, ev=None, sargs=None):
         """Env steps k0..k1-1 (ply k+1 relative to ply_base).  variant "step": one spl_step launch
         per step; "rollout_store"/"rollout_inplace": one spl_rollout launch per RK steps with
         per-step blocks / in place.  Refills every R steps are issued by the library."""
         per = 1 if variant == "step" else RK
-        bufs = get_store() if variant == "rollout_store" else eng_bufs
-        sargs = [mkargs(buf[0], buf[1], bufs), mkargs(buf[1], buf[0], bufs)]
+        sargs = sargs or step_args(variant)
         for i, k in enumerate(range(k0, k1, per)):
             sa = sargs[(k // per) & 1]
             sa.ply = k + 1
@@ -289,6 +293,7 @@ def main():
         eps0 = int(ep_cnt.sum().item())
         barrier(dev)
         ev = events(K // G) if graph is not None else events(K // per)
+        sargs = step_args(variant)
         if graph is None:
             ply_base.fill_(k_base + W)
         for e in ev[0] + ev[1]:  # the HIP events are created on first record: outside the timed region
@@ -302,7 +307,7 @@ def main():
                 graph.replay()
                 ev[1][i].record()
         else:
-            run(variant, 0, K, stream, ev)
+            run(variant, 0, K, stream, ev, sargs)
         t_enq = time.perf_counter()
         torch.cuda.synchronize(dev)
         t_sync = time.perf_counter()
