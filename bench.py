@@ -8,10 +8,11 @@ mask + uniform-random policy, same-step autoreset, obs int32[297] + mask int8[45
 terminated + flags + winner written per table-step, terminal rows to final_obs).  Actions come
 from the device policy (Philox over the new mask).  Two launch shapes compute the same
 trajectories and write the same per-step outputs (tests/test_gpu_parity.py::test_rollout_equals_step_chain):
-  --mode rollout  (headline) one spl_rollout launch per 64 env steps: state stays in registers,
-                  each step's stores drain while the next step computes, and step k's outputs go
-                  to block k of a [64, T, ...] rollout store (≈10 GB at 65536 tables: far larger
-                  than the 256 MiB Infinity Cache, so every output byte reaches HBM)
+  --mode rollout  (headline) one spl_rollout launch per 128 env steps (one PPO rollout of
+                  ppo_splendor.py's --num-steps 128): state stays in registers, each step's stores
+                  drain while the next step computes, and step k's outputs go to block k of a
+                  [128, T, ...] rollout store (≈20 GB at 65536 tables: far larger than the 256 MiB
+                  Infinity Cache, so every output byte reaches HBM)
   --mode step     one spl_step launch per env step (the drop-in SplendorEnv.step path), timed as
                   captured HIP graphs of whole refill periods
 The mode not selected is measured too ("other_mode"), and the rollout kernel is measured a second
@@ -56,7 +57,7 @@ STEP_ALGO_BYTES = {p: 2 * s + 297 * 4 + 45 + 4 + 4 + 1 for p, s in STATE_BYTES.i
 # pool refill period per player count: three pool deals per table must cover the resets between
 # refills (random games last ~77 plies at 2p, ~29 at 4p)
 REFILL_EVERY = {2: 64, 3: 32, 4: 16}
-ROLLOUT_K = 64     # env steps per spl_rollout launch (one fused pool refill per launch at 2p)
+ROLLOUT_K = 128    # env steps per spl_rollout launch = ppo_splendor.py's --num-steps default (:71)
 
 
 def step_plan(mode, steps, warmup, refill_period, rollout_k=ROLLOUT_K, graph_steps=128):
@@ -70,7 +71,7 @@ def step_plan(mode, steps, warmup, refill_period, rollout_k=ROLLOUT_K, graph_ste
              refill cycle, whatever --warmup says)
     G      = steps per captured graph (step mode only; 0 = eager launches): the largest multiple
              of unit that divides K and is <= max(graph_steps, unit); rollout mode is timed eagerly
-             (one ~0.8 ms launch per 64 steps: launch overhead is hidden by the queue)
+             (one ~2 ms launch per 128 steps: launch overhead is hidden by the queue)
     launches = K / per (per = steps per launch)
     """
     if mode not in ("step", "rollout"):

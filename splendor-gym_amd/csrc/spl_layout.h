@@ -75,7 +75,7 @@ constexpr int kLutOutputs = 40;  // top 3 bits of the first 40 MT outputs, 10 pe
 // the kernel): per pair of workgroups (2q, 2q+1), kDelegTasks staged steps (the odd workgroup's
 // 64 tables' state words after the step, [word][lane] u32, room for 4 players) and the flags, one
 // 128-byte line each: the two workgroups' launch counters, then ready and taken per task.
-constexpr int kDelegTasks = 16;
+constexpr int kDelegTasks = 24;  // every 6th step of a 128-step launch (ppo_splendor.py --num-steps 128)
 constexpr int kDelegPayload = 64 * 4 * num_words(4);  // 6 400 B
 constexpr int kFlagLine = 32;            // u32 words per flag
 enum : int { DF_PROD_EPOCH = 0, DF_CONS_EPOCH = 1, DF_TASKS = 2 };  // + 2 * task + {0 ready, 1 taken}

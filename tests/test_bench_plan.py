@@ -32,8 +32,13 @@ def test_step_plan_graph_divides_timed_steps(steps):
 
 
 def test_driver_command_values():
+    # the driver's --steps 20 --warmup 5: two 128-step launches timed (bench.ROLLOUT_K = 128,
+    # ppo_splendor.py --num-steps), two warmed up
+    assert bench.ROLLOUT_K == 128
     p = bench.step_plan("rollout", 20, 5, 64)
-    assert (p["K"], p["W"], p["launches"]) == (128, 128, 2)
+    assert (p["K"], p["W"], p["launches"]) == (256, 256, 2)
+    p64 = bench.step_plan("rollout", 20, 5, 64, rollout_k=64)
+    assert (p64["K"], p64["W"], p64["launches"]) == (128, 128, 2)
     s = bench.step_plan("step", 20, 5, 64)
     assert (s["K"], s["W"], s["G"]) == (64, 64, 64)
 

@@ -1,8 +1,9 @@
 """Full-size and configuration-5 checks on the GPU:
 
-  * the exact headline variant of bench.py (2 players, 65 536 tables, spl_rollout of K = 64 steps,
+  * the exact headline variant of bench.py (2 players, 65 536 tables, spl_rollout of K = 128 steps,
     pool refill every 64 steps fused into the launch, two-wave kernel at 64 tables per workgroup,
-    per-step rollout store with non-temporal stores) equals chained spl_step launches bit for bit,
+    per-step rollout store with non-temporal stores and the cross-XCC delegation) equals chained
+    spl_step launches bit for bit,
     and a 256-table subset of the chain is replayed through the CPU oracle;
   * 4-player sharding invariance (two shards == one engine);
   * BASELINE config 5: batched self-play with the fused fp32 ActorCritic as agent AND opponent
@@ -40,7 +41,7 @@ def store(K, n, dev):
 
 def test_headline_rollout_65536_equals_step_chain_and_oracle():
     import torch
-    n, P, K, R, seed, launches = 65536, 2, 64, 64, 0, 2
+    n, P, K, R, seed, launches = 65536, 2, 128, 64, 0, 2
     chain = engine(n, P, refill_period=R)
     roll = engine(n, P, refill_period=R, refill_fused=True, pipeline=True)  # bench.py defaults
     chain.reset(seeds=range(n))
@@ -77,7 +78,7 @@ def test_headline_rollout_65536_equals_step_chain_and_oracle():
             a_c = na
         assert torch.equal(a_r, a_c), launch
     assert torch.equal(st["c"][0], st["r"][0]) and torch.equal(st["c"][1], st["r"][1])
-    assert int(st["c"][1].sum()) > 50_000  # about one episode per table per 77 plies
+    assert int(st["c"][1].sum()) > 100_000  # about one episode per table per 77 plies
     assert chain.download().tobytes() == roll.download().tobytes()
 
 

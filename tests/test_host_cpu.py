@@ -83,9 +83,9 @@ def test_arena_layout_sizes():
             words = 9 + 4 * P
             b = int(lib.spl_arena_bytes(n, P))
             # state planes + 5 pool planes + 4 deck slot records x 128 B + 64 B PCG record, then per pair
-            # of 64-table workgroups 16 staged steps (64 tables x 25 state words) and 34 flag lines
+            # of 64-table workgroups 24 staged steps (64 tables x 25 state words) and 50 flag lines
             # (rollout-store delegation)
-            deleg = (n // 128) * (16 * 64 * 25 * 4 + 34 * 128)
+            deleg = (n // 128) * (24 * 64 * 25 * 4 + 50 * 128)
             assert b >= (words + 5) * 4 * n + 512 * n + 64 * n + deleg
             assert b % 256 == 0 and b <= (words + 5) * 4 * n + 576 * n + deleg + 6 * 256
 
