@@ -58,15 +58,19 @@ STEP_ALGO_BYTES = {p: 2 * s + 297 * 4 + 45 + 4 + 4 + 1 for p, s in STATE_BYTES.i
 # refills (random games last ~77 plies at 2p, ~29 at 4p)
 REFILL_EVERY = {2: 64, 3: 32, 4: 16}
 ROLLOUT_K = 128    # env steps per spl_rollout launch = ppo_splendor.py's --num-steps default (:71)
+MIN_TIMED_LAUNCHES = 8  # rollout mode times at least this many launches (>= 16 ms), whatever --steps says
 
 
-def step_plan(mode, steps, warmup, refill_period, rollout_k=ROLLOUT_K, graph_steps=128):
+def step_plan(mode, steps, warmup, refill_period, rollout_k=ROLLOUT_K, graph_steps=128,
+              min_launches=MIN_TIMED_LAUNCHES):
     """Turn the requested --steps/--warmup into what is actually run.
 
     unit   = lcm(2 launches, refill period): the two action buffers alternate per launch, and a
              captured graph must hold whole refill periods (the library schedules refills from
              the arena's step counter, which the graph bakes in).
-    K      = steps timed    = --steps rounded up to whole units (>= 1 unit)
+    K      = steps timed    = --steps rounded up to whole units (>= 1 unit), and to at least
+             `min_launches` launches in rollout mode (the driver's --steps 20 would otherwise time
+             two ~2 ms launches, where one box's jitter moves the figure by several percent)
     W      = warm-up steps  = --warmup rounded up to whole units (>= 1 unit: one full launch + a
              refill cycle, whatever --warmup says)
     G      = steps per captured graph (step mode only; 0 = eager launches): the largest multiple
@@ -82,6 +86,8 @@ def step_plan(mode, steps, warmup, refill_period, rollout_k=ROLLOUT_K, graph_ste
     r = int(refill_period)
     unit = 2 * per if r <= 0 else (2 * per) * r // math.gcd(2 * per, r)
     k = max(1, -(-max(int(steps), 1) // unit)) * unit
+    if mode == "rollout":
+        k = max(k, -(-int(min_launches) * per // unit) * unit)
     w = max(1, -(-max(int(warmup), 0) // unit)) * unit
     g = 0
     if mode == "step" and graph_steps and graph_steps > 0:
@@ -96,9 +102,9 @@ def step_plan(mode, steps, warmup, refill_period, rollout_k=ROLLOUT_K, graph_ste
             "requested_steps": int(steps), "requested_warmup": int(warmup)}
 
 
-def cpu_baseline(players, procs, steps_per_proc):
-    """The C oracle (a port of the reference engine) as `procs` single-env random rollouts,
-    one process per core, started BEFORE this process touches the GPU (fork-safe)."""
+def _cpu_leg(players, procs, steps_per_proc):
+    """`procs` single-env random rollouts of the C oracle, one process each (fork, before any GPU
+    use); returns (env steps, wall seconds, mean per-process rate, episodes)."""
     import multiprocessing as mp
     ctx = mp.get_context("fork")
     q = ctx.Queue()
@@ -121,26 +127,47 @@ def cpu_baseline(players, procs, steps_per_proc):
     wall = time.perf_counter() - t0
     for p in ps:
         p.join()
-    total = sum(r[0] for r in res)
-    per_core = sum(r[0] / r[1] for r in res) / len(res)
-    return {"value": round(total / wall, 1), "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "per_core": round(per_core, 1),
-            "sample": (f"C oracle (port of engine/rules.py + envs/splendor_env.py step), {players}p, "
-                       f"{procs} processes x {steps_per_proc} env steps, 1 env each, uniform-random legal "
-                       f"policy with autoreset ({sum(r[2] for r in res)} episodes); reference Python "
-                       "engine measured at 5.4k steps/s/core in SURVEY.md §6")}
+    return (sum(r[0] for r in res), wall, sum(r[0] / r[1] for r in res) / len(res), sum(r[2] for r in res))
 
 
-def load_pmc_traffic(players, tables, variant, steps_per_launch):
-    """HBM bytes per launch of the variant's kernel from the committed rocprofv3 PMC summary."""
+def cpu_share():
+    """CPUs this process may use: the affinity set, capped at the 16 CPUs a one-GPU box grants per
+    GPU (os.cpu_count() and the affinity set show the whole host there)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    return min(16, aff), aff
+
+
+def cpu_baseline(players, procs, steps_per_proc):
+    """The C oracle (a port of the reference engine) as single-env random rollouts, timed on this
+    host BEFORE the process touches the GPU (fork-safe): a 1-core leg (one process) and an all-core
+    leg (`procs` processes, one per core of the box's share)."""
+    n1, w1, _, _ = _cpu_leg(players, 1, steps_per_proc)
+    n, wall, per_core, eps = _cpu_leg(players, procs, steps_per_proc)
+    _, aff = cpu_share()
+    return {"value": round(n / wall, 1), "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "one_core": round(n1 / w1, 1), "per_core_mean_all_core_leg": round(per_core, 1),
+            "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+            "sample": (f"C oracle (port of engine/rules.py + envs/splendor_env.py step), {players}p, 1 env per "
+                       f"process, uniform-random legal policy with autoreset: all-core leg {procs} processes x "
+                       f"{steps_per_proc} env steps ({eps} episodes) = value; 1-core leg 1 process x "
+                       f"{steps_per_proc} steps = one_core.  cores = the box's CPU share (16 per GPU; "
+                       "os_cpu_count is the whole host's).  Reference Python engine: 5.4k steps/s/core, "
+                       "SURVEY.md §6")}
+
+
+def load_pmc_traffic(kernel, tables, steps_per_launch):
+    """HBM bytes per launch of `kernel` on this workload from the committed rocprofv3 PMC summary
+    (tools/pmc.sh -> profiles/pmc_summary.json), or (None, None)."""
     path = os.path.join(REPO, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        if (d.get("players") == players and d.get("tables") == tables
-                and d.get("steps_per_launch", {}).get(variant) == steps_per_launch):
-            return d.get("hbm_bytes_per_launch", {}).get(variant), os.path.relpath(path, REPO)
-    except (OSError, ValueError, AttributeError):
+            e = json.load(f)["entries"].get(f"{kernel}|T{tables}|K{steps_per_launch}")
+        if e and e.get("hbm_bytes_per_launch"):
+            return e["hbm_bytes_per_launch"], f"{os.path.relpath(path, REPO)} ({e.get('source')})"
+    except (OSError, ValueError, KeyError, AttributeError):
         pass
     return None, None
 
@@ -174,16 +201,17 @@ def main():
     ap.add_argument("--pipeline", choices=("auto", "always", "half", "off"), default="auto",
                     help="rollout mode: two-wave pipelined kernel (auto: 32 or 64 tables per workgroup by grid "
                          "size; always: 64; half: 32) vs one wave per 64 tables (off)")
-    ap.add_argument("--delegation", type=int, default=None,
+    ap.add_argument("--delegation", type=int, default=0,
                     help="rollout store: every n-th step the odd-XCC workgroups' rows are stored by their "
-                         "even-XCC partners (default: the library's, 6; 0 = off)")
+                         "even-XCC partners (0 = off, the library default: a 1.5 %% gain, "
+                         "profiles/r03/deleg_ab_r03a.txt)")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank_env = int(os.environ.get("RANK", "0"))
     cpu = None
     if world_env == 1 and rank_env == 0 and not args.no_cpu_baseline:
-        procs = args.cpu_procs or min(16, os.cpu_count() or 1)
+        procs = args.cpu_procs or cpu_share()[0]
         cpu = cpu_baseline(args.players, procs, args.cpu_steps)
 
     import torch
@@ -217,13 +245,15 @@ def main():
     def get_store():
         nonlocal store
         if store is None:
-            store = dict(obs=torch.empty((RK, T, 297), dtype=torch.int32, device=dev),
-                         mask=torch.empty((RK, T, 45), dtype=torch.int8, device=dev),
-                         reward=torch.empty((RK, T), dtype=torch.float32, device=dev),
-                         terminated=torch.empty((RK, T), dtype=torch.uint8, device=dev),
-                         flags=torch.empty((RK, T), dtype=torch.uint8, device=dev),
-                         winner=torch.empty((RK, T), dtype=torch.int8, device=dev),
-                         final_obs=torch.empty((RK, T, 297), dtype=torch.int32, device=dev))
+            # zero-filled once, so the first launches do not pay first-touch costs that the timed
+            # ones never see (a rocprofv3 row then averages like the timed launches)
+            store = dict(obs=torch.zeros((RK, T, 297), dtype=torch.int32, device=dev),
+                         mask=torch.zeros((RK, T, 45), dtype=torch.int8, device=dev),
+                         reward=torch.zeros((RK, T), dtype=torch.float32, device=dev),
+                         terminated=torch.zeros((RK, T), dtype=torch.uint8, device=dev),
+                         flags=torch.zeros((RK, T), dtype=torch.uint8, device=dev),
+                         winner=torch.zeros((RK, T), dtype=torch.int8, device=dev),
+                         final_obs=torch.zeros((RK, T, 297), dtype=torch.int32, device=dev))
         return store
 
     def mkargs(a_in, a_out, bufs):
@@ -355,10 +385,10 @@ def main():
     episodes = int(cnts.sum().item())
 
     def kernel_name(variant):
+        """The kernel the variant launches, as rocprofv3 names it (one name per instantiation)."""
         if variant == "step":
-            return f"spl::k_step<{P}>"
-        rk = "k_rollout" if args.pipeline == "off" else "k_rollout_ws"
-        return f"spl::{rk}<{P}> ({RK} steps per launch, {'per-step store' if variant == 'rollout_store' else 'in place'})"
+            return f"k_step_ws_{P}p"
+        return eng.rollout_kernel_name(per_step=variant == "rollout_store")
 
     def summary(rec):
         v, plan = rec["variant"], rec["plan"]
@@ -380,7 +410,8 @@ def main():
                 "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(achieved / HBM_PEAK_GBS, 4),
                              "frac_of_achievable": round(achieved / HBM_ACHIEVABLE_GBS, 4),
-                             "kernel": kernel_name(v), "kernel_avg_us": round(rec["launch_s"] * 1e6, 2),
+                             "kernel": kernel_name(v), "steps_per_launch": per,
+                             "kernel_avg_us": round(rec["launch_s"] * 1e6, 2),
                              "kernel_timing": rec["kernel_timing"],
                              **({} if rec["eager_s"] is None else
                                 {"eager_launch_us": round(rec["eager_s"] * 1e6, 2)}),
@@ -390,8 +421,7 @@ def main():
 
     def with_traffic(s):
         """The variant's summary with the committed PMC HBM bytes per launch of its kernel."""
-        pmc_key = {"step": "k_step", "rollout_store": "k_rollout_store", "rollout_inplace": "k_rollout"}[s["variant"]]
-        traffic, traffic_src = load_pmc_traffic(P, T, pmc_key, s["plan"]["per"])
+        traffic, traffic_src = load_pmc_traffic(s["roofline"]["kernel"], T, s["plan"]["per"])
         s["roofline"].update(traffic=traffic, traffic_source=traffic_src,
                              traffic_over_algo=None if traffic is None
                              else round(traffic / s["roofline"]["algo_bytes_per_launch"], 4))
@@ -420,7 +450,7 @@ def main():
                        "tables_per_gpu": T, "players": P, "parallelism": f"table-sharded x{world}",
                        "refill_every": R, "refill": args.refill if headline != "step" else "separate",
                        "pipeline": args.pipeline, "rollout_steps_per_launch": RK, "variant": headline,
-                       "delegation": 6 if args.delegation is None else args.delegation,
+                       "delegation": args.delegation,
                        "launch": main_s["launch"], "requested_steps": plan["requested_steps"],
                        "requested_warmup": plan["requested_warmup"],
                        "step_rounding": f"steps/warmup rounded up to whole units of {plan['unit']} (step_plan)"},

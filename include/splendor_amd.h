@@ -124,11 +124,18 @@ int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused);
  * identical in every mode. */
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
 /* spl_rollout with per_step_outputs at 64 tables per workgroup only: rollout-store delegation.  On
- * every `every`-th step (every >= 4; default 6) each workgroup on an odd XCC hands its encoded rows
- * (19 KB of bytes instead of 76 KB of int32) to its partner on the neighbouring even XCC, which
- * stores them after its own steps: MI355X's odd XCCs drain stores ~20 % slower, and the slowest
- * sets the launch time.  0 disables it.  Results are identical either way. */
+ * every `every`-th step (every >= 4; 0 = off) each workgroup on an odd XCC skips that step's encode
+ * and stages its 64 tables' state words after the step (64 x num_words(P) u32, 4.3 KB at 2 players,
+ * sc1 stores, released by s_waitcnt vmcnt(0) before an sc1 ready flag) for its partner on the
+ * neighbouring even XCC, which encodes the rows and stores them into the rollout store after its
+ * own steps: MI355X's odd XCCs drain stores ~20 % slower, and the slowest sets the launch time.
+ * Turned off for grids larger than the resident workgroup capacity (pairs might not run together).
+ * Default: SPL_DELEG_EVERY (DESIGN.md §2 gives the measured A/B).  Results are identical either way. */
 int spl_ctx_set_rollout_delegation(spl_ctx_t *ctx, int every);
+/* The name of the kernel spl_rollout launches for n tables of `players` players under the context's
+ * settings (e.g. "k_rollout_store_2p", "k_rollout_inplace_half_4p"): every instantiation has a name
+ * of its own, so a rocprofv3 summary row maps to one variant.  NULL (spl_last_error) on bad input. */
+const char *spl_rollout_kernel_name(spl_ctx_t *ctx, int32_t n, int32_t players, int32_t per_step_outputs);
 
 int64_t spl_arena_bytes(int32_t n, int32_t players);
 /* Zero the arena and mark every table's pool as not dealt (must precede the first spl_reset

@@ -37,7 +37,7 @@ struct KArena {
     uint8_t *slots;    // [n][2][128] deck records
     uint8_t *pcg;      // [n][64] engine-seed streams
     int n;
-    uint8_t *deleg;    // [n/128][kDelegTasks][64 x 297] staged observation blocks (rollout-store delegation)
+    uint8_t *deleg;    // [n/128][kDelegTasks][num_words(P) x 64] u32 staged state words (rollout-store delegation)
     uint32_t *dflags;  // [n/128][kDelegFlagWords] its flags
 };
 
@@ -119,7 +119,7 @@ __device__ uint64_t *g_rstamps;
         rst_hi[i] = lane_id() == (k) ? (int)(uint32_t)(tt_ >> 32) : rst_hi[i];                   \
         __builtin_amdgcn_sched_barrier(0);                                                       \
     } while (0)
-// k_rollout_ws: both waves keep kWsStamps stamps per step in registers (lane k = step k, K <= 64),
+// rollout_ws (k_rollout_store_*, k_rollout_inplace_*): both waves keep kWsStamps stamps per step in registers (lane k = step k, K <= 64),
 // written to g_wsstamps[workgroup][wave][step][kWsStamps] at the end.
 constexpr int kWsStamps = 11;  // 0-3 per step; 4-10 sub-phases of the rules wave
 __device__ uint64_t *g_wsstamps;
@@ -160,7 +160,11 @@ __device__ int g_stream_limit = MTStream::kMaxOut;
 #endif
 constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 #ifndef SPL_DELEG_EVERY
-#define SPL_DELEG_EVERY 6  // rollout-store delegation period (spl_ctx_set_rollout_delegation)
+// rollout-store delegation period (spl_ctx_set_rollout_delegation): off by default.  Alternating
+// A/B on one box, 12 launches per arm of 128 steps at 65 536 tables: 1999 +- 25 us off vs
+// 1969 +- 34 us every 6th step, a 1.5 % gain (profiles/r03/deleg_ab_r03a.txt) -- under the 2 %
+// that would pay for a cross-XCC hand-off in the headline kernel
+#define SPL_DELEG_EVERY 0
 #endif
 #ifndef SPL_STEP_OBS_NT
 #define SPL_STEP_OBS_NT false  // k_step_ws observation stores non-temporal (A/B switch)
@@ -1826,7 +1830,7 @@ struct __align__(16) WsLDS : Consts {
     __device__ __forceinline__ uint32_t *deal_mtx(int b) { return kScrInSlot ? mtx : &st[b][0][0]; }
 };
 static_assert(sizeof(WsLDS<2>) <= 40960 && sizeof(WsLDS<3>) <= 40960 && sizeof(WsLDS<4>) <= 40960,
-              "k_rollout_ws needs four workgroups per CU");
+              "the two-wave rollout needs four workgroups per CU");
 
 template <int P>
 __device__ __forceinline__ uint32_t tab_word(const Tab<P> &T, int w) {
@@ -1869,7 +1873,7 @@ __device__ __forceinline__ void ws_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
-// SplendorEnv.step for every table with the rules / output split of k_rollout_ws, for ONE step:
+// SplendorEnv.step for every table with the rules / output split of the two-wave rollout, for ONE step:
 // 128-thread workgroups of 64 tables.  The RULES wave loads, steps and autoresets its tables and
 // hands the new state words (and the pre-reset words of tables that just ended) to the OUTPUT
 // wave through LDS; the output wave encodes and stores the observation rows (terminal rows first)
@@ -1887,11 +1891,10 @@ struct __align__(16) StepWsLDS : Consts {
     uint32_t mbits[96];
     uint8_t rows[64 * kObsDim];  // observation staging; before hand-off 1 the rules wave's deal scratch + LaneMT
 };
-static_assert(sizeof(StepWsLDS<4>) <= 40960, "k_step_ws needs four workgroups per CU");
+static_assert(sizeof(StepWsLDS<4>) <= 40960, "k_step_ws_* needs four workgroups per CU");
 
 template <int P>
-__global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) {
-    __shared__ StepWsLDS<P> L;
+__device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, KStep S) {
     constexpr int kW = StepWsLDS<P>::kW;
     const int lane = lane_id();
     const bool rules_wave = threadIdx.x < 64;
@@ -1902,7 +1905,7 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
     const bool want_final = S.autoreset && S.final_obs != nullptr;
     STAMP(0);
     if (rules_wave) {
-        __builtin_amdgcn_s_setprio(SPL_WS_PRIO);  // as in k_rollout_ws: 27.9 -> 27.3 us
+        __builtin_amdgcn_s_setprio(SPL_WS_PRIO);  // as in the rollout: 27.9 -> 27.3 us
         Tab<P> T;
         int action = 0;
         Deal pool = empty_deal();
@@ -2004,7 +2007,24 @@ __global__ __launch_bounds__(128) void k_step_ws(KArena A, KTables Tb, KStep S) 
     }
 }
 
-// Rollout-store delegation (k_rollout_ws<P, 64, true>, spl_ctx_set_rollout_delegation).  The
+// one kernel name per player count (see RolloutKernel)
+template <int P>
+struct StepWsKernel;
+#define SPL_STEP_WS_KERNEL(NAME, P_)                                                   \
+    __global__ __launch_bounds__(128) void NAME(KArena A, KTables Tb, KStep S) {         \
+        __shared__ StepWsLDS<P_> L;                                                      \
+        step_ws<P_>(L, A, Tb, S);                                                        \
+    }                                                                                    \
+    template <>                                                                          \
+    struct StepWsKernel<P_> {                                                            \
+        static constexpr void (*fn)(KArena, KTables, KStep) = NAME;                      \
+    };
+SPL_STEP_WS_KERNEL(k_step_ws_2p, 2)
+SPL_STEP_WS_KERNEL(k_step_ws_3p, 3)
+SPL_STEP_WS_KERNEL(k_step_ws_4p, 4)
+#undef SPL_STEP_WS_KERNEL
+
+// Rollout-store delegation (rollout_ws<P, 64, true>, spl_ctx_set_rollout_delegation).  The
 // XCCs of an MI355X do not drain stores equally fast: with the rollout store's own write pattern
 // and nothing else running (tools/microbench_store_xcc.hip), workgroups on odd XCCs (odd blockIdx)
 // finish ~20 % after those on even XCCs, whichever addresses they write; in the kernel the slowest
@@ -2066,10 +2086,10 @@ __device__ __forceinline__ void unstage_state(const uint8_t *slot, Tab<P> &T) {
 // kStore: per-step outputs (a [K][n][...] rollout store) or every step into the same [n][...] block;
 // a template argument so that the two variants are separate kernels in a profile.
 template <int P, int TPW, bool kStore>
-__global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep S, int K, int refill, int deleg_every) {
+__device__ __forceinline__ void rollout_ws(WsLDS<P> &L, KArena A, KTables Tb, KStep S, int K, int refill,
+                                           int deleg_every) {
     static_assert(TPW == 64 || TPW == 32, "64 or 32 tables per workgroup");
     constexpr bool per_step = kStore;
-    __shared__ WsLDS<P> L;
     constexpr int kW = WsLDS<P>::kW;
     const int lane = lane_id();
     const bool rules_wave = threadIdx.x < 64;
@@ -2266,10 +2286,10 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
                 if (valid && get_moves(T.sw) > 255) obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
             }
             if (pend >= 0 && k == pend_k + 2) {
-                // two steps of block stores (> 63 vector-memory instructions, the counter's
-                // limit) were issued after the staged rows, so they have completed; the wait
-                // states it for the ready flag's sake
-                asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+                // release (guide rule (2)): every sc1 store of the staged words has completed
+                // before the ready flag is stored; by now two steps of block stores sit behind
+                // them, so the wait also drains those
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
                 flag_store(ready_flag(pend), dl.epoch << 1);
                 pend = -1;
             }
@@ -2332,6 +2352,34 @@ __global__ __launch_bounds__(128) void k_rollout_ws(KArena A, KTables Tb, KStep 
 #endif
     }
 }
+
+// One kernel name per instantiation: a rocprofv3 --stats summary names kernels by the text before
+// the template argument list when it truncates, so the per-step store (the headline), the in-place
+// variant and the 32-tables-per-workgroup shapes must differ there to be separate rows.
+template <int P, int TPW, bool kStore>
+struct RolloutKernel;
+#define SPL_ROLLOUT_KERNEL(NAME, P_, TPW_, ST_)                                                               \
+    __global__ __launch_bounds__(128) void NAME(KArena A, KTables Tb, KStep S, int K, int refill, int deleg) { \
+        __shared__ WsLDS<P_> L;                                                                                \
+        rollout_ws<P_, TPW_, ST_>(L, A, Tb, S, K, refill, deleg);                                              \
+    }                                                                                                          \
+    template <>                                                                                                \
+    struct RolloutKernel<P_, TPW_, ST_> {                                                                      \
+        static constexpr void (*fn)(KArena, KTables, KStep, int, int, int) = NAME;                             \
+    };
+SPL_ROLLOUT_KERNEL(k_rollout_store_2p, 2, 64, true)
+SPL_ROLLOUT_KERNEL(k_rollout_store_3p, 3, 64, true)
+SPL_ROLLOUT_KERNEL(k_rollout_store_4p, 4, 64, true)
+SPL_ROLLOUT_KERNEL(k_rollout_store_half_2p, 2, 32, true)
+SPL_ROLLOUT_KERNEL(k_rollout_store_half_3p, 3, 32, true)
+SPL_ROLLOUT_KERNEL(k_rollout_store_half_4p, 4, 32, true)
+SPL_ROLLOUT_KERNEL(k_rollout_inplace_2p, 2, 64, false)
+SPL_ROLLOUT_KERNEL(k_rollout_inplace_3p, 3, 64, false)
+SPL_ROLLOUT_KERNEL(k_rollout_inplace_4p, 4, 64, false)
+SPL_ROLLOUT_KERNEL(k_rollout_inplace_half_2p, 2, 32, false)
+SPL_ROLLOUT_KERNEL(k_rollout_inplace_half_3p, 3, 32, false)
+SPL_ROLLOUT_KERNEL(k_rollout_inplace_half_4p, 4, 32, false)
+#undef SPL_ROLLOUT_KERNEL
 
 // Explicit reset (SplendorEnv.reset / VectorEnv.reset), then observation + mask of all tables.
 template <int P>
@@ -2607,7 +2655,7 @@ struct spl_ctx_s {
     int refill_period;
     int refill_fused;  // spl_rollout: refill inside the rollout launch (default) or as a k_refill launch after it
     int pipeline;      // spl_rollout: 0 one wave per 64 tables, 1 two-wave (auto tables per workgroup), 2 / 3 two-wave at 64 / 32
-    int ws_resident[5];  // k_rollout_ws<P>: workgroups resident per device (occupancy x CUs), index P
+    int ws_resident[5];  // k_rollout_store_<P>p: workgroups resident per device (occupancy x CUs), index P
     int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
     void *stage;
     size_t stage_bytes;
@@ -2661,7 +2709,7 @@ constexpr int kStepWaves = SPL_STEP_WAVES;  // k_step waves per workgroup
 #ifndef SPL_STEP_WS
 #define SPL_STEP_WS 1
 #endif
-constexpr bool kStepWs = SPL_STEP_WS != 0;  // spl_step: two-wave k_step_ws (else k_step)
+constexpr bool kStepWs = SPL_STEP_WS != 0;  // spl_step: two-wave k_step_ws_<P>p (else k_step)
 
 extern "C" {
 
@@ -2763,9 +2811,9 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         int occ[5] = {0, 0, 0, 0, 0};
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], k_rollout_ws<2, 64, true>, 128, 0));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[3], k_rollout_ws<3, 64, true>, 128, 0));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[4], k_rollout_ws<4, 64, true>, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], RolloutKernel<2, 64, true>::fn, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[3], RolloutKernel<3, 64, true>::fn, 128, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[4], RolloutKernel<4, 64, true>::fn, 128, 0));
         for (int q = 0; q < 5; ++q) ws_resident[q] = occ[q] * cus;
     }
     spl_ctx_t *c = new spl_ctx_t();
@@ -2936,7 +2984,7 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     const KArena A = karena(arena);
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (kStepWs) {
-        DISPATCH_P(arena->players, hipLaunchKernelGGL(k_step_ws<PP>, dim3(blocks_for(arena->n)), dim3(128), 0, s, A,
+        DISPATCH_P(arena->players, hipLaunchKernelGGL(StepWsKernel<PP>::fn, dim3(blocks_for(arena->n)), dim3(128), 0, s, A,
                                                       ktables(ctx), S));
     } else {
         DISPATCH_P(arena->players,
@@ -2948,6 +2996,31 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     if (a->autoreset && ctx->refill_period > 0 && arena->steps % ctx->refill_period == 0)
         return spl_refill(ctx, arena, stream);
     return SPL_OK;
+}
+
+// tables per workgroup of the two-wave rollout (0 = the one-wave k_rollout).  Auto: 32 tables per
+// workgroup when 64 would leave half of the resident workgroup slots empty
+static int rollout_tpw(const spl_ctx_t *ctx, int32_t n, int32_t players) {
+    if (ctx->pipeline == 2) return 64;
+    if (ctx->pipeline == 3) return 32;
+    if (ctx->pipeline == 1) return 2 * (int64_t)blocks_for(n) <= ctx->ws_resident[players] ? 32 : 64;
+    return 0;
+}
+
+const char *spl_rollout_kernel_name(spl_ctx_t *ctx, int32_t n, int32_t players, int32_t per_step_outputs) {
+    static const char *const names[2][2][3] = {
+        {{"k_rollout_inplace_2p", "k_rollout_inplace_3p", "k_rollout_inplace_4p"},
+         {"k_rollout_inplace_half_2p", "k_rollout_inplace_half_3p", "k_rollout_inplace_half_4p"}},
+        {{"k_rollout_store_2p", "k_rollout_store_3p", "k_rollout_store_4p"},
+         {"k_rollout_store_half_2p", "k_rollout_store_half_3p", "k_rollout_store_half_4p"}}};
+    static const char *const one_wave[3] = {"k_rollout<2>", "k_rollout<3>", "k_rollout<4>"};
+    if (!ctx || n <= 0 || players < 2 || players > 4) {
+        fail(SPL_E_ARG, "spl_rollout_kernel_name: bad arguments");
+        return nullptr;
+    }
+    const int tpw = rollout_tpw(ctx, n, players);
+    if (tpw == 0) return one_wave[players - 2];
+    return names[per_step_outputs ? 1 : 0][tpw == 32 ? 1 : 0][players - 2];
 }
 
 int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, int32_t steps, int32_t per_step_outputs,
@@ -2968,20 +3041,18 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
                           ? (int)std::min<int64_t>(steps, (before + steps) / ctx->refill_period - before / ctx->refill_period)
                           : 0;
     // two-wave kernel (WsLDS<P> fits four workgroups per CU at every player count)
-    // (pipeline 1 = auto, 2 = two-wave at 64 tables per workgroup, 3 = two-wave at 32).  Auto: two-wave
-    // with 32 tables per workgroup when 64 would leave half the resident slots empty
+    // (pipeline 1 = auto, 2 = two-wave at 64 tables per workgroup, 3 = two-wave at 32)
     const int64_t resident = ctx->ws_resident[arena->players];
-    int tpw = 0;
-    if (ctx->pipeline == 2) tpw = 64;
-    else if (ctx->pipeline == 3) tpw = 32;
-    else if (ctx->pipeline == 1) tpw = 2 * (int64_t)blocks_for(arena->n) <= resident ? 32 : 64;
+    const int tpw = rollout_tpw(ctx, arena->n, arena->players);
     const bool p_out = per_step_outputs != 0;
+    // delegation pairs must run at the same time: off when the grid exceeds what is resident at once
+    const int deleg = (int64_t)blocks_for(arena->n) <= resident ? ctx->deleg_every : 0;
 #define SPL_LAUNCH_WS(TPW, BLOCKS)                                                                           \
     DISPATCH_P(arena->players, if (p_out) {                                                                  \
-        hipLaunchKernelGGL((k_rollout_ws<PP, TPW, true>), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
-                           (int)steps, fused, ctx->deleg_every);                                             \
+        hipLaunchKernelGGL((RolloutKernel<PP, TPW, true>::fn), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
+                           (int)steps, fused, deleg);                                                        \
     } else {                                                                                                 \
-        hipLaunchKernelGGL((k_rollout_ws<PP, TPW, false>), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
+        hipLaunchKernelGGL((RolloutKernel<PP, TPW, false>::fn), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
                            (int)steps, fused, 0);                                                            \
     })
     if (tpw == 64) {

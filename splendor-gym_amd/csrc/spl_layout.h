@@ -71,7 +71,7 @@ constexpr int kLutTc = 128, kLutTp = 4, kLutSt = 3, kLutSb = 16;
 constexpr int kLutEntries = kLutTc * kLutTp * kLutSt * kLutSb;
 constexpr int kLutOutputs = 40;  // top 3 bits of the first 40 MT outputs, 10 per word
 
-// Rollout-store delegation (k_rollout_ws at 64 tables per workgroup with per-step outputs; see
+// Rollout-store delegation (k_rollout_store_<P>p at 64 tables per workgroup with per-step outputs; see
 // the kernel): per pair of workgroups (2q, 2q+1), kDelegTasks staged steps (the odd workgroup's
 // 64 tables' state words after the step, [word][lane] u32, room for 4 players) and the flags, one
 // 128-byte line each: the two workgroups' launch counters, then ready and taken per task.

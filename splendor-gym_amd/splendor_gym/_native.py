@@ -76,7 +76,8 @@ TABLE_DTYPE = np.dtype([("num_players", "<i4"), ("bank", "<i4", 6), ("players", 
                         ("turn_count", "<i4"), ("move_count", "<i4"), ("game_over", "<i4"),
                         ("winner", "<i4"), ("turn_limit_reached", "<i4")])
 
-# every symbol the header declares (tests/test_abi_exports.py checks the library exports them)
+# every symbol the header declares (tests/test_host_cpu.py::test_library_exports_every_header_symbol
+# checks that the library exports them)
 SIGNATURES = {
     "spl_abi_version": ([], c_int32),
     "spl_last_error": ([], ctypes.c_char_p),
@@ -87,6 +88,7 @@ SIGNATURES = {
     "spl_ctx_set_rollout_pipeline": ([c_void_p, c_int32], c_int32),
     "spl_ctx_set_rollout_delegation": ([c_void_p, c_int32], c_int32),
     "spl_ctx_token_lut": ([c_void_p, c_void_p, c_int64], c_int64),
+    "spl_rollout_kernel_name": ([c_void_p, c_int32, c_int32, c_int32], ctypes.c_char_p),
     "spl_arena_bytes": ([c_int32, c_int32], c_int64),
     "spl_arena_init": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p], c_int32),
     "spl_reset": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],

@@ -226,6 +226,13 @@ class Engine:
         self._keep_actions = (actions, bufs)
         return bufs
 
+    def rollout_kernel_name(self, per_step=True):
+        """Name of the kernel rollout() launches for this engine (as a rocprofv3 summary lists it)."""
+        name = self.lib.spl_rollout_kernel_name(self.ctx, self.n, self.P, 1 if per_step else 0)
+        if name is None:
+            check(self.lib, -1)
+        return name.decode()
+
     def refill(self):
         with self.torch.cuda.device(self.device):
             check(self.lib, self.lib.spl_refill(self.ctx, ctypes.byref(self.desc), self.stream()))

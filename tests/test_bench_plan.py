@@ -18,7 +18,9 @@ def test_rollout_plan_rounds_up_to_whole_launches(steps, players):
     assert p["W"] >= 64 + r or p["W"] >= p["unit"]        # one full launch and a refill cycle
     assert p["W"] >= 64 and p["W"] % p["unit"] == 0
     assert p["G"] == 0                                    # rollout mode is timed eagerly
-    assert p["K"] - steps < p["unit"]                     # smallest whole-unit cover
+    assert p["launches"] >= bench.MIN_TIMED_LAUNCHES      # never a two-launch timed region
+    # smallest whole-unit cover of max(steps, MIN_TIMED_LAUNCHES launches)
+    assert p["K"] - max(steps, bench.MIN_TIMED_LAUNCHES * 64) < p["unit"]
 
 
 @pytest.mark.parametrize("steps", [1, 20, 100, 1024])
@@ -32,13 +34,13 @@ def test_step_plan_graph_divides_timed_steps(steps):
 
 
 def test_driver_command_values():
-    # the driver's --steps 20 --warmup 5: two 128-step launches timed (bench.ROLLOUT_K = 128,
-    # ppo_splendor.py --num-steps), two warmed up
-    assert bench.ROLLOUT_K == 128
+    # the driver's --steps 20 --warmup 5: eight 128-step launches timed (bench.ROLLOUT_K = 128,
+    # ppo_splendor.py --num-steps; >= 16 ms of GPU time, VERDICT r02 "Next round" 1), two warmed up
+    assert bench.ROLLOUT_K == 128 and bench.MIN_TIMED_LAUNCHES == 8
     p = bench.step_plan("rollout", 20, 5, 64)
-    assert (p["K"], p["W"], p["launches"]) == (256, 256, 2)
+    assert (p["K"], p["W"], p["launches"]) == (1024, 256, 8)
     p64 = bench.step_plan("rollout", 20, 5, 64, rollout_k=64)
-    assert (p64["K"], p64["W"], p64["launches"]) == (128, 128, 2)
+    assert (p64["K"], p64["W"], p64["launches"]) == (512, 128, 8)
     s = bench.step_plan("step", 20, 5, 64)
     assert (s["K"], s["W"], s["G"]) == (64, 64, 64)
 
@@ -48,6 +50,8 @@ def test_eager_step_plan_and_disabled_refill():
     assert p["G"] == 0 and p["unit"] == 2 and p["K"] == 20 and p["launches"] == 20
     q = bench.step_plan("rollout", 200, 0, 0, rollout_k=16)
     assert q["unit"] == 32 and q["K"] == 224 and q["launches"] == 14
+    q1 = bench.step_plan("rollout", 1, 0, 0, rollout_k=16, min_launches=1)
+    assert q1["K"] == 32 and q1["launches"] == 2
 
 
 def test_algorithmic_bytes_constants():

@@ -2,7 +2,7 @@
 
   * the exact headline variant of bench.py (2 players, 65 536 tables, spl_rollout of K = 128 steps,
     pool refill every 64 steps fused into the launch, two-wave kernel at 64 tables per workgroup,
-    per-step rollout store with non-temporal stores and the cross-XCC delegation) equals chained
+    per-step rollout store with non-temporal stores; delegation off, the default) equals chained
     spl_step launches bit for bit,
     and a 256-table subset of the chain is replayed through the CPU oracle;
   * 4-player sharding invariance (two shards == one engine);

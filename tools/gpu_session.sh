@@ -1,0 +1,51 @@
+#!/bin/bash
+# One GPU session (round 3).  Steps by name, run in order; each GPU step has its own time limit and
+# the chain stops at the first failure.
+#   tools/gpu_session.sh TAG step [step ...]
+# steps: tests smoke driver prof deleg multi pmc2p pmcmulti selfplay vec policy
+set -o pipefail
+TAG=${1:?tag}
+shift
+O=gpurun_out
+mkdir -p $O
+export TMPDIR=/tmp
+run() {  # run NAME SECONDS CMD... ; output to $O/NAME_$TAG.{out,err}
+  local name=$1 secs=$2
+  shift 2
+  echo "== $name"
+  timeout -k 10 $secs "$@" > $O/${name}_$TAG.out 2> $O/${name}_$TAG.err
+  local rc=$?
+  if [ $rc -ne 0 ]; then echo "$name failed rc=$rc"; tail -30 $O/${name}_$TAG.err; tail -30 $O/${name}_$TAG.out; exit 1; fi
+  tail -c 1500 $O/${name}_$TAG.out
+}
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread --durations=12 ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    driver) run bench_driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    prof)
+      # the driver's exact command under rocprofv3: one summary row per kernel instantiation
+      run prof_driver 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_driver_$TAG -o run -- \
+          python3 bench.py --gpus 1 --steps 20 --warmup 5
+      cp $O/prof_driver_$TAG/run_kernel_stats.csv $O/kernel_stats_driver_$TAG.csv 2>/dev/null || \
+          find $O/prof_driver_$TAG -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats_driver_$TAG.csv \;
+      head -8 $O/kernel_stats_driver_$TAG.csv ;;
+    deleg) run deleg_ab 600 python3 tools/deleg_ab.py --rounds 12 --arms 0,6 ;;
+    multi)
+      run bench_3p 600 python3 bench.py --no-cpu-baseline --players 3
+      run bench_4p 600 python3 bench.py --no-cpu-baseline --players 4
+      run bench_4p_32768 600 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 ;;
+    pmc2p) bash tools/pmc.sh ${TAG}_2p 2 65536 store all || exit 1
+           bash tools/pmc.sh ${TAG}_2p_inplace 2 65536 inplace traffic || exit 1
+           bash tools/pmc.sh ${TAG}_2p_step 2 65536 step all || exit 1 ;;
+    pmcmulti) bash tools/pmc.sh ${TAG}_3p 3 65536 store traffic || exit 1
+              bash tools/pmc.sh ${TAG}_4p 4 65536 store traffic || exit 1
+              bash tools/pmc.sh ${TAG}_4p_32768 4 32768 store all || exit 1 ;;
+    selfplay) run sp_pool 300 python tools/bench_selfplay.py
+              run sp_frozen 300 python tools/bench_selfplay.py --opponent frozen ;;
+    vec) run vec_step 300 python tools/bench_vec_step.py ;;
+    policy) run policy 300 python tools/bench_policy.py --iters 20 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "session $TAG done"

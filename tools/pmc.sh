@@ -1,28 +1,39 @@
 #!/bin/bash
-# PMC passes for the step, rollout and refill kernels (one rocprofv3 --pmc pass per counter group, each
-# with --kernel-trace only as gpurun requires).  The bench runs one variant (--only): VARIANT=store
-# (headline: rollout with per-step blocks of a [64, T, ...] store), inplace, or step.
+# PMC passes over one bench workload (one rocprofv3 --pmc pass per counter group, each with
+# --kernel-trace only, as gpurun requires), then the summary into profiles/pmc_summary.json.
+#   tools/pmc.sh TAG PLAYERS TABLES VARIANT [GROUPS]
+# VARIANT: store (rollout, per-step blocks of a [128, T, ...] store; the headline), inplace, step.
+# GROUPS: "traffic" (FETCH_SIZE; WRITE_SIZE only) or "all" (default: traffic + SQ/TCC groups).
 set -o pipefail
-TAG=${1:-r02}
-VARIANT=${VARIANT:-store}
+TAG=${1:?tag}
+P=${2:-2}
+T=${3:-65536}
+VARIANT=${4:-store}
+WHICH=${5:-all}
 OUT=gpurun_out/pmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+COMMON="--no-cpu-baseline --only --players $P --tables $T"
 if [ "$VARIANT" = "step" ]; then
-  BENCH="python3 bench.py --no-cpu-baseline --only --mode step --graph-steps 0 --steps 64 --warmup 64"
+  ARGS="$COMMON --mode step --graph-steps 0 --steps 64 --warmup 64"
 else
-  BENCH="python3 bench.py --no-cpu-baseline --only --mode rollout --outputs $VARIANT --steps 128 --warmup 128"
+  ARGS="$COMMON --mode rollout --outputs $VARIANT --steps 128 --warmup 128"
 fi
-GROUPS_DEFAULT="FETCH_SIZE;WRITE_SIZE;\
-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU;\
-SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM SQ_WAIT_INST_LDS;\
-GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_BRANCH SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INST_LEVEL_VMEM;\
+TRAFFIC="FETCH_SIZE;WRITE_SIZE"
+MORE="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU;\
+SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS;\
+GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_BRANCH SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_INST_LEVEL_VMEM;\
 TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_EA0_RDREQ_DRAM TCC_EA0_WRREQ_DRAM"
-IFS=';' read -ra GROUPS_LIST <<< "${PMC_GROUPS:-$GROUPS_DEFAULT}"
+if [ "$WHICH" = "traffic" ]; then G="$TRAFFIC"; else G="$TRAFFIC;$MORE"; fi
+IFS=';' read -ra GROUPS_LIST <<< "$G"
 i=0
 for grp in "${GROUPS_LIST[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${grp} --kernel-include-regex "k_step|k_rollout|k_refill" \
-      --output-format csv -d $OUT/p$i -o run -- $BENCH > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc ${grp} --kernel-include-regex "k_step|k_rollout|k_refill" \
+      --output-format csv -d $OUT/p$i -o run -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pmc pass $i failed"; exit 1; }
 done
-echo "pmc done"
+# the summary accumulates workloads: start from the committed one (copy it back into profiles/)
+[ -f gpurun_out/pmc_summary.json ] || cp profiles/pmc_summary.json gpurun_out/pmc_summary.json
+python3 tools/pmc_summary.py $OUT gpurun_out/pmc_summary.json --players $P --tables $T --rollout-steps 128 \
+    > $OUT/summary.txt || { echo "pmc summary failed"; exit 1; }
+cat $OUT/summary.txt
