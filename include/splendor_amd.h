@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 3
+#define SPL_ABI_VERSION 4
 
 /* ---- per-table flag bits (uint8) --------------------------------------------------- */
 #define SPL_F_ILLEGAL 0x01        /* info["illegal_action"]      envs/splendor_env.py:64-66 */
@@ -101,6 +101,13 @@ typedef struct spl_step_args_s {
     int64_t table0;          /* global id of table 0 (sharding: streams keyed by global id) */
     float *ep_return;        /* [n] or NULL: += final reward of player 0 on termination      */
     uint32_t *ep_count;      /* [n] or NULL: += 1 on termination                             */
+    uint8_t *info;           /* [4][n] or NULL (spl_step only): 0/1 bytes of the gymnasium info
+                                planes illegal_action, draw, turn_limit (the SPL_F_ILLEGAL / DRAW /
+                                TURN_LIMIT bits of `flags`), then the step's `truncated` (always 0:
+                                SplendorEnv.step never truncates, envs/splendor_env.py:61-90)   */
+    uint64_t *errors;        /* [1] or NULL (spl_step only): += the number of tables whose flags
+                                carry SPL_F_OOB or SPL_F_AFTER_TERMINAL (the reference's
+                                ValueError / RuntimeError cases, envs/splendor_env.py:53-63)   */
 } spl_step_args_t;
 
 int spl_abi_version(void);

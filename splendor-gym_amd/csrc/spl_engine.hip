@@ -59,6 +59,8 @@ struct KStep {
     int32_t *next_actions;
     float *ep_return;
     uint32_t *ep_count;
+    uint8_t *info;             // nullable: [4][n] info planes + truncated (spl_step)
+    unsigned long long *errors;  // nullable: running count of tables with an error flag (spl_step)
     const uint64_t *ply_base;  // nullable: device counter added to `ply` (graph replays)
     uint64_t policy_seed;
     uint64_t ply;
@@ -1527,6 +1529,23 @@ __device__ __forceinline__ void store_final_rows(const uint8_t *rows_lds, uint64
     }
 }
 
+// spl_step's gymnasium info planes (illegal_action, draw, turn_limit as 0/1 bytes; truncated = 0) and the running
+// count of tables whose flags carry the reference's exceptions (out-of-range action, step after
+// termination): one atomic per wave that has any.  Wave-uniform call (the ballot).
+__device__ __forceinline__ void store_step_info(const KStep &S, int n, int t, bool valid, uint32_t f) {
+    if (S.info && valid) {
+        S.info[t] = (f & SPL_F_ILLEGAL) ? 1 : 0;
+        S.info[(size_t)n + t] = (f & SPL_F_DRAW) ? 1 : 0;
+        S.info[2 * (size_t)n + t] = (f & SPL_F_TURN_LIMIT) ? 1 : 0;
+        S.info[3 * (size_t)n + t] = 0;  // truncated
+    }
+    if (S.errors) {
+        const uint64_t bad = __ballot(valid && (f & (SPL_F_OOB | SPL_F_AFTER_TERMINAL)) != 0);
+        if (bad && lane_id() == __ffsll((unsigned long long)bad) - 1)
+            atomicAdd(S.errors, (unsigned long long)__popcll(bad));
+    }
+}
+
 // SplendorEnv.step for every table (envs/splendor_env.py:51-90) + same-step autoreset.
 //
 // Every global load of the step (state, action, pool deal words, the deck card the action
@@ -1621,6 +1640,7 @@ __global__ __launch_bounds__(64 * W) void k_step(KArena A, KTables Tb, KStep S) 
         if (patch) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
         if (fpatch) S.final_obs[(size_t)t * kObsDim + 295] = fin_moves;
     }
+    store_step_info(S, A.n, t, valid, o.flags);
     if (valid) {
         if (!abl(ABL_SMALL_OUT)) {
             S.reward[t] = o.reward;
@@ -1949,6 +1969,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         L.mask[lane] = o.mask;
         wave_lds_sync();
         store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+        store_step_info(S, A.n, t, valid, o.flags);
         if (valid) {
             S.reward[t] = o.reward;
             S.terminated[t] = o.term ? 1 : 0;
@@ -2968,6 +2989,8 @@ static KStep kstep(const spl_step_args_t *a) {
     S.next_actions = a->next_actions;
     S.ep_return = a->ep_return;
     S.ep_count = a->ep_count;
+    S.info = a->info;
+    S.errors = reinterpret_cast<unsigned long long *>(a->errors);
     S.ply_base = a->ply_base;
     S.policy_seed = a->policy_seed;
     S.ply = a->ply;

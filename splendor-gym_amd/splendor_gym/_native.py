@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 LIB_NAME = "libsplendor_amd.so"
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # per-table flag bits (include/splendor_amd.h)
 POLICY_UNIFORM, POLICY_GREEDY_V1, POLICY_BASIC_PRIORITY = 0, 1, 2  # SPL_POLICY_* (device next_actions)
@@ -35,7 +35,7 @@ class StepArgs(ctypes.Structure):
                 ("terminated", c_void_p), ("flags", c_void_p), ("winner", c_void_p),
                 ("final_obs", c_void_p), ("autoreset", c_int32), ("policy", c_int32), ("next_actions", c_void_p),
                 ("ply_base", c_void_p), ("policy_seed", c_uint64), ("ply", c_uint64), ("table0", c_int64),
-                ("ep_return", c_void_p), ("ep_count", c_void_p)]
+                ("ep_return", c_void_p), ("ep_count", c_void_p), ("info", c_void_p), ("errors", c_void_p)]
 
 
 class MlpDesc(ctypes.Structure):

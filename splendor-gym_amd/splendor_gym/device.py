@@ -103,10 +103,11 @@ class Engine:
             pass
 
     # ------------------------------------------------------------------------------------
-    def reset(self, seeds=None, mask=None, obs=True):
+    def reset(self, seeds=None, mask=None, obs=True, obs_out=None, mask_out=None):
         """Reset tables (all, or where `mask` is true).  seeds: None continues every table's
         engine-seed stream (reset() without a seed); else one seed per table (reset(seed=s)).
-        Writes self.obs / self.mask for every table."""
+        Writes every table's observation / action mask to obs_out / mask_out (default self.obs /
+        self.mask; obs=False writes neither)."""
         torch = self.torch
         pcg = None
         if seeds is not None:
@@ -120,11 +121,12 @@ class Engine:
             if m.numel() != self.n:
                 raise ValueError("mask must have one entry per table")
         with torch.cuda.device(self.device):
-            check(self.lib, self.lib.spl_reset(self.ctx, ctypes.byref(self.desc), ptr(pcg), ptr(m),
-                                               ptr(self.obs) if obs else None, ptr(self.mask) if obs else None,
+            o = (self.obs if obs_out is None else obs_out) if obs else None
+            mk = (self.mask if mask_out is None else mask_out) if obs else None
+            check(self.lib, self.lib.spl_reset(self.ctx, ctypes.byref(self.desc), ptr(pcg), ptr(m), ptr(o), ptr(mk),
                                                self.stream()))
         self._keep = (pcg, m)  # alive until the async reset has consumed them
-        return self.obs, self.mask
+        return o, mk
 
     def deal(self, engine_seeds, mask=None, obs=True):
         """initial_state(P, seed) for every table (or where `mask` is true) from explicit engine

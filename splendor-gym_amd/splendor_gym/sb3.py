@@ -190,7 +190,7 @@ class SplendorSB3VecEnv(_VecEnvBase):
             for i in done_idx:  # SB3 DummyVecEnv: the reset info of an auto-reset env
                 self.reset_infos[i] = {"action_mask": mask[i].copy(), "to_play": int(obs[i, 294])}
         self._last = (obs, mask)
-        n_act = int(getattr(self.single_action_space, "n", 45))
+        n_act = int(getattr(self.action_space, "n", 45))
         P = self.num_players
 
         def build(i):

@@ -365,7 +365,7 @@ def test_vector_env_action_errors():
             vec.step(bad)  # host actions: before any launch
         acts = vec.sample_actions(seed=2, ply=0).clone()
         obs, rew, term, trunc, info = vec.step(acts)
-        fl = vec.engine.flags
+        fl = vec.last_flags
         assert torch.equal(info["illegal_action"], (fl & _native.F_ILLEGAL) != 0)
         assert torch.equal(info["draw"], (fl & _native.F_DRAW) != 0)
         assert torch.equal(info["turn_limit"], (fl & _native.F_TURN_LIMIT) != 0)
@@ -380,6 +380,42 @@ def test_vector_env_action_errors():
             with pytest.raises(ValueError, match="deferred"):
                 vec.step(vec.sample_actions(seed=2, ply=2).clone())
         vec.close()
+
+
+def test_vector_env_returns_fresh_arrays_while_held():
+    """copy=True (gymnasium SyncVectorEnv's default): what a step returned is not overwritten by later
+    steps while the caller holds it (the old step() returned buffers the next step
+    overwrote); copy=False returns the same buffers every step."""
+    import torch
+    from splendor_gym import SplendorVectorEnv
+    n = 256
+    vec = SplendorVectorEnv(n, device="cuda:0")
+    vec.reset(seed=3)
+    held = []
+    for k in range(6):
+        obs, rew, term, trunc, info = vec.step(vec.sample_actions(seed=4, ply=k).clone())
+        snap = [t.clone() for t in (obs, rew, term, trunc, info["action_mask"], info["illegal_action"],
+                                    info["to_play"], info["final_observation"])]
+        held.append(((obs, rew, term, trunc, info["action_mask"], info["illegal_action"], info["to_play"],
+                      info["final_observation"]), snap))
+    row = held[0][0][0][7]  # a view into the first step's obs, the tuple dropped below
+    row_snap = row.clone()
+    for live, snap in held:
+        for a, b in zip(live, snap):
+            assert torch.equal(a, b)
+    held.clear()
+    for k in range(6, 12):
+        vec.step(vec.sample_actions(seed=4, ply=k).clone())
+    assert torch.equal(row, row_snap)  # a view keeps its block alive
+    # dropped results are recycled: the ring does not grow without bound
+    assert len(vec._ring) <= vec.RING + 1
+    vec.close()
+    alias = SplendorVectorEnv(n, device="cuda:0", copy=False)
+    alias.reset(seed=3)
+    a = alias.step(alias.sample_actions(seed=4, ply=0).clone())
+    b = alias.step(alias.sample_actions(seed=4, ply=1).clone())
+    assert a[0].data_ptr() == b[0].data_ptr() and not b[3].any()
+    alias.close()
 
 
 @pytest.mark.slow

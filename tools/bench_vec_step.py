@@ -21,8 +21,8 @@ def main():
     import torch
     from splendor_gym import SplendorVectorEnv
     out = {"tables": args.tables}
-    for mode in ("sync", "deferred"):
-        vec = SplendorVectorEnv(args.tables, device="cuda:0", check_actions=mode)
+    for mode, copy in (("sync", True), ("deferred", True), ("sync", False), ("deferred", False)):
+        vec = SplendorVectorEnv(args.tables, device="cuda:0", check_actions=mode, copy=copy)
         obs, info = vec.reset(seed=0)
         for k in range(32):  # warm-up
             obs, rew, term, trunc, info = vec.step(vec.sample_actions(seed=1, ply=k))
@@ -32,7 +32,8 @@ def main():
             obs, rew, term, trunc, info = vec.step(vec.sample_actions(seed=1, ply=100 + k))
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.steps
-        out[mode] = {"vector_env_step_us": round(dt * 1e6, 2), "env_steps_per_s": round(args.tables / dt, 1)}
+        out[f"{mode}{'' if copy else '_nocopy'}"] = {"vector_env_step_us": round(dt * 1e6, 2),
+                                                     "env_steps_per_s": round(args.tables / dt, 1)}
         vec.close()
     print(json.dumps(out))
 

@@ -43,7 +43,9 @@ for step in "$@"; do
               bash tools/pmc.sh ${TAG}_4p_32768 4 32768 store all || exit 1 ;;
     selfplay) run sp_pool 300 python tools/bench_selfplay.py
               run sp_frozen 300 python tools/bench_selfplay.py --opponent frozen ;;
-    vec) run vec_step 300 python tools/bench_vec_step.py ;;
+    vec) run vec_step 300 python tools/bench_vec_step.py
+         run prof_vec 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_vec_$TAG -o run -- python3 tools/bench_vec_step.py
+         cp $O/prof_vec_$TAG/run_kernel_stats.csv $O/kernel_stats_vec_$TAG.csv; head -6 $O/kernel_stats_vec_$TAG.csv | cut -c1-200 ;;
     policy) run policy 300 python tools/bench_policy.py --iters 20 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
