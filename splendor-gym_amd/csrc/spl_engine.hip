@@ -96,7 +96,8 @@ __device__ uint32_t g_bounds_flags;
     } while (0)
 #endif
 enum : uint32_t {
-    BC_TABLE = 1, BC_SLOT = 2, BC_DECK = 4, BC_LUT = 8, BC_SCRATCH = 16, BC_BYTE = 32, BC_ROWS = 64, BC_CARD = 128
+    BC_TABLE = 1, BC_SLOT = 2, BC_DECK = 4, BC_LUT = 8, BC_SCRATCH = 16, BC_BYTE = 32, BC_ROWS = 64, BC_CARD = 128,
+    BC_SPIN = 256  // a wave gave up waiting for an LDS hand-off (dealer rollout)
 };
 
 // Phase stamps for the diagnostic build only (-DSPL_STAMPS, tools/stamps.py): lane 0 of every
@@ -2100,16 +2101,191 @@ __device__ __forceinline__ void unstage_state(const uint8_t *slot, Tab<P> &T) {
     for (int w = 0; w < num_words(P); ++w) set_tab_word(T, w, v[w]);
 }
 
+// ---- the dealer wave (rollout for grids of at most two workgroups per CU) ----------------------
+// A pool refill deal is a ~90 us serial integer chain per wave (MT19937 init, stream, Fisher-Yates).
+// Fused into the rules wave it stalls that wave's steps for its whole length: at 4 players a
+// 128-step launch needs ~8 of them per table, ~45 % of the rules wave's time on a half-full chip
+// (C4's 32 768 tables per GPU).  When the grid leaves room for a third wave per workgroup (two
+// workgroups of 64 tables per CU: 6 waves on 4 SIMDs), a DEALER wave deals instead, beside the
+// rules and output waves:
+//   * the rules wave owns the ring bookkeeping (status word: live record, pend = consumed records
+//     not yet requested) and posts a batch -- one record per table, the earliest consumed one, the
+//     next in the engine-seed stream -- whenever the dealer is idle and some table has pend > 0;
+//   * the dealer owns the engine-seed streams (PCG64 records) and the deal scratch; it deals the
+//     batch into the slot records (global) and the board / noble words into LDS, drains its stores
+//     (s_waitcnt vmcnt(0): the waves of a workgroup share one L1, so that is the workgroup-scope
+//     release), then counts the batch done;
+//   * a table that ends while its next record is in flight waits for the batch; one whose pool is
+//     spent (all three records consumed) posts a batch of its own and waits (the old inline deal).
+// Deals are taken from each stream in episode order either way, so results do not depend on when
+// a batch runs.  The three waves hand off through LDS counters (no s_barrier: the dealer cannot
+// join a per-step barrier while it runs a 90 us deal).
+struct DealerLDS {
+    static constexpr int kStride = 100;  // deal scratch bytes per lane (25 dwords: odd, conflict-free)
+    uint8_t scr[64 * kStride];
+    uint32_t mtx[624];        // the dealer's LaneMT continuation (one lane at a time)
+    uint32_t rdeal[5][64];    // board / noble words of the last batch's deals ([word][lane])
+    uint8_t rq[64];           // slot record to deal per table, 0xFF = none
+    uint32_t dreq, ddone;     // batches posted (rules wave) / dealt (dealer)
+    uint32_t rdone, odone;    // steps handed off by the rules wave / finished by the output wave
+    uint32_t stop;            // rules wave: no more batches
+};
+template <int P>
+struct __align__(16) WsDealLDS : WsLDS<P> {
+    DealerLDS dl;
+};
+static_assert(sizeof(WsDealLDS<2>) <= 81920 && sizeof(WsDealLDS<3>) <= 81920 && sizeof(WsDealLDS<4>) <= 81920,
+              "the dealer rollout needs two workgroups per CU");
+
+__device__ __forceinline__ uint32_t lds_poll(const uint32_t *p) {
+    const uint32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // later LDS reads stay below the poll
+    return __builtin_amdgcn_readfirstlane(v);
+}
+// lane 0 publishes `v` after this wave's earlier LDS writes have landed
+__device__ __forceinline__ void lds_publish(uint32_t *p, uint32_t v) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    if (lane_id() == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Every wait is bounded (~2^25 polls, seconds): a lost hand-off would corrupt results (and set
+// BC_SPIN in a bounds-check build) rather than leave waves spinning on the GPU.
+constexpr uint32_t kSpinLimit = 1u << 25;
+__device__ __forceinline__ void lds_wait_ge(const uint32_t *p, uint32_t v) {
+    for (uint32_t spins = 0; lds_poll(p) < v; ++spins) {
+        if (spins > kSpinLimit) {
+            SPL_CHECK(false, BC_SPIN);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+__device__ __forceinline__ Deal deal_of_lds(const DealerLDS &D, int lane) {
+    return Deal{{D.rdeal[0][lane], D.rdeal[1][lane], D.rdeal[2][lane]}, D.rdeal[3][lane], D.rdeal[4][lane]};
+}
+
+// The dealer wave: batches until the rules wave stops and none is left.
+template <int P>
+__device__ __forceinline__ void dealer_loop(DealerLDS &D, const KArena &A, int t0) {
+    const int lane = lane_id();
+    uint32_t done = 0;
+    for (;;) {
+        uint32_t req;
+        for (uint32_t spins = 0;; ++spins) {
+            req = lds_poll(&D.dreq);
+            if (req != done || lds_poll(&D.stop)) break;
+            if (spins > kSpinLimit) {
+                SPL_CHECK(false, BC_SPIN);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+        if (req == done) break;  // stopped, nothing pending
+        const int slot = D.rq[lane];
+        const int t = t0 + lane;
+        if (slot != 0xFF) {
+            SPL_CHECK(t < A.n && slot < kSlotRecords, BC_TABLE);
+            Deal d;
+            deal_next<P>(A, t, slot, &D.scr[lane * DealerLDS::kStride], d, D.mtx);
+            D.rdeal[0][lane] = d.board[0];
+            D.rdeal[1][lane] = d.board[1];
+            D.rdeal[2][lane] = d.board[2];
+            D.rdeal[3][lane] = d.nob0;
+            D.rdeal[4][lane] = d.nob1;
+        }
+        __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): the records and engine-seed streams are written
+        lds_publish(&D.ddone, ++done);
+    }
+}
+
+// the rules wave posts a batch: lanes with `want` request slot record `slot` of their table
+__device__ __forceinline__ void dealer_post(DealerLDS &D, bool want, int slot, uint32_t &my_req) {
+    D.rq[lane_id()] = want ? (uint8_t)slot : (uint8_t)0xFF;
+    lds_publish(&D.dreq, ++my_req);
+}
+
+// The rules wave's side of the dealer after step_rules (wave-uniform call): settle a finished
+// batch, make sure every table that ended has its next record dealt (waiting for the batch in
+// flight, or posting one for a spent pool), run the same-step autoreset (flip_to_pool without its
+// inline deal), then post a new batch when the dealer is idle.
+template <int P>
+__device__ __forceinline__ void dealer_step(DealerLDS &D, Tab<P> &T, const KArena &A, int t, bool valid, bool ends,
+                                            bool autoreset, Deal &pool, bool &pool_dirty, uint32_t &my_req,
+                                            uint32_t &infl, bool &pool_stale, StepOut &o) {
+    constexpr int kPools = kSlotRecords - 1;
+    const int lane = lane_id();
+    auto settle = [&]() {  // the last batch's records are dealt; its words fill a stale `pool`
+        infl = 0u;
+        if (pool_stale) {
+            pool = deal_of_lds(D, lane);
+            pool_stale = false;
+            pool_dirty = true;
+        }
+    };
+    bool idle = lds_poll(&D.ddone) == my_req;
+    if (idle) settle();
+    uint32_t misc = T.sw[SW_MISC];
+    int pend = pend_of(misc);
+    const int nxt = (active_of(misc) + 1) % kSlotRecords;
+    const bool spent = ends && pend >= kPools;  // all three pool records consumed: deal the next now
+    const bool blocked = ends && !spent && (((infl >> nxt) & 1u) != 0u || pool_stale);
+    if (__any(spent || blocked)) {
+        if (!idle) {
+            lds_wait_ge(&D.ddone, my_req);
+            settle();
+            idle = true;
+        }
+        if (__any(spent)) {
+            dealer_post(D, spent, nxt, my_req);  // nxt is the earliest consumed record when pend == 3
+            if (spent) {
+                pend -= 1;
+                misc = (misc & ~ST_PEND) | ((uint32_t)pend << ST_PEND_SHIFT);
+                pool_stale = true;
+            }
+            lds_wait_ge(&D.ddone, my_req);
+            settle();
+        }
+    }
+    if (ends) {  // flip_to_pool: the next record is dealt and `pool` holds its words
+        const int pend2 = pend + 1;  // the old live record is consumed
+        fresh_state(T, ring_bits(nxt, pend2), pool);
+        if (pend2 < kPools) {
+            const int nxt2 = (nxt + 1) % kSlotRecords;
+            if ((infl >> nxt2) & 1u) pool_stale = true;  // in flight: its words come with the batch
+            else pool = rec_deal(slot_rec(A, t, nxt2));
+        }
+        pool_dirty = true;
+        o.flags |= SPL_F_RESET;
+        o.mask = kFreshDealMask;
+        misc = T.sw[SW_MISC];
+        pend = pend2;
+    } else {
+        T.sw[SW_MISC] = misc;
+    }
+    const bool want = valid && autoreset && pend > 0;
+    if (idle && __any(want)) {  // refill: every table's earliest consumed record, next in its stream
+        const int slot = (active_of(misc) - pend + kSlotRecords) % kSlotRecords;
+        dealer_post(D, want, slot, my_req);
+        if (want) {
+            T.sw[SW_MISC] = (misc & ~ST_PEND) | ((uint32_t)(pend - 1) << ST_PEND_SHIFT);
+            infl = 1u << slot;
+            if (pend == kPools) pool_stale = true;  // the next record itself is being dealt
+        }
+    }
+}
+
 // TPW = tables per workgroup: 64, or 32 for grids too small to give every SIMD a wave (e.g. the
 // 32 768-table share of a 4-player 8-GPU run): twice the workgroups, lanes 32-63 idle.  The rules
 // work is latency-bound at one wave per SIMD, so half-populated waves on every SIMD finish a step
 // in about the time full ones take on half of them.
 // kStore: per-step outputs (a [K][n][...] rollout store) or every step into the same [n][...] block;
 // a template argument so that the two variants are separate kernels in a profile.
-template <int P, int TPW, bool kStore>
-__device__ __forceinline__ void rollout_ws(WsLDS<P> &L, KArena A, KTables Tb, KStep S, int K, int refill,
+// kDealer: a third wave deals the pool refills (DealerLDS above; 64 tables per workgroup).
+template <int P, int TPW, bool kStore, bool kDealer = false, class LdsT = WsLDS<P>>
+__device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep S, int K, int refill,
                                            int deleg_every) {
     static_assert(TPW == 64 || TPW == 32, "64 or 32 tables per workgroup");
+    static_assert(!kDealer || TPW == 64, "the dealer variant runs 64 tables per workgroup");
     constexpr bool per_step = kStore;
     constexpr int kW = WsLDS<P>::kW;
     const int lane = lane_id();
@@ -2120,6 +2296,11 @@ __device__ __forceinline__ void rollout_ws(WsLDS<P> &L, KArena A, KTables Tb, KS
     const int rows = min(TPW, A.n - t0);
     const bool want_final = S.autoreset && S.final_obs != nullptr;
     load_tables_lds(L, Tb);
+    if constexpr (kDealer) {  // the hand-off counters start at zero (LDS is not initialised)
+        if (threadIdx.x == 0) {
+            L.dl.dreq = L.dl.ddone = L.dl.rdone = L.dl.odone = L.dl.stop = 0u;
+        }
+    }
     ws_sync();
 
     WSHWID(rules_wave ? 0 : 1);
@@ -2129,8 +2310,18 @@ __device__ __forceinline__ void rollout_ws(WsLDS<P> &L, KArena A, KTables Tb, KS
 #ifdef SPL_STAMPS
     const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
+    if constexpr (kDealer) {
+        if (threadIdx.x >= 128) {
+            dealer_loop<P>(L.dl, A, t0);
+            return;
+        }
+    }
     if (rules_wave) {
-        const RefillSlots rs = refill_slots(K, S.autoreset ? refill : 0);
+        const RefillSlots rs = refill_slots(K, (S.autoreset && !kDealer) ? refill : 0);
+        // dealer bookkeeping (per lane): slots whose deal is in flight (valid while a batch is
+        // outstanding) and whether `pool` still lacks the next record's words
+        uint32_t my_req = 0, infl = 0;
+        bool pool_stale = false;
         Tab<P> T;
         int action = 0;
         Deal pool = empty_deal();
@@ -2153,6 +2344,9 @@ __device__ __forceinline__ void rollout_ws(WsLDS<P> &L, KArena A, KTables Tb, KS
             const int b = k & 1;
             const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
             WSSTAMP(0, k);
+            if constexpr (kDealer) {
+                if (k >= 2) lds_wait_ge(&L.dl.odone, (uint32_t)(k - 1));  // slot b: step k-2 is stored
+            }
             // token-return continuation (LaneMT) in this step's free state slot
 #ifdef SPL_STAMPS
             auto sub = [&](int i) { WSSTAMP(i, k); };
@@ -2176,8 +2370,13 @@ __device__ __forceinline__ void rollout_ws(WsLDS<P> &L, KArena A, KTables Tb, KS
                 }
             }
             const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;  // per termination, as k_step
-            if (valid && o.term && S.autoreset)
-                autoreset_table(T, A, t, pool, L.scratch(b, lane), L.deal_mtx(b), o, pool_dirty);
+            if constexpr (kDealer) {
+                dealer_step<P>(L.dl, T, A, t, valid, valid && o.term && S.autoreset, S.autoreset != 0, pool, pool_dirty,
+                               my_req, infl, pool_stale, o);
+            } else {
+                if (valid && o.term && S.autoreset)
+                    autoreset_table(T, A, t, pool, L.scratch(b, lane), L.deal_mtx(b), o, pool_dirty);
+            }
             WSSTAMP(7, k);
             L.small[b][lane] = pack_small(valid, o, wnr, valid && o.term, ep_add);  // stored by the output wave
             action = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
@@ -2189,8 +2388,20 @@ __device__ __forceinline__ void rollout_ws(WsLDS<P> &L, KArena A, KTables Tb, KS
             const uint64_t fin_listed = __ballot(fin_me && idx < WsLDS<P>::kTerm);  // outside the lane-0 branch
             if (lane == 0) L.fin[b] = fin_listed;
             WSSTAMP(2, k);
-            ws_sync();  // hand-off of step k
+            if constexpr (kDealer) {
+                lds_publish(&L.dl.rdone, (uint32_t)(k + 1));  // hand-off of step k
+            } else {
+                ws_sync();  // hand-off of step k
+            }
             WSSTAMP(3, k);
+        }
+        if constexpr (kDealer) {  // no more batches; the last one lands before the state is stored
+            lds_publish(&L.dl.stop, 1u);
+            lds_wait_ge(&L.dl.ddone, my_req);
+            if (pool_stale) {
+                pool = deal_of_lds(L.dl, lane);
+                pool_dirty = true;
+            }
         }
 #ifdef SPL_STAMPS
         {
@@ -2219,7 +2430,7 @@ __device__ __forceinline__ void rollout_ws(WsLDS<P> &L, KArena A, KTables Tb, KS
 #endif
         // delegation: both workgroups of a full pair take part (the same test on both sides)
         Deleg dl{false, false, (int)(blockIdx.x >> 1), deleg_every, 0u};
-        if (TPW == 64 && kStore && deleg_every >= 4 && (int)(blockIdx.x | 1u) * 64 + 64 <= A.n) {
+        if (TPW == 64 && kStore && !kDealer && deleg_every >= 4 && (int)(blockIdx.x | 1u) * 64 + 64 <= A.n) {
             dl.on = true;
             dl.producer = (blockIdx.x & 1u) != 0;
             uint32_t *ep = A.dflags + (size_t)dl.pair * kDelegFlagWords + (dl.producer ? DF_PROD_EPOCH : DF_CONS_EPOCH) * kFlagLine;
@@ -2233,7 +2444,11 @@ __device__ __forceinline__ void rollout_ws(WsLDS<P> &L, KArena A, KTables Tb, KS
         int pend = -1, pend_k = -1;  // producer: task staged at step pend_k, ready flag not yet set
         uint32_t staged = 0u;        // producer: tasks staged (not stored here)
         for (int k = 0; k < K; ++k) {
-            ws_sync();  // hand-off of step k
+            if constexpr (kDealer) {
+                lds_wait_ge(&L.dl.rdone, (uint32_t)(k + 1));  // hand-off of step k
+            } else {
+                ws_sync();  // hand-off of step k
+            }
             WSSTAMP(0, k);
             const int b = k & 1;
             const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
@@ -2314,6 +2529,7 @@ __device__ __forceinline__ void rollout_ws(WsLDS<P> &L, KArena A, KTables Tb, KS
                 flag_store(ready_flag(pend), dl.epoch << 1);
                 pend = -1;
             }
+            if constexpr (kDealer) lds_publish(&L.dl.odone, (uint32_t)(k + 1));  // slot b is free again
             WSSTAMP(3, k);
         }
 #ifdef SPL_STAMPS
@@ -2401,6 +2617,25 @@ SPL_ROLLOUT_KERNEL(k_rollout_inplace_half_2p, 2, 32, false)
 SPL_ROLLOUT_KERNEL(k_rollout_inplace_half_3p, 3, 32, false)
 SPL_ROLLOUT_KERNEL(k_rollout_inplace_half_4p, 4, 32, false)
 #undef SPL_ROLLOUT_KERNEL
+// the dealer variants (three waves, 64 tables per workgroup; grids of at most two workgroups per CU)
+template <int P, bool kStore>
+struct RolloutDealerKernel;
+#define SPL_DEALER_KERNEL(NAME, P_, ST_)                                                                       \
+    __global__ __launch_bounds__(192) void NAME(KArena A, KTables Tb, KStep S, int K, int refill, int deleg) { \
+        __shared__ WsDealLDS<P_> L;                                                                            \
+        rollout_ws<P_, 64, ST_, true>(L, A, Tb, S, K, refill, deleg);                                          \
+    }                                                                                                          \
+    template <>                                                                                                \
+    struct RolloutDealerKernel<P_, ST_> {                                                                      \
+        static constexpr void (*fn)(KArena, KTables, KStep, int, int, int) = NAME;                             \
+    };
+SPL_DEALER_KERNEL(k_rollout_store_dealer_2p, 2, true)
+SPL_DEALER_KERNEL(k_rollout_store_dealer_3p, 3, true)
+SPL_DEALER_KERNEL(k_rollout_store_dealer_4p, 4, true)
+SPL_DEALER_KERNEL(k_rollout_inplace_dealer_2p, 2, false)
+SPL_DEALER_KERNEL(k_rollout_inplace_dealer_3p, 3, false)
+SPL_DEALER_KERNEL(k_rollout_inplace_dealer_4p, 4, false)
+#undef SPL_DEALER_KERNEL
 
 // Explicit reset (SplendorEnv.reset / VectorEnv.reset), then observation + mask of all tables.
 template <int P>
@@ -2509,12 +2744,23 @@ __global__ __launch_bounds__(64) void k_observe(KArena A, KTables Tb, int32_t *o
     if (mask_out) store_mask_block(L.mask, L.mbits, rows, mask_out + (size_t)t0 * 45);
 }
 
+// One wave per 64 tables: the wave's 64 x 45 mask bytes are read coalesced (64 consecutive bytes
+// per instruction) into LDS, then each lane packs its table's row (a per-lane stride-45 byte
+// walk would touch a new 64-byte segment per lane per byte).
 __global__ __launch_bounds__(64) void k_sample(int n, const int8_t *mask, int32_t *actions, uint64_t seed, uint64_t ply,
                                                int64_t table0) {
-    const int t = blockIdx.x * 64 + lane_id();
+    __shared__ int8_t rows[64 * 45];
+    const int t0 = blockIdx.x * 64, lane = lane_id();
+    const int nb = min(64, n - t0) * 45;
+    const int8_t *src = mask + (size_t)t0 * 45;
+#pragma unroll 5
+    for (int i = lane; i < nb; i += 64) rows[i] = src[i];
+    wave_lds_sync();
+    const int t = t0 + lane;
     if (t >= n) return;
     uint64_t m = 0;
-    for (int i = 0; i < 45; ++i) m |= (uint64_t)(mask[(size_t)t * 45 + i] != 0) << i;
+#pragma unroll
+    for (int i = 0; i < 45; ++i) m |= (uint64_t)(rows[lane * 45 + i] != 0) << i;
     actions[t] = sample_uniform(m, seed, (uint64_t)(table0 + t), ply);
 }
 
@@ -2677,6 +2923,7 @@ struct spl_ctx_s {
     int refill_fused;  // spl_rollout: refill inside the rollout launch (default) or as a k_refill launch after it
     int pipeline;      // spl_rollout: 0 one wave per 64 tables, 1 two-wave (auto tables per workgroup), 2 / 3 two-wave at 64 / 32
     int ws_resident[5];  // k_rollout_store_<P>p: workgroups resident per device (occupancy x CUs), index P
+    int dealer_resident[5];  // k_rollout_store_dealer_<P>p: the same for the three-wave dealer variant
     int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
     void *stage;
     size_t stage_bytes;
@@ -2827,7 +3074,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         memcpy(&nrec[i], b, 8);
     }
     HIP_TRY(hipSetDevice(device));
-    int ws_resident[5];
+    int ws_resident[5], dealer_resident[5];
     {
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -2836,6 +3083,11 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[3], RolloutKernel<3, 64, true>::fn, 128, 0));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[4], RolloutKernel<4, 64, true>::fn, 128, 0));
         for (int q = 0; q < 5; ++q) ws_resident[q] = occ[q] * cus;
+        int docc[5] = {0, 0, 0, 0, 0};
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&docc[2], RolloutDealerKernel<2, true>::fn, 192, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&docc[3], RolloutDealerKernel<3, true>::fn, 192, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&docc[4], RolloutDealerKernel<4, true>::fn, 192, 0));
+        for (int q = 0; q < 5; ++q) dealer_resident[q] = docc[q] * cus;
     }
     spl_ctx_t *c = new spl_ctx_t();
     c->device = device;
@@ -2844,6 +3096,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     c->deleg_every = SPL_DELEG_EVERY;
     c->pipeline = 1;
     memcpy(c->ws_resident, ws_resident, sizeof(ws_resident));
+    memcpy(c->dealer_resident, dealer_resident, sizeof(dealer_resident));
     if (hipMalloc(&c->cards, sizeof(uint4) * 90) != hipSuccess || hipMalloc(&c->nobles, sizeof(uint2) * 10) != hipSuccess ||
         hipMalloc(&c->lut, sizeof(uint4) * kLutEntries) != hipSuccess) {
         spl_ctx_destroy(c);
@@ -2879,7 +3132,7 @@ int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period) {
 
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on) {
     if (!ctx) return fail(SPL_E_ARG, "null ctx");
-    if (on < 0 || on > 3) return fail(SPL_E_ARG, "rollout pipeline must be 0..3");
+    if (on < 0 || on > 4) return fail(SPL_E_ARG, "rollout pipeline must be 0..4");
     ctx->pipeline = on;
     return SPL_OK;
 }
@@ -3021,12 +3274,16 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     return SPL_OK;
 }
 
-// tables per workgroup of the two-wave rollout (0 = the one-wave k_rollout).  Auto: 32 tables per
-// workgroup when 64 would leave half of the resident workgroup slots empty
+// The rollout kernel shape: tables per workgroup of the two-wave rollout (0 = the one-wave
+// k_rollout), or kDealerShape for the three-wave dealer variant.  Auto (pipeline 1): the dealer
+// variant when every workgroup is resident at once with its third wave (at most two per CU, e.g.
+// C4's 32 768 tables per GPU), else two waves at 64 tables per workgroup.
+constexpr int kDealerShape = -1;
 static int rollout_tpw(const spl_ctx_t *ctx, int32_t n, int32_t players) {
     if (ctx->pipeline == 2) return 64;
     if (ctx->pipeline == 3) return 32;
-    if (ctx->pipeline == 1) return 2 * (int64_t)blocks_for(n) <= ctx->ws_resident[players] ? 32 : 64;
+    if (ctx->pipeline == 4) return kDealerShape;
+    if (ctx->pipeline == 1) return (int64_t)blocks_for(n) <= ctx->dealer_resident[players] ? kDealerShape : 64;
     return 0;
 }
 
@@ -3037,12 +3294,16 @@ const char *spl_rollout_kernel_name(spl_ctx_t *ctx, int32_t n, int32_t players, 
         {{"k_rollout_store_2p", "k_rollout_store_3p", "k_rollout_store_4p"},
          {"k_rollout_store_half_2p", "k_rollout_store_half_3p", "k_rollout_store_half_4p"}}};
     static const char *const one_wave[3] = {"k_rollout<2>", "k_rollout<3>", "k_rollout<4>"};
+    static const char *const dealer[2][3] = {
+        {"k_rollout_inplace_dealer_2p", "k_rollout_inplace_dealer_3p", "k_rollout_inplace_dealer_4p"},
+        {"k_rollout_store_dealer_2p", "k_rollout_store_dealer_3p", "k_rollout_store_dealer_4p"}};
     if (!ctx || n <= 0 || players < 2 || players > 4) {
         fail(SPL_E_ARG, "spl_rollout_kernel_name: bad arguments");
         return nullptr;
     }
     const int tpw = rollout_tpw(ctx, n, players);
     if (tpw == 0) return one_wave[players - 2];
+    if (tpw == kDealerShape) return dealer[per_step_outputs ? 1 : 0][players - 2];
     return names[per_step_outputs ? 1 : 0][tpw == 32 ? 1 : 0][players - 2];
 }
 
@@ -3078,7 +3339,15 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
         hipLaunchKernelGGL((RolloutKernel<PP, TPW, false>::fn), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
                            (int)steps, fused, 0);                                                            \
     })
-    if (tpw == 64) {
+    if (tpw == kDealerShape) {
+        DISPATCH_P(arena->players, if (p_out) {
+            hipLaunchKernelGGL((RolloutDealerKernel<PP, true>::fn), dim3(blocks_for(arena->n)), dim3(192), 0, s, A,
+                               ktables(ctx), S, (int)steps, fused, 0);
+        } else {
+            hipLaunchKernelGGL((RolloutDealerKernel<PP, false>::fn), dim3(blocks_for(arena->n)), dim3(192), 0, s, A,
+                               ktables(ctx), S, (int)steps, fused, 0);
+        })
+    } else if (tpw == 64) {
         SPL_LAUNCH_WS(64, blocks_for(arena->n));
     } else if (tpw == 32) {
         SPL_LAUNCH_WS(32, (unsigned)((arena->n + 31) / 32));

@@ -21,9 +21,10 @@ class Engine:
     so results do not depend on how tables are split across GPUs.
     refill_period / refill_fused: pool refill every `refill_period` steps; rollout() runs a due
     refill inside its launch unless refill_fused is False (results are the same either way).
-    pipeline: rollout() kernel choice, same results in every mode: True = two-wave pipelined kernel
-              (32 or 64 tables per workgroup by grid size); "always" / "half" = two-wave at 64 / 32
-              tables per workgroup; False = one wave per 64 tables.
+    pipeline: rollout() kernel choice, same results in every mode: True = auto (the three-wave dealer
+              variant for grids of at most two workgroups per CU, else two-wave at 64 tables per
+              workgroup); "always" / "half" = two-wave at 64 / 32 tables per workgroup; "dealer" = the
+              dealer variant; False = one wave per 64 tables.
     """
 
     # pool refill period by player count (three pool deals per table cover the resets in between;
@@ -55,7 +56,7 @@ class Engine:
         # rollout(): a due refill runs inside the rollout launch (True) or as a refill launch after it
         check(self.lib, self.lib.spl_ctx_set_refill_fused(self.ctx, 1 if refill_fused else 0))
         # rollout(): two-wave pipelined kernel or one wave per 64 tables; same results
-        pipe = {"always": 2, "half": 3}.get(pipeline, 1 if pipeline else 0)
+        pipe = {"always": 2, "half": 3, "dealer": 4}.get(pipeline, 1 if pipeline else 0)
         check(self.lib, self.lib.spl_ctx_set_rollout_pipeline(self.ctx, pipe))
         # rollout() into a per-step store: every n-th step the odd-XCC workgroups' rows are stored by
         # their even-XCC partners (None = the library default, 0 = off); same results

@@ -90,6 +90,8 @@ class _OutBlock:
 class SplendorVectorEnv:
     metadata = {"render_modes": [], "autoreset_mode": "same-step"}
     RING = 3  # output blocks kept for copy=True (a loop holding one step's results while stepping needs 2)
+    DEFER_LAG = 2  # check_actions="deferred": a step's error is raised at the latest this many steps later
+    DEFER_RING = 8
 
     def __init__(self, num_envs, num_players=2, device=None, autoreset=True, refill_period=None, table0=0,
                  to_numpy=False, check_actions="sync", copy=True):
@@ -98,8 +100,9 @@ class SplendorVectorEnv:
         # "sync": the reference's exceptions (out-of-range action, step after termination) are raised
         # by the step() that caused them, which reads one count back from the GPU per step when the
         # actions are a device tensor (host actions are range-checked on the host).  "deferred":
-        # the same check is read back asynchronously and raised by the NEXT step()/reset() call, so
-        # the host never waits for the step kernel.
+        # the count is copied back asynchronously and checked without blocking by later calls; a
+        # step's error is raised at the latest by the DEFER_LAG-th step() after it (or by reset()),
+        # so the host never drains the GPU queue.
         self.check_actions = check_actions
         self.num_envs = int(num_envs)
         self.num_players = int(num_players)
@@ -120,7 +123,9 @@ class SplendorVectorEnv:
         self._errors_seen = 0
         self._ring = [self._new_block()]
         self._cur = 0
-        self._pending = None  # deferred check: (pinned count, event, step index)
+        self._pending = []  # deferred check: (ring slot, step index) of copies not yet checked
+        self._pin = torch.zeros(self.DEFER_RING, dtype=torch.int64).pin_memory() if check_actions == "deferred" else None
+        self._events = [torch.cuda.Event() for _ in range(self.DEFER_RING)] if check_actions == "deferred" else None
         self._steps = 0
         e = self.engine
         self._lib, self._ctx, self._desc = e.lib, e.ctx, ctypes.byref(e.desc)
@@ -167,7 +172,7 @@ class SplendorVectorEnv:
         return self._stream
 
     def reset(self, *, seed=None, options=None):
-        self._raise_pending()
+        self._raise_pending(block_all=True)
         seeds = vector_seeds(seed, self.num_envs)
         if seeds is None and not self._seeded:
             seeds = [None] * self.num_envs  # gymnasium: first reset without a seed draws entropy
@@ -188,17 +193,23 @@ class SplendorVectorEnv:
             raise ValueError(f"Action out of bounds for action_space (envs {bad[:8]})")
         raise RuntimeError(f"Cannot call step() after episode termination. Call reset(). (envs {bad[:8]})")
 
-    def _raise_pending(self):
-        """Deferred check: raise the error of an earlier step once its count has come back."""
-        if self._pending is None:
-            return
-        count, event, step = self._pending
-        self._pending = None
-        event.synchronize()
-        if int(count.item()) != self._errors_seen:
-            self._errors_seen = int(count.item())
-            raise ValueError(f"step {step}: an out-of-range action or a step after termination (the "
-                             f"reference's ValueError / RuntimeError; check_actions='deferred' reports it one call late)")
+    def _raise_pending(self, block_all=False):
+        """Deferred check: raise the error of an earlier step once its count has come back (copies
+        that have landed are checked without blocking; one DEFER_LAG steps old, or every one when
+        block_all, is waited for)."""
+        while self._pending:
+            slot, step = self._pending[0]
+            ev = self._events[slot]
+            if not (block_all or self._steps - step >= self.DEFER_LAG or ev.query()):
+                break
+            ev.synchronize()
+            self._pending.pop(0)
+            count = int(self._pin[slot])
+            if count != self._errors_seen:
+                self._errors_seen = count
+                self._pending.clear()
+                raise ValueError(f"step {step}: an out-of-range action or a step after termination (the reference's "
+                                 "ValueError / RuntimeError; check_actions='deferred' reports it a few calls late)")
 
     def _device_actions(self, actions):
         """(int32 contiguous device tensor, host_checked) for any action container."""
@@ -239,12 +250,12 @@ class SplendorVectorEnv:
                     self._errors_seen = count
                     self._raise_errors(b.flags)
             else:
-                torch = self._torch
-                count = torch.empty(1, dtype=torch.int64, pin_memory=True)
-                count.copy_(self._errors, non_blocking=True)
-                event = torch.cuda.Event()
-                event.record(self._stream_obj)
-                self._pending = (count, event, self._steps)
+                slot = self._steps % self.DEFER_RING
+                if len(self._pending) >= self.DEFER_RING - 1:
+                    self._raise_pending(block_all=True)
+                self._pin[slot:slot + 1].copy_(self._errors, non_blocking=True)
+                self._events[slot].record(self._stream_obj)
+                self._pending.append((slot, self._steps))
         info = {
             "action_mask": b.mask,
             "to_play": b.to_play,

@@ -43,7 +43,7 @@ def main():
         assert np.array_equal(e.obs.cpu().numpy(), ref["obs"]), k
         out["steps"] += n
     # every rollout kernel at 2 / 3 / 4 players, per-step store and in place, fused refills
-    for P, pipe in ((2, True), (2, False), (3, True), (4, True), (4, "half")):
+    for P, pipe in ((2, True), (2, False), (3, True), (4, True), (4, "half"), (2, "always"), (4, "dealer")):
         r = Engine(512, P, pipeline=pipe)
         r.reset(seeds=range(512))
         a = torch.zeros(512, dtype=torch.int32, device=r.device)

@@ -376,9 +376,13 @@ def test_vector_env_action_errors():
             with pytest.raises(ValueError, match="envs \\[9\\]"):
                 vec.step(dev_bad)
         else:
-            vec.step(dev_bad)  # returns; the error comes back with the next call
+            vec.step(dev_bad)  # returns; the error comes back with a later call (DEFER_LAG at the latest)
             with pytest.raises(ValueError, match="deferred"):
-                vec.step(vec.sample_actions(seed=2, ply=2).clone())
+                for k in range(vec.DEFER_LAG):
+                    vec.step(vec.sample_actions(seed=2, ply=2 + k).clone())
+            vec.step(dev_bad)
+            with pytest.raises(ValueError, match="deferred"):
+                vec.reset(seed=8)  # reset() waits for every pending check
         vec.close()
 
 

@@ -206,7 +206,9 @@ def test_unseeded_tables_deal_engine_seed_zero(orc):
                                                           (4, 64, True, False, 16), (3, 64, True, "always", 32),
                                                           (4, 16, True, True, 0), (3, 16, True, True, 0),
                                                           (2, 16, True, "always", 16), (4, 64, True, "always", 16),
-                                                          (4, 16, True, "always", 0), (2, 16, False, "half", 16)])
+                                                          (4, 16, True, "always", 0), (2, 16, False, "half", 16),
+                                                          (4, 128, True, "dealer", 16), (2, 16, True, "dealer", 0),
+                                                          (3, 64, False, "dealer", 32), (4, 64, True, "dealer", 1)])
 def test_rollout_equals_step_chain(P, K, refill_fused, pipeline, R):
     """spl_rollout(K) is K chained spl_step calls (next_actions fed back, plies ply..ply+K-1):
     every per-step output, the terminal rows of final_obs, episode statistics, the next action
@@ -214,8 +216,9 @@ def test_rollout_equals_step_chain(P, K, refill_fused, pipeline, R):
     fused into the rollout launch (each wave at its own step; several per launch when it spans
     several refill periods) or launched after it, or never (R = 0: inline deals once the pool ring is
     spent, through the deal scratch that shares the state slot at 4 players); the two-wave
-    pipelined kernel (any player count; 32 tables per workgroup by default at this size, 64 when
-    forced) or one wave per 64 tables."""
+    pipelined kernel (32 or 64 tables per workgroup), the three-wave dealer variant (the auto choice
+    at this size: a third wave deals the refills, spent pools post a batch and wait) or one wave per
+    64 tables."""
     import torch
     n, launches, seed = 1024, 5 if K <= 16 else 3, 11
     chain = engine(n, P, refill_period=R)
