@@ -2129,6 +2129,7 @@ struct DealerLDS {
     uint32_t dreq, ddone;     // batches posted (rules wave) / dealt (dealer)
     uint32_t rdone, odone;    // steps handed off by the rules wave / finished by the output wave
     uint32_t stop;            // rules wave: no more batches
+    uint32_t abort;           // a wait ran out (lds_wait_ge): every later wait returns at once
 };
 template <int P>
 struct __align__(16) WsDealLDS : WsLDS<P> {
@@ -2148,13 +2149,15 @@ __device__ __forceinline__ void lds_publish(uint32_t *p, uint32_t v) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     if (lane_id() == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// Every wait is bounded (~2^25 polls, seconds): a lost hand-off would corrupt results (and set
-// BC_SPIN in a bounds-check build) rather than leave waves spinning on the GPU.
-constexpr uint32_t kSpinLimit = 1u << 25;
-__device__ __forceinline__ void lds_wait_ge(const uint32_t *p, uint32_t v) {
+// Every wait is bounded (~2^22 polls, a fraction of a second; a legitimate wait is one deal, ~0.1 ms):
+// a lost hand-off would corrupt results (and set BC_SPIN in a bounds-check build) rather than leave
+// waves spinning on the GPU, and once one wait has run out the workgroup's later waits return at once.
+constexpr uint32_t kSpinLimit = 1u << 22;
+__device__ __forceinline__ void lds_wait_ge(DealerLDS &D, const uint32_t *p, uint32_t v) {
     for (uint32_t spins = 0; lds_poll(p) < v; ++spins) {
-        if (spins > kSpinLimit) {
+        if (spins > kSpinLimit || lds_poll(&D.abort)) {
             SPL_CHECK(false, BC_SPIN);
+            if (lane_id() == 0) __hip_atomic_store(&D.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             break;
         }
         __builtin_amdgcn_s_sleep(1);
@@ -2174,7 +2177,7 @@ __device__ __forceinline__ void dealer_loop(DealerLDS &D, const KArena &A, int t
         for (uint32_t spins = 0;; ++spins) {
             req = lds_poll(&D.dreq);
             if (req != done || lds_poll(&D.stop)) break;
-            if (spins > kSpinLimit) {
+            if (spins > kSpinLimit || lds_poll(&D.abort)) {
                 SPL_CHECK(false, BC_SPIN);
                 break;
             }
@@ -2231,7 +2234,7 @@ __device__ __forceinline__ void dealer_step(DealerLDS &D, Tab<P> &T, const KAren
     const bool blocked = ends && !spent && (((infl >> nxt) & 1u) != 0u || pool_stale);
     if (__any(spent || blocked)) {
         if (!idle) {
-            lds_wait_ge(&D.ddone, my_req);
+            lds_wait_ge(D, &D.ddone, my_req);
             settle();
             idle = true;
         }
@@ -2242,7 +2245,7 @@ __device__ __forceinline__ void dealer_step(DealerLDS &D, Tab<P> &T, const KAren
                 misc = (misc & ~ST_PEND) | ((uint32_t)pend << ST_PEND_SHIFT);
                 pool_stale = true;
             }
-            lds_wait_ge(&D.ddone, my_req);
+            lds_wait_ge(D, &D.ddone, my_req);
             settle();
         }
     }
@@ -2298,7 +2301,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
     load_tables_lds(L, Tb);
     if constexpr (kDealer) {  // the hand-off counters start at zero (LDS is not initialised)
         if (threadIdx.x == 0) {
-            L.dl.dreq = L.dl.ddone = L.dl.rdone = L.dl.odone = L.dl.stop = 0u;
+            L.dl.dreq = L.dl.ddone = L.dl.rdone = L.dl.odone = L.dl.stop = L.dl.abort = 0u;
         }
     }
     ws_sync();
@@ -2345,7 +2348,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
             WSSTAMP(0, k);
             if constexpr (kDealer) {
-                if (k >= 2) lds_wait_ge(&L.dl.odone, (uint32_t)(k - 1));  // slot b: step k-2 is stored
+                if (k >= 2) lds_wait_ge(L.dl, &L.dl.odone, (uint32_t)(k - 1));  // slot b: step k-2 is stored
             }
             // token-return continuation (LaneMT) in this step's free state slot
 #ifdef SPL_STAMPS
@@ -2397,7 +2400,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         }
         if constexpr (kDealer) {  // no more batches; the last one lands before the state is stored
             lds_publish(&L.dl.stop, 1u);
-            lds_wait_ge(&L.dl.ddone, my_req);
+            lds_wait_ge(L.dl, &L.dl.ddone, my_req);
             if (pool_stale) {
                 pool = deal_of_lds(L.dl, lane);
                 pool_dirty = true;
@@ -2445,7 +2448,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         uint32_t staged = 0u;        // producer: tasks staged (not stored here)
         for (int k = 0; k < K; ++k) {
             if constexpr (kDealer) {
-                lds_wait_ge(&L.dl.rdone, (uint32_t)(k + 1));  // hand-off of step k
+                lds_wait_ge(L.dl, &L.dl.rdone, (uint32_t)(k + 1));  // hand-off of step k
             } else {
                 ws_sync();  // hand-off of step k
             }
