@@ -32,7 +32,7 @@ class Engine:
     DEFAULT_REFILL = {2: 64, 3: 32, 4: 16}
 
     def __init__(self, num_tables, num_players=2, device=None, refill_period=None, table0=0, refill_fused=True,
-                 pipeline=True, delegation=None):
+                 pipeline=True, delegation=None, cards=None):
         torch = _native.require_gpu()
         self.torch = torch
         self.lib = _native.load_library()
@@ -44,24 +44,9 @@ class Engine:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
-        cards, nobles = load_tables()
-        ctx = ctypes.c_void_p()
-        with torch.cuda.device(self.device):
-            check(self.lib, self.lib.spl_ctx_create(self.device.index, cards.ctypes.data, nobles.ctypes.data,
-                                                    ctypes.byref(ctx)))
-        self.ctx = ctx
-        if refill_period is None:
-            refill_period = self.DEFAULT_REFILL.get(int(num_players), 16)
-        check(self.lib, self.lib.spl_ctx_set_refill_period(self.ctx, int(refill_period)))
-        # rollout(): a due refill runs inside the rollout launch (True) or as a refill launch after it
-        check(self.lib, self.lib.spl_ctx_set_refill_fused(self.ctx, 1 if refill_fused else 0))
-        # rollout(): two-wave pipelined kernel or one wave per 64 tables; same results
-        pipe = {"always": 2, "half": 3, "dealer": 4}.get(pipeline, 1 if pipeline else 0)
-        check(self.lib, self.lib.spl_ctx_set_rollout_pipeline(self.ctx, pipe))
-        # rollout() into a per-step store: every n-th step the odd-XCC workgroups' rows are stored by
-        # their even-XCC partners (None = the library default, 0 = off); same results
-        if delegation is not None:
-            check(self.lib, self.lib.spl_ctx_set_rollout_delegation(self.ctx, int(delegation)))
+        self._settings = (refill_period, refill_fused, pipeline, delegation)
+        self.ctx = None
+        self._create_ctx(cards)
         nbytes = int(self.lib.spl_arena_bytes(self.n, self.P))
         dev = self.device
         self._arena_raw = torch.zeros(nbytes + 256, dtype=torch.uint8, device=dev)
@@ -86,6 +71,47 @@ class Engine:
         self.io_step_bytes = offs[6][3]  # obs .. winner
         with torch.cuda.device(dev):
             check(self.lib, self.lib.spl_arena_init(self.ctx, ctypes.byref(self.desc), self.stream()))
+
+    def _create_ctx(self, cards=None):
+        """A library context over the card table `cards` (int32 [90, 8]; None = the canonical
+        engine/data/tables.json) and the canonical nobles, with this engine's settings."""
+        torch = self.torch
+        base_cards, nobles = load_tables()
+        tbl = base_cards if cards is None else np.ascontiguousarray(np.asarray(cards, np.int32))
+        if tbl.shape != (90, 8):
+            raise ValueError("card table must be int32 [90, 8]")
+        ctx = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_ctx_create(self.device.index, tbl.ctypes.data, nobles.ctypes.data,
+                                                    ctypes.byref(ctx)))
+        self.ctx = ctx
+        self.custom_cards = None if cards is None else tbl.copy()
+        refill_period, refill_fused, pipeline, delegation = self._settings
+        num_players = self.P
+        if refill_period is None:
+            refill_period = self.DEFAULT_REFILL.get(int(num_players), 16)
+        check(self.lib, self.lib.spl_ctx_set_refill_period(self.ctx, int(refill_period)))
+        # rollout(): a due refill runs inside the rollout launch (True) or as a refill launch after it
+        check(self.lib, self.lib.spl_ctx_set_refill_fused(self.ctx, 1 if refill_fused else 0))
+        # rollout(): two-wave pipelined kernel or one wave per 64 tables; same results
+        pipe = {"always": 2, "half": 3, "dealer": 4}.get(pipeline, 1 if pipeline else 0)
+        check(self.lib, self.lib.spl_ctx_set_rollout_pipeline(self.ctx, pipe))
+        # rollout() into a per-step store: every n-th step the odd-XCC workgroups' rows are stored by
+        # their even-XCC partners (None = the library default, 0 = off); same results
+        if delegation is not None:
+            check(self.lib, self.lib.spl_ctx_set_rollout_delegation(self.ctx, int(delegation)))
+
+    def set_card_table(self, cards=None):
+        """Evaluate the tables from now on with card table `cards` (int32 [90, 8]; None = canonical):
+        a new context over the same arena (the table state does not depend on the context)."""
+        same = (cards is None and self.custom_cards is None) or (
+            cards is not None and self.custom_cards is not None and np.array_equal(cards, self.custom_cards))
+        if same:
+            return
+        self.torch.cuda.synchronize(self.device)
+        old = self.ctx
+        self._create_ctx(cards)
+        self.lib.spl_ctx_destroy(old)
 
     # ------------------------------------------------------------------------------------
     def stream(self):

@@ -11,10 +11,14 @@ Each call uploads the view into a one-table scratch arena on the current GPU, la
 and downloads the result (synchronous; for debugging, logging and crafted-state tests — the
 batched Engine / SplendorVectorEnv are the throughput paths).  There is no CPU fallback.
 
-Deviations (documented in DESIGN.md §8): apply_action validates the move as SplendorEnv.step does
+Cards edited in place (``state.board[1][0].cost = {...}``, the reference's
+tests/test_afford_nobles_obs.py:16-17) are honoured: a state whose cards differ from the canonical
+data is evaluated on a scratch arena whose context was built from that state's card table
+(SplendorState.card_table), and apply_action's result keeps the input's Card objects.
+
+Deviation (documented in DESIGN.md §12): apply_action validates the move as SplendorEnv.step does
 and raises ValueError for a move that is illegal in the state (the reference applies it
-unchecked) and RuntimeError on a terminal state; card and noble data are the constant device
-tables, so a Card's cost cannot be edited in place.
+unchecked) and RuntimeError on a terminal state.
 """
 from typing import List, Optional
 
@@ -25,23 +29,29 @@ from .encode import TOTAL_ACTIONS
 from .state import SplendorState
 
 _SCRATCH = {}
+_CUSTOM_KEEP = 8  # scratch engines kept for edited card tables (oldest dropped first)
 
 
-def _scratch(num_players):
-    """One-table arena per player count on the current device (created on first use)."""
+def _scratch(num_players, cards=None):
+    """One-table arena per (player count, device, card table) on the current device (created on first
+    use); cards = an edited int32 [90, 8] card table or None for the canonical one."""
     import torch
     from ..device import Engine
     dev = torch.cuda.current_device() if torch.cuda.is_available() else None
-    key = (int(num_players), dev)
+    key = (int(num_players), dev, None if cards is None else cards.tobytes())
     eng = _SCRATCH.get(key)
     if eng is None:
-        eng = Engine(1, int(num_players), refill_period=0)
+        if cards is not None:
+            custom = [k for k in _SCRATCH if k[2] is not None]
+            for k in custom[:max(0, len(custom) - _CUSTOM_KEEP + 1)]:
+                _SCRATCH.pop(k).close()
+        eng = Engine(1, int(num_players), refill_period=0, cards=cards)
         _SCRATCH[key] = eng
     return eng
 
 
 def _load(state):
-    eng = _scratch(state.num_players)
+    eng = _scratch(state.num_players, state.card_table())
     eng.upload(state.to_record())
     return eng
 
@@ -74,7 +84,7 @@ def apply_action(state, action: int) -> SplendorState:
         raise RuntimeError("apply_action on a terminal state (game over and to_play == 0)")
     if flags & (_native.F_ILLEGAL | _native.F_DRAW):
         raise ValueError(f"action {a} is not legal in this state (the device engine applies legal moves only)")
-    return SplendorState.from_record(eng.download(0, 1)[0])
+    return SplendorState.from_record(eng.download(0, 1)[0], cards=state.cards())
 
 
 def compute_winner(state) -> Optional[int]:

@@ -36,8 +36,12 @@ def load_tables():
     return cards, nobles
 
 
-@dataclass(frozen=True)
+@dataclass
 class Card:
+    """A card of one state (state.py:36-42).  Like the reference's (which initial_state loads afresh
+    for every game), each host view holds its own Card objects, so a test may edit one in place
+    (``card.cost = {...}``, tests/test_afford_nobles_obs.py:16-17): the edited fields reach the device
+    as a card table of that state (SplendorState.card_table, evaluated on a context built from it)."""
     id: int
     tier: int
     color: str
@@ -54,20 +58,38 @@ class Noble:
 
 _CARDS = None
 _NOBLES = None
+_CARD_ROWS = None
 
 
 def cards_by_id():
-    global _CARDS, _NOBLES
+    """The canonical cards (shared, read-only by convention): use card_copy() for a state's own."""
+    global _CARDS, _NOBLES, _CARD_ROWS
     if _CARDS is None:
         c, n = load_tables()
-        # read-only costs: the device holds one constant card table, so an edited cost could not
-        # reach it (the reference tests edit card.cost in place; here that raises)
+        _CARD_ROWS = c
         _CARDS = [Card(i, int(r[0]), STANDARD_COLORS[int(r[1])], int(r[2]),
                        MappingProxyType({STANDARD_COLORS[k]: int(r[3 + k]) for k in range(5) if r[3 + k]}))
                   for i, r in enumerate(c)]
         _NOBLES = [Noble(1000 + i, MappingProxyType({STANDARD_COLORS[k]: int(r[k]) for k in range(5) if r[k]}),
                          int(r[5])) for i, r in enumerate(n)]
     return _CARDS
+
+
+def card_copy(i):
+    """A fresh, editable Card with the canonical data of card id `i`."""
+    c = cards_by_id()[i]
+    return Card(c.id, c.tier, c.color, c.points, dict(c.cost))
+
+
+def card_row(card):
+    """The device table row [tier, colour, points, cost w,b,g,r,k] of a Card's current fields."""
+    return [int(card.tier), STANDARD_COLORS.index(card.color), int(card.points)] + \
+        [int(card.cost.get(c, 0)) for c in STANDARD_COLORS]
+
+
+def canonical_card_rows():
+    cards_by_id()
+    return _CARD_ROWS
 
 
 def nobles_by_index():
@@ -112,7 +134,7 @@ class SplendorState:
     turn_limit_reached: bool = False
 
     def copy(self) -> "SplendorState":
-        """Independent lists, shared (immutable) cards and nobles (state.py:89-104)."""
+        """Independent lists, shared cards and nobles (state.py:89-104)."""
         return SplendorState(
             num_players=self.num_players, bank=list(self.bank),
             players=[PlayerState(tokens=list(p.tokens), bonuses=list(p.bonuses), prestige=p.prestige,
@@ -122,10 +144,48 @@ class SplendorState:
             nobles=list(self.nobles), to_play=self.to_play, turn_count=self.turn_count, move_count=self.move_count,
             game_over=self.game_over, winner_index=self.winner_index, turn_limit_reached=self.turn_limit_reached)
 
+    def cards(self):
+        """Every Card object of this state (board, decks, reserved), by id."""
+        out = {}
+        for t in (1, 2, 3):
+            for c in self.board[t]:
+                if c is not None:
+                    out[c.id] = c
+            for c in self.decks[t]:
+                out[c.id] = c
+        for p in self.players:
+            for c in p.reserved:
+                out[c.id] = c
+        return out
+
+    def card_table(self):
+        """int32 [90, 8] device card table with this state's edited cards, or None when every card of
+        the state has its canonical data (then the shared device tables apply)."""
+        base = canonical_card_rows()
+        tbl = None
+        for i, c in self.cards().items():
+            row = card_row(c)
+            if list(base[i]) != row:
+                if tbl is None:
+                    tbl = np.array(base, np.int32, copy=True)
+                tbl[i] = row
+        return tbl
+
     @classmethod
-    def from_record(cls, r):
-        """numpy record of _native.TABLE_DTYPE -> SplendorState."""
-        cards, nobles = cards_by_id(), nobles_by_index()
+    def from_record(cls, r, cards=None):
+        """numpy record of _native.TABLE_DTYPE -> SplendorState.  cards (optional, id -> Card): objects
+        to reuse (a state derived from another keeps its Card objects, edits included); every other
+        card is a fresh copy of the canonical data."""
+        nobles = nobles_by_index()
+        own = {} if cards is None else cards
+
+        class _Cards:
+            def __getitem__(self, i):
+                c = own.get(i)
+                if c is None:
+                    c = own[i] = card_copy(i)
+                return c
+        cards = _Cards()
         P = int(r["num_players"])
         players = []
         for p in range(P):

@@ -34,6 +34,7 @@ class SplendorEnv(Env):
         self._view_rec = None    # its record bytes when handed out
         self._seeded = False
         self._terminal = False
+        self._cards = {}
         _native.load_library()  # fail loudly at construction if the HIP engine is missing
         _native.require_gpu()
 
@@ -70,6 +71,8 @@ class SplendorEnv(Env):
         else:                                     # continue this env's np_random stream
             eng.reset(seeds=None)
         self._view = None
+        self._cards = {}  # this episode's Card objects (a new game deals fresh, canonical cards)
+        eng.set_card_table(None)
         obs, mask = self._fetch()
         self._terminal = False
         self.current_player = int(obs[294])
@@ -135,7 +138,7 @@ class SplendorEnv(Env):
         if self._eng is None:
             return None
         if self._view is None:
-            self._view = SplendorState.from_record(self._eng.download(0, 1)[0])
+            self._view = SplendorState.from_record(self._eng.download(0, 1)[0], cards=self._cards)
             self._view_rec = self._view.to_record().tobytes()
         return self._view
 
@@ -149,17 +152,24 @@ class SplendorEnv(Env):
         return int(self.current_player)
 
     def _flush_view(self):
-        """Upload host edits of the view handed out by `state` (no-op when unchanged)."""
+        """Upload host edits of the view handed out by `state` (no-op when unchanged).  Edited card
+        fields (card.cost = ...) switch the env to a context built from the state's card table for
+        the rest of the episode (the edited Card object stays in every later view)."""
         if self._view is None:
             return
         rec = self._view.to_record()
         if rec.tobytes() != self._view_rec:
             self._eng.upload(rec)
             self._view_rec = rec.tobytes()
+        self._cards.update(self._view.cards())
+        self._eng.set_card_table(self._view.card_table())
 
     def set_state(self, state: SplendorState) -> None:
         """Replace the device table by `state` (also what in-place edits of .state do implicitly)."""
-        self._engine().upload(state.to_record())
+        eng = self._engine()
+        eng.upload(state.to_record())
+        self._cards = dict(state.cards())
+        eng.set_card_table(state.card_table())
         self._view = None
         self.current_player = int(state.to_play)
 

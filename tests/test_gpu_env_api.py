@@ -462,3 +462,80 @@ def test_engine_rules_reference_cases():  # test_rules.py:8-43, test_afford_nobl
     assert sum(1 for n in nxt.nobles if n is None) == 1  # exactly one noble per turn
     obs = encode_observation(initial_state(seed=0))
     assert obs.shape == (OBSERVATION_DIM,) and obs.dtype == np.int32
+
+
+def test_affordability_with_an_edited_card_cost():  # test_afford_nobles_obs.py:9-28
+    """The reference test edits a board card's cost in place (card.cost = {...}); the functional API
+    evaluates that state on a context built from the state's card table."""
+    from splendor_gym.engine import apply_action, initial_state, legal_moves
+    from splendor_gym.engine.state import COLOR_INDEX
+    state = initial_state(seed=123)
+    p = state.players[state.to_play]
+    p.tokens = [0, 1, 0, 1, 0, 1]  # one blue, one red, one gold
+    p.bonuses = [0, 0, 0, 1, 0]    # one red bonus
+    card = state.board[1][0]
+    card.cost = {"red": 2, "blue": 2}
+    state.bank = [4, 4, 4, 4, 4, 5]
+    mask = legal_moves(state)
+    assert mask[15] == 1  # buy tier-1 slot 0: red 2-1 bonus = 1 token, blue 2 = 1 token + 1 gold
+    nxt = apply_action(state, 15)
+    prev = nxt.players[(nxt.to_play - 1) % nxt.num_players]
+    assert prev.tokens[COLOR_INDEX["gold"]] <= 1
+    assert all(t >= 0 for t in prev.tokens)
+    # exactly what the edited cost implies (state.py:61-71 + rules.py:101-115): all tokens spent
+    assert prev.tokens == [0, 0, 0, 0, 0, 0]
+    assert nxt.bank == [4, 5, 4, 5, 4, 6]
+    assert all(c is None or c.id != card.id for c in nxt.board[1])  # the edited card left the board
+    # the same buy is illegal with the card's canonical cost whenever that cost is not coverable
+    from splendor_gym.engine.state import cards_by_id
+    canon = cards_by_id()[card.id]
+    base_need = sum(max(0, canon.cost.get(c, 0) - b) for c, b in zip(("white", "blue", "green", "red", "black"),
+                                                                       p.bonuses))
+    if base_need > 3:
+        state.board[1][0] = type(card)(canon.id, canon.tier, canon.color, canon.points, dict(canon.cost))
+        assert legal_moves(state)[15] == 0
+
+
+def test_edited_card_cost_through_the_env_and_the_oracle():
+    """The same edit through SplendorEnv.state (write-through): the env switches to the edited card
+    table for the episode; legal mask, step outputs and the next observation equal the CPU oracle
+    evaluating the edited card table (oracle/splendor_oracle.c with its own card table)."""
+    from splendor_gym.envs import SplendorEnv
+    env = SplendorEnv()
+    obs, info = env.reset(seed=31)
+    s = env.state
+    p = s.players[s.to_play]
+    p.tokens = [0, 1, 0, 1, 0, 1]
+    p.bonuses = [0, 0, 0, 1, 0]
+    card = s.board[1][0]
+    card.cost = {"red": 2, "blue": 2}
+    s.bank = [4, 4, 4, 4, 4, 5]
+    tbl, rec = s.card_table(), s.to_record()
+    assert tbl is not None and list(tbl[card.id][3:]) == [0, 2, 0, 2, 0]
+    m = env.legal_mask()
+    assert m[15] == 1
+    obs2, r, term, trunc, info2 = env.step(15)
+    assert r == 0.0 and not term and info2["action_mask"].shape == (45,)
+    # the CPU oracle on the same edited card table (orc_set_tables), restored afterwards
+    from oracle.oracle import Oracle, table_to_view
+    orc = Oracle()
+    orc.L.orc_set_tables(np.ascontiguousarray(tbl).ctypes.data, orc.nobles.ctypes.data)
+    try:
+        view = table_to_view(rec)
+        ref_mask = orc.legal(view)
+        ref = orc.env_step(view, 15)
+    finally:
+        orc.L.orc_set_tables(orc.cards.ctypes.data, orc.nobles.ctypes.data)
+    assert int((m.astype(np.uint64) << np.arange(45, dtype=np.uint64)).sum()) == ref_mask
+    assert not ref["error"] and np.array_equal(obs2, ref["obs"]) and np.float32(r) == np.float32(ref["reward"])
+    assert int((info2["action_mask"].astype(np.uint64) << np.arange(45, dtype=np.uint64)).sum()) == ref["mask"]
+    after = env.state
+    assert after.players[0].tokens == [0, 0, 0, 0, 0, 0] and after.players[0].bonuses[STD.index(card.color)] >= 1
+    assert after.bank == [4, 5, 4, 5, 4, 6]
+    # the edited object stays the episode's card: a later view shows the edited cost wherever it is
+    assert all(c.cost == {"red": 2, "blue": 2} for c in after.cards().values() if c.id == card.id)
+    env.reset(seed=31)  # a new game deals canonical cards again
+    assert env.state.card_table() is None
+
+
+STD = ["white", "blue", "green", "red", "black"]

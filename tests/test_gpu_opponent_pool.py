@@ -118,7 +118,7 @@ def test_pool_self_play_matches_per_env_wrappers():
     pool.add_snapshot(ms[2])
     fused = {0: FusedActorCritic(ms[0], with_critic=False), 1: FusedActorCritic(ms[1], with_critic=False),
              2: FusedActorCritic(ms[2], with_critic=False)}
-    n, steps, seed = 8, 140, 300
+    n, steps, seed = 256, 140, 300  # >= 256 tables
 
     def greedy_of(net):
         def policy(obs, info):

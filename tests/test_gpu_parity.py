@@ -111,6 +111,14 @@ def test_trajectories_p2_device_policy(orc, refill_period):
     assert resets > 1000
 
 
+def test_trajectories_c2_2000_plies(orc):
+    """SURVEY §8(d) C2 at its specified depth: 2 players, 4 096 tables, 2 000 plies of the device
+    uniform-random policy (with injected illegal / out-of-range actions), the default refill period,
+    every output of every ply bit-compared with the oracle and the full table state every 250 plies."""
+    resets = run_parity(orc, 2, 4096, 2000, 64, 4321, True, check_state_every=250)
+    assert resets > 4096 * 2000 // 90  # ~one episode per 77 plies per table
+
+
 @pytest.mark.parametrize("P", [3, 4])
 def test_trajectories_multiplayer(orc, P):
     resets = run_parity(orc, P, 1024, 200, 8, 99 * P, False)

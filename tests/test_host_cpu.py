@@ -249,3 +249,27 @@ def test_bounds_check_hook_absent_from_product_build():
     assert lib.spl_debug_bounds_flags(ctypes.byref(v), 0) == -1  # product library: not a checked build
     assert b"bounds-check" in lib.spl_last_error()
     assert lib.spl_debug_set_stream_limit(0) == -1 and lib.spl_debug_set_stream_limit(455) == -1
+
+
+def test_edited_cards_make_a_card_table():
+    """Host views own their Card objects (the reference loads fresh cards per game): an in-place cost
+    edit (tests/test_afford_nobles_obs.py:16-17) shows as that state's device card table, a derived
+    state keeps the edited object, and the canonical cards stay untouched."""
+    from oracle.oracle import Oracle, view_to_table
+    from splendor_gym.engine.state import SplendorState, canonical_card_rows, cards_by_id
+    rec = view_to_table(Oracle().initial_state(2, 123))
+    s = SplendorState.from_record(rec)
+    assert s.card_table() is None
+    card = s.board[1][0]
+    card.cost = {"red": 2, "blue": 2}
+    tbl = s.card_table()
+    base = canonical_card_rows()
+    assert tbl.shape == (90, 8) and tbl.dtype == np.int32
+    assert tbl[card.id].tolist() == [card.tier, ["white", "blue", "green", "red", "black"].index(card.color),
+                                     card.points, 0, 2, 0, 2, 0]
+    assert np.array_equal(np.delete(tbl, card.id, 0), np.delete(base, card.id, 0))
+    derived = SplendorState.from_record(rec, cards=s.cards())
+    assert derived.board[1][0] is card and np.array_equal(derived.card_table(), tbl)
+    assert dict(cards_by_id()[card.id].cost) != card.cost
+    fresh = SplendorState.from_record(rec)
+    assert fresh.board[1][0] is not card and fresh.card_table() is None
