@@ -2752,12 +2752,18 @@ __global__ __launch_bounds__(64) void k_observe(KArena A, KTables Tb, int32_t *o
 // walk would touch a new 64-byte segment per lane per byte).
 __global__ __launch_bounds__(64) void k_sample(int n, const int8_t *mask, int32_t *actions, uint64_t seed, uint64_t ply,
                                                int64_t table0) {
-    __shared__ int8_t rows[64 * 45];
+    __shared__ uint32_t rows_w[64 * 45 / 4];
+    int8_t *rows = reinterpret_cast<int8_t *>(rows_w);
     const int t0 = blockIdx.x * 64, lane = lane_id();
     const int nb = min(64, n - t0) * 45;
     const int8_t *src = mask + (size_t)t0 * 45;
-#pragma unroll 5
-    for (int i = lane; i < nb; i += 64) rows[i] = src[i];
+    if ((reinterpret_cast<uintptr_t>(src) & 3u) == 0 && nb == 64 * 45) {  // 720 dwords, 12 per lane
+        const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src);
+#pragma unroll
+        for (int i = lane; i < 64 * 45 / 4; i += 64) rows_w[i] = s4[i];
+    } else {
+        for (int i = lane; i < nb; i += 64) rows[i] = src[i];
+    }
     wave_lds_sync();
     const int t = t0 + lane;
     if (t >= n) return;

@@ -90,7 +90,10 @@ class _OutBlock:
 class SplendorVectorEnv:
     metadata = {"render_modes": [], "autoreset_mode": "same-step"}
     RING = 3  # output blocks kept for copy=True (a loop holding one step's results while stepping needs 2)
-    DEFER_LAG = 2  # check_actions="deferred": a step's error is raised at the latest this many steps later
+    # check_actions="deferred": the running error count is copied back after every DEFER_EVERY-th step
+    # (a step's error is raised at the latest DEFER_EVERY + DEFER_LAG steps later, or by reset())
+    DEFER_EVERY = 4
+    DEFER_LAG = 2
     DEFER_RING = 8
 
     def __init__(self, num_envs, num_players=2, device=None, autoreset=True, refill_period=None, table0=0,
@@ -100,9 +103,9 @@ class SplendorVectorEnv:
         # "sync": the reference's exceptions (out-of-range action, step after termination) are raised
         # by the step() that caused them, which reads one count back from the GPU per step when the
         # actions are a device tensor (host actions are range-checked on the host).  "deferred":
-        # the count is copied back asynchronously and checked without blocking by later calls; a
-        # step's error is raised at the latest by the DEFER_LAG-th step() after it (or by reset()),
-        # so the host never drains the GPU queue.
+        # the count is copied back asynchronously every DEFER_EVERY steps and checked without blocking
+        # by later calls; a step's error is raised at the latest DEFER_EVERY * (DEFER_LAG + 1) steps
+        # after it (or by reset()), so the host never drains the GPU queue.
         self.check_actions = check_actions
         self.num_envs = int(num_envs)
         self.num_players = int(num_players)
@@ -124,6 +127,7 @@ class SplendorVectorEnv:
         self._ring = [self._new_block()]
         self._cur = 0
         self._pending = []  # deferred check: (ring slot, step index) of copies not yet checked
+        self._unchecked = 0  # steps since the last error-count copy (deferred) that may carry an error
         self._pin = torch.zeros(self.DEFER_RING, dtype=torch.int64).pin_memory() if check_actions == "deferred" else None
         self._events = [torch.cuda.Event() for _ in range(self.DEFER_RING)] if check_actions == "deferred" else None
         self._steps = 0
@@ -172,6 +176,8 @@ class SplendorVectorEnv:
         return self._stream
 
     def reset(self, *, seed=None, options=None):
+        if self._unchecked and self.check_actions == "deferred":
+            self._queue_check()
         self._raise_pending(block_all=True)
         seeds = vector_seeds(seed, self.num_envs)
         if seeds is None and not self._seeded:
@@ -193,6 +199,16 @@ class SplendorVectorEnv:
             raise ValueError(f"Action out of bounds for action_space (envs {bad[:8]})")
         raise RuntimeError(f"Cannot call step() after episode termination. Call reset(). (envs {bad[:8]})")
 
+    def _queue_check(self):
+        """Copy the running error count back asynchronously (deferred mode)."""
+        self._unchecked = 0
+        slot = self._steps % self.DEFER_RING
+        if len(self._pending) >= self.DEFER_RING - 1:
+            self._raise_pending(block_all=True)
+        self._pin[slot:slot + 1].copy_(self._errors, non_blocking=True)
+        self._events[slot].record(self._stream_obj)
+        self._pending.append((slot, self._steps))
+
     def _raise_pending(self, block_all=False):
         """Deferred check: raise the error of an earlier step once its count has come back (copies
         that have landed are checked without blocking; one DEFER_LAG steps old, or every one when
@@ -200,7 +216,7 @@ class SplendorVectorEnv:
         while self._pending:
             slot, step = self._pending[0]
             ev = self._events[slot]
-            if not (block_all or self._steps - step >= self.DEFER_LAG or ev.query()):
+            if not (block_all or self._steps - step >= self.DEFER_LAG * self.DEFER_EVERY or ev.query()):
                 break
             ev.synchronize()
             self._pending.pop(0)
@@ -244,18 +260,14 @@ class SplendorVectorEnv:
         self._steps += 1
         # the step-after-termination error needs autoreset off; out-of-range host actions were caught
         if not (host_checked and self.autoreset):
+            self._unchecked += 1
             if self.check_actions == "sync":
                 count = int(self._errors.item())
                 if count != self._errors_seen:
                     self._errors_seen = count
                     self._raise_errors(b.flags)
-            else:
-                slot = self._steps % self.DEFER_RING
-                if len(self._pending) >= self.DEFER_RING - 1:
-                    self._raise_pending(block_all=True)
-                self._pin[slot:slot + 1].copy_(self._errors, non_blocking=True)
-                self._events[slot].record(self._stream_obj)
-                self._pending.append((slot, self._steps))
+            elif self._unchecked >= self.DEFER_EVERY:
+                self._queue_check()
         info = {
             "action_mask": b.mask,
             "to_play": b.to_play,

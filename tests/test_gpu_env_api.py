@@ -376,9 +376,9 @@ def test_vector_env_action_errors():
             with pytest.raises(ValueError, match="envs \\[9\\]"):
                 vec.step(dev_bad)
         else:
-            vec.step(dev_bad)  # returns; the error comes back with a later call (DEFER_LAG at the latest)
+            vec.step(dev_bad)  # returns; the error comes back with a later call
             with pytest.raises(ValueError, match="deferred"):
-                for k in range(vec.DEFER_LAG):
+                for k in range(vec.DEFER_EVERY * (vec.DEFER_LAG + 1)):
                     vec.step(vec.sample_actions(seed=2, ply=2 + k).clone())
             vec.step(dev_bad)
             with pytest.raises(ValueError, match="deferred"):
