@@ -172,6 +172,73 @@ def load_pmc_traffic(kernel, tables, steps_per_launch):
     return None, None
 
 
+def selfplay_line(dev, rank, world, N, iters, warmup):
+    """BASELINE config 5 per GPU: the PPO rollout step of ppo_splendor.py:227-269 for N tables —
+    the agent's fused fp32 ActorCritic (get_action_and_value: actor + critic + masked sample) and
+    DualStepVectorEnv.dual_step with the reference's opponent supplier (current policy p=0.25, else
+    one of 12 frozen snapshots per episode, greedy; reset after done), all weights from the
+    reference checkpoint (tests/golden/ppo_splendor_latest.safetensors, fixture data), captured in a
+    hipGraph.  A dual step is two env-steps.  Timed like the headline: barrier +
+    synchronize around `iters` replays, max over ranks."""
+    import torch
+    from safetensors.torch import load_file
+    from splendor_gym.fused_policy import FusedActorCritic, OpponentPool
+    from splendor_gym.parallel import barrier, max_over_ranks
+    from splendor_gym.policy import ActorCritic
+    from splendor_gym.selfplay import DualStepVectorEnv
+    ckpt = os.path.join(REPO, "tests", "golden", "ppo_splendor_latest.safetensors")
+
+    def net():
+        m = ActorCritic().to(dev).eval()
+        m.load_state_dict(load_file(ckpt, device=str(dev)))
+        return m
+
+    agent = net()
+    agent_k = FusedActorCritic(agent, precision="fp32")
+    pool = OpponentPool(agent, pool_size=12, p_current=0.25, seed=99)
+    for _ in range(12):
+        pool.add_snapshot(net())
+    env = DualStepVectorEnv(N, device=dev, opponent=pool, table0=rank * N, opponent_obs=False)
+    obs, info = env.reset(seed=rank * N)
+    mask = info["action_mask"]
+    ply_t = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def iteration():
+        with torch.no_grad():
+            ply_t.add_(1)
+            a, _, _, _ = agent_k.act(obs, mask, seed=1234, table0=rank * N, ply_base=ply_t)
+            return env.dual_step(a)
+
+    for _ in range(warmup):
+        iteration()
+    torch.cuda.synchronize(dev)
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        iteration()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        iteration()
+    graph.replay()
+    torch.cuda.synchronize(dev)
+    barrier(dev)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        graph.replay()
+    torch.cuda.synchronize(dev)
+    barrier(dev)
+    el = max_over_ranks(time.perf_counter() - t0, device=dev)
+    env.close()
+    return {"metric": f"env-steps/sec (whole node), 2p self-play, on-device fp32 ActorCritic, {N} tables/GPU",
+            "value": round(2 * N * world * iters / el, 1), "unit": "env-steps/s",
+            "ms_per_dual_step": round(el / iters * 1e3, 4), "iters": iters, "dtype": "fp32",
+            "config": {"workload": "BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused fp32 MFMA) + "
+                                   "DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of 12 frozen "
+                                   "snapshots per episode, greedy), reset after done; hipGraph replays",
+                       "tables_per_gpu": N, "weights": "reference checkpoint runs/ppo_splendor/ppo_splendor_latest.pt"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,6 +268,9 @@ def main():
     ap.add_argument("--pipeline", choices=("auto", "always", "half", "off"), default="auto",
                     help="rollout mode: two-wave pipelined kernel (auto: 32 or 64 tables per workgroup by grid "
                          "size; always: 64; half: 32) vs one wave per 64 tables (off)")
+    ap.add_argument("--sp-tables", type=int, default=65536,
+                    help="tables per GPU of the config-5 self-play line (0 = skip it)")
+    ap.add_argument("--sp-iters", type=int, default=64, help="timed dual steps of the config-5 line")
     ap.add_argument("--delegation", type=int, default=0,
                     help="rollout store: every n-th step the odd-XCC workgroups' rows are stored by their "
                          "even-XCC partners (0 = off, the library default: a 1.5 %% gain, "
@@ -379,6 +449,9 @@ def main():
     for v in variants:
         recs[v] = measure(v, k_next)
         k_next = recs[v]["k_next"]
+    sp = None
+    if args.sp_tables > 0 and not args.only:
+        sp = selfplay_line(dev, rank, world, args.sp_tables, args.sp_iters, warmup=8)
     # correctness canaries on the measured run: no error flags, episodes completed
     bad = int(((eng.flags & (_native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT)) != 0).sum().item())
     rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
@@ -464,6 +537,8 @@ def main():
             s = with_traffic(summary(recs[v]))
             s.pop("plan")
             out["in_place_l3" if v == "rollout_inplace" else ("other_mode" if v == "step" else v)] = s
+        if sp is not None:
+            out["config5_selfplay"] = sp
         print(json.dumps(out))
     eng.close()
     if world > 1:

@@ -2759,8 +2759,12 @@ __global__ __launch_bounds__(64) void k_sample(int n, const int8_t *mask, int32_
     const int8_t *src = mask + (size_t)t0 * 45;
     if ((reinterpret_cast<uintptr_t>(src) & 3u) == 0 && nb == 64 * 45) {  // 720 dwords, 12 per lane
         const uint32_t *s4 = reinterpret_cast<const uint32_t *>(src);
+        uint32_t v[12];
 #pragma unroll
-        for (int i = lane; i < 64 * 45 / 4; i += 64) rows_w[i] = s4[i];
+        for (int j = 0; j < 12; ++j) v[j] = lane + 64 * j < 720 ? s4[lane + 64 * j] : 0u;
+#pragma unroll
+        for (int j = 0; j < 12; ++j)
+            if (lane + 64 * j < 720) rows_w[lane + 64 * j] = v[j];
     } else {
         for (int i = lane; i < nb; i += 64) rows[i] = src[i];
     }

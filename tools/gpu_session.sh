@@ -2,7 +2,7 @@
 # One GPU session (round 3).  Steps by name, run in order; each GPU step has its own time limit and
 # the chain stops at the first failure.
 #   tools/gpu_session.sh TAG step [step ...]
-# steps: tests smoke driver prof deleg multi pmc2p pmcmulti selfplay vec policy
+# steps: tests smoke driver prof deleg profc4 pmcc4 multi pmc2p pmcmulti selfplay vec policy
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -31,6 +31,12 @@ for step in "$@"; do
           find $O/prof_driver_$TAG -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats_driver_$TAG.csv \;
       head -8 $O/kernel_stats_driver_$TAG.csv ;;
     deleg) run deleg_ab 600 python3 tools/deleg_ab.py --rounds 12 --arms 0,6 ;;
+    profc4)
+      run prof_c4 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4_$TAG -o run -- \
+          python3 bench.py --no-cpu-baseline --players 4 --tables 32768
+      cp $O/prof_c4_$TAG/run_kernel_stats.csv $O/kernel_stats_c4_$TAG.csv; head -5 $O/kernel_stats_c4_$TAG.csv | cut -c1-160 ;;
+    pmcc4) bash tools/pmc.sh ${TAG}_4p_32768 4 32768 store all || exit 1
+           bash tools/pmc.sh ${TAG}_4p_32768_inplace 4 32768 inplace traffic || exit 1 ;;
     multi)
       run bench_3p 600 python3 bench.py --no-cpu-baseline --players 3
       run bench_4p 600 python3 bench.py --no-cpu-baseline --players 4
