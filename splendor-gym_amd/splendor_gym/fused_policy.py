@@ -156,9 +156,12 @@ class OpponentPool:
     (spl_policy_act_grouped: tables sorted by network, one network per workgroup), fp32.
 
     Images: slot 0 is the current policy (re-packed by refresh(), e.g. after each PPO update);
-    snapshots live in a ring of pool_size + 2 slots, so a snapshot that leaves the pool keeps its
-    weights until two more snapshots are added — episodes already playing it finish against it, as
-    the reference's per-episode frozen copies do.  (The reference appends agent.state_dict(), whose
+    snapshots live in a ring of pool_size + 2 slots.  A snapshot that leaves the pool keeps its
+    weights while any table's current episode still plays it (the per-table opponent tensors of the
+    envs using the pool are tracked: DualStepVectorEnv registers its own), so episodes already
+    playing it finish against it, as the reference's per-episode frozen copies do; add_snapshot
+    writes the next ring slot that no pool member and no running episode uses, growing the ring
+    (up to 64 images) when every slot is busy.  (The reference appends agent.state_dict(), whose
     tensors alias the live parameters, so its "frozen" pool entries are the current weights at the
     episode's start; add_snapshot here copies the weights at the time it is called.)"""
 
@@ -179,7 +182,31 @@ class OpponentPool:
         self.slots = torch.zeros(max(1, self.pool_size), dtype=torch.int32, device=self.device)
         self._scratch = None
         self._keep = []
+        self._users = []  # per-table image-slot tensors of the envs playing this pool (track())
         self.refresh()
+
+    def track(self, group_of):
+        """Register a per-table opponent tensor (image slot per table): add_snapshot never overwrites
+        a slot that one of its tables still plays."""
+        self._users.append(group_of)
+
+    def _in_use(self):
+        used = set()
+        for g in self._users:
+            used.update(int(x) for x in self.torch.unique(g).tolist())
+        return used
+
+    def _grow(self):
+        """One more image slot (the ring is full of snapshots still in play)."""
+        if self.n_images >= 64:
+            raise RuntimeError("OpponentPool: every one of the 64 image slots is in play; add snapshots less often "
+                               "than episodes end")
+        t = self.torch
+        bigger = t.zeros((self.n_images + 1) * self.image_bytes, dtype=t.uint8, device=self.device)
+        bigger[:self.images.numel()].copy_(self.images)
+        self.images = bigger
+        self.n_images += 1
+        return self.n_images - 1
 
     def _stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
@@ -200,8 +227,12 @@ class OpponentPool:
     def add_snapshot(self, model=None):
         """pool.append(snapshot); pool.pop(0) beyond pool_size (ppo_splendor.py:366-370).  `model`
         defaults to the agent (its weights now)."""
-        slot = 1 + self._next
-        self._next = (self._next + 1) % (self.n_images - 1)
+        busy = set(self.pool) | self._in_use() | {0}
+        ring = self.n_images - 1
+        slot = next((1 + (self._next + k) % ring for k in range(ring) if 1 + (self._next + k) % ring not in busy), None)
+        if slot is None:
+            slot = self._grow()
+        self._next = slot % (self.n_images - 1)  # the ring position after `slot`
         self._pack(self.agent if model is None else model, slot)
         self.pool.append(slot)
         if len(self.pool) > self.pool_size:

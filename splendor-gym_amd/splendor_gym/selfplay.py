@@ -92,6 +92,7 @@ class DualStepVectorEnv:
         if self.pool is not None:  # per-table opponent of the current episode, and each table's episode count
             self.opp_group = z(t.int32)
             self.episode = z(t.int32)
+            self.pool.track(self.opp_group)  # slots still in play are not overwritten by add_snapshot
         e = self.eng
         ra, ta, fa, wa = self.small_a
         p = lambda x: None if x is None else x.data_ptr()

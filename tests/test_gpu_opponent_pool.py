@@ -162,3 +162,33 @@ def test_pool_self_play_matches_per_env_wrappers():
         assert info_v["opponent_index"].cpu().tolist() == [s.groups[-1] for s in sups], k
     assert ended >= n
     assert len({g for s in sups for g in s.groups}) == 3  # all three networks played
+
+
+def test_snapshot_in_play_is_not_overwritten():
+    """a snapshot that left the pool must keep its weights while a table's running episode
+    still plays it; add_snapshot skips busy slots (and grows the ring when all are busy)."""
+    import torch
+    from splendor_gym.fused_policy import OpponentPool
+    ms = models(6, seed=21)
+    pool = OpponentPool(ms[0], pool_size=1, p_current=0.0, seed=1)  # ring of 3 snapshot slots
+    playing = torch.zeros(8, dtype=torch.int32, device="cuda")
+    pool.track(playing)
+    pool.add_snapshot(ms[1])
+    first = pool.pool[0]
+    playing[3] = first  # table 3's episode plays the first snapshot
+    img = pool.images[first * pool.image_bytes:(first + 1) * pool.image_bytes].clone()
+    for m in ms[2:]:
+        pool.add_snapshot(m)  # the first leaves the pool at once (pool_size 1)
+        assert first not in pool.pool
+        assert torch.equal(pool.images[first * pool.image_bytes:(first + 1) * pool.image_bytes], img)
+    assert pool.n_images == 1 + 1 + 2  # one busy slot fits the ring: no growth needed
+    # every non-member slot busy: the ring grows instead of overwriting
+    playing[:3] = torch.tensor([s for s in range(1, pool.n_images) if s not in pool.pool and s != first][:3],
+                               dtype=torch.int32)
+    n0 = pool.n_images
+    pool.add_snapshot(ms[1])
+    assert pool.n_images == n0 + 1 and pool.pool[-1] == n0
+    assert torch.equal(pool.images[first * pool.image_bytes:(first + 1) * pool.image_bytes], img)
+    playing.zero_()
+    pool.add_snapshot(ms[2])  # nothing busy: the ring position moves on, reusing freed slots
+    assert pool.pool[-1] != n0
