@@ -49,6 +49,12 @@ for step in "$@"; do
               bash tools/pmc.sh ${TAG}_4p_32768 4 32768 store all || exit 1 ;;
     selfplay) run sp_pool 300 python tools/bench_selfplay.py
               run sp_frozen 300 python tools/bench_selfplay.py --opponent frozen ;;
+    bench) run bench_default 600 python3 bench.py ;;
+    rank2)  # the driver's N>1 launch rehearsed with 2 ranks on this one card (collectives over gloo)
+      export SPLENDOR_DIST_BACKEND=gloo
+      run bench_2rank 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 20 --warmup 5
+      unset SPLENDOR_DIST_BACKEND ;;
     vec) run vec_step 300 python tools/bench_vec_step.py
          run prof_vec 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_vec_$TAG -o run -- python3 tools/bench_vec_step.py
          cp $O/prof_vec_$TAG/run_kernel_stats.csv $O/kernel_stats_vec_$TAG.csv; head -6 $O/kernel_stats_vec_$TAG.csv | cut -c1-200 ;;
