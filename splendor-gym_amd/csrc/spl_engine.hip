@@ -1905,11 +1905,13 @@ __device__ __forceinline__ void ws_sync() {
 template <int P>
 struct __align__(16) StepWsLDS : Consts {
     static constexpr int kW = SW_COUNT + 4 * P;  // state words per table
+    static constexpr int kTermRows = 16;  // terminal rows the rules wave encodes per step (the rest: output wave)
     uint32_t st[kW][64];   // state after the step (and autoreset)
     uint32_t fst[kW][64];  // pre-reset state of the tables that ended (final_observation)
     uint64_t mask[64];
-    uint64_t fin;          // lanes with a terminal row
+    uint64_t fin;          // terminal rows left to the output wave (beyond kTermRows)
     uint32_t mbits[96];
+    uint32_t trow[kTermRows][75];  // the rules wave's terminal rows, compacted (297 bytes in 75 dwords)
     uint8_t rows[64 * kObsDim];  // observation staging; before hand-off 1 the rules wave's deal scratch + LaneMT
 };
 static_assert(sizeof(StepWsLDS<4>) <= 40960, "k_step_ws_* needs four workgroups per CU");
@@ -1953,7 +1955,12 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
 #pragma unroll
             for (int w = 0; w < kW; ++w) L.fst[w][lane] = tab_word(T, w);
         }
-        const uint64_t fin = __ballot(fin_me);
+        // terminal rows: the first kTermRows of the wave are encoded and stored by this wave after
+        // hand-off 1 (it has no gathers left then), the rest by the output wave
+        const uint64_t fin_all = __ballot(fin_me);
+        const int fidx = __popcll(fin_all & ((1ull << lane) - 1ull));
+        const uint64_t fin_rules = __ballot(fin_me && fidx < StepWsLDS<P>::kTermRows);
+        const uint64_t fin = fin_all & ~fin_rules;
         if (lane == 0) L.fin = fin;
         const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;
         bool pool_dirty = false;
@@ -1964,6 +1971,30 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         STAMP(3);
         ws_sync();  // hand-off 1: state words (deal scratch in `rows` free again)
         STAMP(4);
+        if (fin_rules) {  // info["final_observation"] rows, compacted in trow, stored row by row
+            Tab<P> F;
+#pragma unroll
+            for (int w = 0; w < kW; ++w) set_tab_word(F, w, L.fst[w][lane]);
+            const bool mine = (fin_rules >> lane) & 1ull;
+            if (mine) {
+                uint32_t R[76];
+                build_row(F, L, R);
+#pragma unroll
+                for (int j = 0; j < 75; ++j) L.trow[fidx][j] = R[j];
+            }
+            wave_lds_sync();
+            const uint8_t *tb = reinterpret_cast<const uint8_t *>(&L.trow[0][0]);
+            int k = 0;
+            for (uint64_t m = fin_rules; m; m &= m - 1, ++k) {
+                const int r = __ffsll((unsigned long long)m) - 1;
+                int32_t *dst = S.final_obs + (size_t)(t0 + r) * kObsDim;
+                for (int e = lane; e < kObsDim; e += 64) dst[e] = (int32_t)tb[k * 300 + e];
+            }
+            if (__any(mine && get_moves(F.sw) > 255)) {  // move_count > 255: crafted states only
+                __builtin_amdgcn_s_waitcnt(0);
+                if (mine && get_moves(F.sw) > 255) S.final_obs[(size_t)t * kObsDim + 295] = get_moves(F.sw);
+            }
+        }
         if (o.mask & kMaskDeferred) o.mask = legal_of(T, L);
         STAMP(5);
         // masks and small outputs leave from this wave while the output wave streams the rows
