@@ -211,6 +211,69 @@ __device__ __forceinline__ void layer_tanh(Enter &enter, const float (&B)[NB], f
     }
 }
 
+// The per-table epilogue over one table's 45 logits (`row`) and mask bytes: greedy masked argmax
+// (training_utils.py:263-276) or masked_categorical's sample, log-prob and entropy, plus the critic
+// value (ppo_splendor.py:40-59).
+template <bool kCritic, bool kSample>
+__device__ __forceinline__ void act_epilogue(const ActArgs &a, const float *row, const uint8_t *mrow, int64_t t,
+                                             float value) {
+    float lv[kAct];
+    uint64_t legal = 0;
+#pragma unroll
+    for (int k = 0; k < kAct; ++k) {
+        lv[k] = row[k];
+        legal |= (uint64_t)(mrow[k] != 0) << k;
+    }
+    int act = 0;
+    if constexpr (!kSample) {
+        // logits.masked_fill(mask < 0.5, -inf).argmax(): first maximum; all-illegal -> 0
+        float best = -__builtin_inff();
+#pragma unroll
+        for (int k = 0; k < kAct; ++k) {
+            const bool better = ((legal >> k) & 1) && lv[k] > best;
+            best = better ? lv[k] : best;
+            act = better ? k : act;
+        }
+    } else {
+        // masked_categorical: illegal -> -inf unless the row has no legal action; fp32 softmax
+        const uint64_t allow = legal ? legal : (1ull << kAct) - 1;
+        float mx = -__builtin_inff();
+#pragma unroll
+        for (int k = 0; k < kAct; ++k) mx = ((allow >> k) & 1) ? fmaxf(mx, lv[k]) : mx;
+        float S = 0.f, T = 0.f;
+#pragma unroll
+        for (int k = 0; k < kAct; ++k) {
+            const float d = lv[k] - mx, p = ((allow >> k) & 1) ? expf(d) : 0.f;
+            lv[k] = p;
+            S += p;
+            T += p * d;
+        }
+        const float logS = logf(S);
+        const uint64_t ply = a.ply + (a.ply_base ? *a.ply_base : 0ull);
+        const uint4 rnd = philox4x32(make_uint4((uint32_t)(a.table0 + t), (uint32_t)((uint64_t)(a.table0 + t) >> 32),
+                                                (uint32_t)ply, (uint32_t)(ply >> 32)),
+                                     make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32) ^ 0xA5C3E1F7u));
+        const float target = (float)(rnd.x >> 8) * (1.f / 16777216.f) * S;
+        float cum = 0.f;
+        int last = 0;
+        bool found = false;
+#pragma unroll
+        for (int k = 0; k < kAct; ++k) {
+            const bool al = (allow >> k) & 1;
+            cum += lv[k];
+            last = al ? k : last;
+            const bool hit = al && !found && cum > target;
+            act = hit ? k : act;
+            found = found || hit;
+        }
+        if (!found) act = last;
+        if (a.logprob) a.logprob[t] = row[act] - mx - logS;
+        if (a.entropy) a.entropy[t] = logS - T / S;
+        if (kCritic) a.value[t] = value;
+    }
+    a.action[t] = act;
+}
+
 // <false, false> greedy actor, <false, true> sampling actor, <true, true> critic + sampling actor
 // (get_action_and_value), <true, false> critic only (ActorCritic.get_value, ppo_splendor.py:51)
 template <bool kCritic, bool kSample>
@@ -348,66 +411,112 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         for (int i = lane; i < valid * kAct; i += 64)
             a.logits[table_of(i / kAct) * kAct + i % kAct] = lg[(i / kAct) * kLogitRow + i % kAct];
     }
-    if (g == 0 && r < valid) {
-        const int64_t t = table_of(r);
-        const float *row = lg + r * kLogitRow;
-        const uint8_t *mrow = ms + r * kAct;
-        float lv[kAct];
-        uint64_t legal = 0;
+    if (g == 0 && r < valid) act_epilogue<kCritic, kSample>(a, lg + r * kLogitRow, ms + r * kAct, table_of(r), value);
+}
+
+// ---- narrow workgroups: the tails of the grouped evaluation ----------------------------------
+// 65 536 tables fill exactly two rounds of one 128-table workgroup per CU, so the partial last
+// workgroup of every network (the group's tail) used to spill into a third round that took a whole
+// round's time (each wave's MFMA chain is latency-bound, however few tables it carries).  A group's
+// full 128-table workgroups stay in k_act32; its tail runs here in wave-tiles of 16 tables, ONE
+// wave-tile per workgroup, the 16 output tiles of each hidden layer split over the 8 waves (wave w:
+// tiles w and w + 8), the weights read straight from the image (L2-resident, shared by every
+// workgroup of the network) with a deeper software prefetch than the LDS ring needs, and each
+// layer's outputs exchanged through LDS.  A tail wave-tile takes ~1/8 of a full workgroup's time.
+template <int KS, int NB>
+__device__ __forceinline__ f32x4 tile_mma_global(const uint8_t *chunk, const float (&B)[NB], int lane) {
+    static_assert(KS <= NB && KS % 4 == 0, "B fragments");
+    constexpr int NG = KS / 4, D = 6, NR = D + 1;  // A fragments 6 groups (24 MFMAs) ahead: an L2 round trip
+    const float *bias = reinterpret_cast<const float *>(chunk + kBiasOff) + 4 * (lane >> 4);
+    f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
+    const f32x4 *A = reinterpret_cast<const f32x4 *>(chunk) + lane;
+    f32x4 af[NR];
 #pragma unroll
-        for (int k = 0; k < kAct; ++k) {
-            lv[k] = row[k];
-            legal |= (uint64_t)(mrow[k] != 0) << k;
-        }
-        int act = 0;
-        if constexpr (!kSample) {
-            // logits.masked_fill(mask < 0.5, -inf).argmax(): first maximum; all-illegal -> 0
-            float best = -__builtin_inff();
+    for (int q = 0; q < D; ++q) af[q] = A[q * 64];
 #pragma unroll
-            for (int k = 0; k < kAct; ++k) {
-                const bool better = ((legal >> k) & 1) && lv[k] > best;
-                best = better ? lv[k] : best;
-                act = better ? k : act;
-            }
-        } else {
-            // masked_categorical: illegal -> -inf unless the row has no legal action; fp32 softmax
-            const uint64_t allow = legal ? legal : (1ull << kAct) - 1;
-            float mx = -__builtin_inff();
+    for (int q = 0; q < NG; ++q) {
+        if (q + D < NG) af[(q + D) % NR] = A[(q + D) * 64];
 #pragma unroll
-            for (int k = 0; k < kAct; ++k) mx = ((allow >> k) & 1) ? fmaxf(mx, lv[k]) : mx;
-            float S = 0.f, T = 0.f;
-#pragma unroll
-            for (int k = 0; k < kAct; ++k) {
-                const float d = lv[k] - mx, p = ((allow >> k) & 1) ? expf(d) : 0.f;
-                lv[k] = p;
-                S += p;
-                T += p * d;
-            }
-            const float logS = logf(S);
-            const uint64_t ply = a.ply + (a.ply_base ? *a.ply_base : 0ull);
-            const uint4 rnd = philox4x32(make_uint4((uint32_t)(a.table0 + t), (uint32_t)((uint64_t)(a.table0 + t) >> 32),
-                                                    (uint32_t)ply, (uint32_t)(ply >> 32)),
-                                         make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32) ^ 0xA5C3E1F7u));
-            const float target = (float)(rnd.x >> 8) * (1.f / 16777216.f) * S;
-            float cum = 0.f;
-            int last = 0;
-            bool found = false;
-#pragma unroll
-            for (int k = 0; k < kAct; ++k) {
-                const bool al = (allow >> k) & 1;
-                cum += lv[k];
-                last = al ? k : last;
-                const bool hit = al && !found && cum > target;
-                act = hit ? k : act;
-                found = found || hit;
-            }
-            if (!found) act = last;
-            if (a.logprob) a.logprob[t] = row[act] - mx - logS;
-            if (a.entropy) a.entropy[t] = logS - T / S;
-            if (kCritic) a.value[t] = value;
-        }
-        a.action[t] = act;
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[q % NR][j], B[4 * q + j], acc, 0, 0, 0);
     }
+    return acc;
+}
+
+// one hidden layer split over the 8 waves: tiles wave and wave + 8, then every wave gathers all
+// 16 tiles' tanh outputs (its next layer's B fragments) from LDS
+template <int KS, int NB>
+__device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const float (&B)[NB], float (&H)[kKs2],
+                                             float *xbuf, int wave, int lane) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int t = wave + 8 * h;
+        const f32x4 acc = tile_mma_global<KS>(W + (size_t)(chunk0 + t) * kChunk, B, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xbuf[(4 * t + i) * 64 + lane] = tanh_f32(acc[i]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kKs2; ++k) H[k] = xbuf[k * 64 + lane];
+    __syncthreads();  // xbuf is written again by the next layer
+}
+
+template <bool kSample>
+__global__ __launch_bounds__(512) void k_act32_narrow(const uint8_t *__restrict__ Wbase, ActArgs a) {
+    __shared__ __attribute__((aligned(16))) float xbuf[kTiles * 4 * 64];  // 16 KB: one layer's outputs
+    __shared__ float lg[kRowsPerWave * kLogitRow];
+    __shared__ uint8_t ms[kMaskWave];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+    const int b = (int)blockIdx.x, G = a.groups;
+    const int32_t *ntab = a.gtab + 2 * G + 2;  // per group: first narrow workgroup; ntab[G] = total
+    if (b >= ntab[G]) return;                  // past the last tail's workgroups (every wave leaves)
+    int grp = 0;
+    for (int i = 1; i < G; ++i) grp = ntab[i] <= b ? i : grp;
+    const uint8_t *W = Wbase + (size_t)grp * a.image_stride;
+    const int64_t gfirst = a.gtab[G + 1 + grp], gend = a.gtab[G + 2 + grp];
+    const int64_t tbase = gfirst + (gend - gfirst) / kRowsPerBlock * kRowsPerBlock + (int64_t)(b - ntab[grp]) * kRowsPerWave;
+    const int valid = (int)max<int64_t>(0, min<int64_t>(kRowsPerWave, gend - tbase));
+    const int32_t tid_own = lane < valid ? a.order[tbase + lane] : 0;
+    const int64_t xt = valid > 0 ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : 0;
+    const int32_t *xrow = a.obs + (size_t)xt * kObs;
+    float X[kKs1];
+#pragma unroll
+    for (int s = 0; s < kKs1; ++s) {
+        const int k = 4 * s + g;
+        X[s] = k < kObs ? (float)xrow[k < kObs ? k : 0] : 0.f;
+    }
+    if (wave == 0) {  // the wave-tile's mask bytes (gathered rows), for the epilogue
+        constexpr int kMI = (kMaskWave + 63) / 64;
+        uint32_t mv[kMI];
+#pragma unroll
+        for (int i = 0; i < kMI; ++i) {
+            const int e = lane + 64 * i, row = e / kAct;
+            const int32_t tt = __shfl(tid_own, row < kRowsPerWave ? row : 0);
+            mv[i] = e < valid * kAct ? (uint32_t)(uint8_t)a.mask[(int64_t)tt * kAct + e % kAct] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < kMI; ++i) {
+            const int e = lane + 64 * i;
+            if (e < valid * kAct) ms[e] = (uint8_t)mv[i];
+        }
+    }
+    float H1[kKs2], H2[kKs2];
+    narrow_layer<kKs1>(W, 0, X, H1, xbuf, wave, lane);
+    narrow_layer<kKs2>(W, kTiles, H1, H2, xbuf, wave, lane);
+    if (wave < kActTiles) {  // logits: waves 0..2 take one 16-row tile each
+        const f32x4 L = tile_mma_global<kKs2>(W + (size_t)(2 * kTiles + wave) * kChunk, H2, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int act = 16 * wave + 4 * g + i;
+            if (act < kAct) lg[r * kLogitRow + act] = L[i];
+        }
+    }
+    __syncthreads();
+    if (wave == 0 && a.logits) {
+        for (int i = lane; i < valid * kAct; i += 64)
+            a.logits[(int64_t)a.order[tbase + i / kAct] * kAct + i % kAct] = lg[(i / kAct) * kLogitRow + i % kAct];
+    }
+    if (wave == 0 && g == 0 && r < valid)
+        act_epilogue<false, kSample>(a, lg + r * kLogitRow, ms + r * kAct, (int64_t)__shfl(tid_own, r), 0.f);
 }
 
 }  // namespace splp32
@@ -443,17 +552,23 @@ __global__ __launch_bounds__(256) void k_group_count(int n, int G, const int32_t
     if (threadIdx.x < G && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
 }
 
+// per group g: gtab[g] its first full (128-table) workgroup of k_act32, gtab[G + 1 + g] its first
+// position in `order`, ntab[g] its first narrow (16-table tail) workgroup of k_act32_narrow
 __global__ __launch_bounds__(64) void k_group_scan(int G, int32_t *counts, int32_t *cursor, int32_t *gtab) {
     if (threadIdx.x != 0) return;
-    int wg = 0, pos = 0;
+    int32_t *ntab = gtab + 2 * G + 2;
+    int wg = 0, nw = 0, pos = 0;
     for (int g = 0; g < G; ++g) {
         gtab[g] = wg;
+        ntab[g] = nw;
         gtab[G + 1 + g] = pos;
         cursor[g] = pos;
-        wg += (counts[g] + kRowsPerBlock - 1) / kRowsPerBlock;
+        wg += counts[g] / kRowsPerBlock;
+        nw += (counts[g] % kRowsPerBlock + kRowsPerWave - 1) / kRowsPerWave;
         pos += counts[g];
     }
     gtab[G] = wg;
+    ntab[G] = nw;
     gtab[2 * G + 1] = pos;
 }
 
@@ -478,7 +593,7 @@ __global__ __launch_bounds__(256) void k_group_scatter(int n, int G, const int32
 
 constexpr int kMaxGroups = 64;
 
-int64_t splp32_group_scratch(int32_t n, int32_t groups) { return 4 * ((int64_t)4 * groups + 2 + n); }
+int64_t splp32_group_scratch(int32_t n, int32_t groups) { return 4 * ((int64_t)5 * groups + 3 + n); }
 
 // image: a packed fp32 image (full when has_critic); critic: evaluate the critic (SAMPLE with value)
 int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, int32_t n, const spl_act_args_t *args,
@@ -492,8 +607,9 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
     if (groups > 0) {  // sort the tables by network, then one workgroup per 128 tables of one group
         if (groups > kMaxGroups) return spl_fail(SPL_E_ARG, "at most 64 networks per grouped call");
         if (critic) return spl_fail(SPL_E_ARG, "grouped evaluation serves actor-only images");
+        // scratch: counts[G] | cursor[G] | gtab[2G + 2] | ntab[G + 1] | order[n]
         int32_t *counts = static_cast<int32_t *>(scratch), *cursor = counts + groups, *gtab = cursor + groups;
-        int32_t *order = gtab + 2 * groups + 2;
+        int32_t *order = gtab + 2 * groups + 2 + groups + 1;
         const hipStream_t s = (hipStream_t)stream;
         if (hipMemsetAsync(counts, 0, sizeof(int32_t) * groups, s) != hipSuccess)
             return spl_fail(SPL_E_HIP, "group scratch clear");
@@ -505,7 +621,7 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
         a.gtab = gtab;
         a.groups = groups;
         a.image_stride = image_stride;
-        grid.x += groups;  // every group may end in a partial workgroup
+        // full workgroups only (at most n / 128 of them); the tails go to k_act32_narrow below
     }
     const hipStream_t s = (hipStream_t)stream;
     const uint8_t *W = img;
@@ -518,6 +634,13 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
         hipLaunchKernelGGL((k_act32<false, true>), grid, block, 0, s, W, a);
     else
         hipLaunchKernelGGL((k_act32<false, false>), grid, block, 0, s, W, a);
+    if (groups > 0) {  // the groups' tails: at most 8 wave-tiles of 16 tables per group
+        const dim3 ngrid((unsigned)(groups * (kRowsPerBlock / kRowsPerWave)));
+        if (sample)
+            hipLaunchKernelGGL((k_act32_narrow<true>), ngrid, block, 0, s, W, a);
+        else
+            hipLaunchKernelGGL((k_act32_narrow<false>), ngrid, block, 0, s, W, a);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return spl_fail(SPL_E_HIP, std::string("k_act32 launch: ") + hipGetErrorString(e));
     return SPL_OK;

@@ -75,6 +75,42 @@ def test_grouped_act_equals_each_network():
     assert (out == 77).all()
 
 
+@pytest.mark.parametrize("n", [5000, 65536])
+def test_grouped_sampling_and_logits_equal_each_network(n):
+    """spl_policy_act_grouped in SAMPLE mode with logits: full 128-table workgroups (k_act32) and the
+    16-table tail workgroups (k_act32_narrow, hidden units split over the waves, weights from global
+    memory) give every table exactly its own network's logits, action and log-prob — the draw is
+    keyed by the table id, so it equals the per-network launch's."""
+    import ctypes
+    import torch
+    from splendor_gym import _native
+    from splendor_gym.fused_policy import FusedActorCritic, OpponentPool
+    ms = models(5, seed=8)
+    pool = OpponentPool(ms[0], pool_size=4)
+    for m in ms[1:]:
+        pool.add_snapshot(m)
+    obs, mask = states(n, seed=2)
+    g = torch.randint(0, 5, (n,), dtype=torch.int32, device=obs.device)
+    act = torch.empty(n, dtype=torch.int32, device=obs.device)
+    lp = torch.empty(n, dtype=torch.float32, device=obs.device)
+    ent = torch.empty(n, dtype=torch.float32, device=obs.device)
+    lg = torch.empty(n, 45, dtype=torch.float32, device=obs.device)
+    nb = int(pool.lib.spl_policy_group_scratch_bytes(n, pool.n_images))
+    scratch = torch.empty(nb, dtype=torch.uint8, device=obs.device)
+    a = _native.ActArgs(obs=obs.data_ptr(), mask=mask.data_ptr(), action=act.data_ptr(), logprob=lp.data_ptr(),
+                        entropy=ent.data_ptr(), value=None, logits=lg.data_ptr(), seed=41, ply=3, ply_base=None,
+                        table0=0, mode=_native.ACT_SAMPLE, image=_native.PREC_FP32 << 1)
+    _native.check(pool.lib, pool.lib.spl_policy_act_grouped(pool.images.data_ptr(), pool.image_bytes, pool.n_images,
+                                                            g.data_ptr(), scratch.data_ptr(), n, ctypes.byref(a),
+                                                            ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    for i, m in enumerate(ms):
+        f = FusedActorCritic(m, with_critic=False)
+        wa, wl, we, _, wlg = f.act(obs, mask, seed=41, ply=3, want_logits=True)
+        sel = g == i
+        assert torch.equal(lg[sel], wlg[sel]), i
+        assert torch.equal(act[sel], wa[sel]) and torch.equal(lp[sel], wl[sel]) and torch.equal(ent[sel], we[sel]), i
+
+
 def test_draw_matches_host_and_statistics():
     import torch
     from splendor_gym.fused_policy import OpponentPool

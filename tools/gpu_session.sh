@@ -50,6 +50,10 @@ for step in "$@"; do
     selfplay) run sp_pool 300 python tools/bench_selfplay.py
               run sp_frozen 300 python tools/bench_selfplay.py --opponent frozen ;;
     bench) run bench_default 600 python3 bench.py ;;
+    stepmode) run bench_step 300 python3 bench.py --mode step --only --no-cpu-baseline --sp-tables 0
+              run prof_step 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_step_$TAG -o run -- \
+                  python3 bench.py --mode step --only --no-cpu-baseline --sp-tables 0
+              cp $O/prof_step_$TAG/run_kernel_stats.csv $O/kernel_stats_step_$TAG.csv; head -4 $O/kernel_stats_step_$TAG.csv | cut -c1-160 ;;
     rank2)  # the driver's N>1 launch rehearsed with 2 ranks on this one card (collectives over gloo)
       export SPLENDOR_DIST_BACKEND=gloo
       run bench_2rank 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
