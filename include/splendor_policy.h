@@ -81,8 +81,10 @@ int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const sp
  * current policy or one frozen snapshot): `images` holds n_images actor-only fp32 images, image i at
  * images + i * image_bytes; table t is evaluated with image group_of[t] (device [n]; tables with an
  * index outside 0..n_images-1 get no action).  Tables are counting-sorted by image into `scratch`
- * (spl_policy_group_scratch_bytes(n, n_images) bytes, caller-owned device memory) and every
- * workgroup evaluates 128 tables of one image; results equal spl_policy_act on each image. */
+ * (spl_policy_group_scratch_bytes(n, n_images) bytes, caller-owned device memory, ZERO-FILLED before
+ * its first use: the call leaves its counters zeroed for the next one); every image's full 128-table
+ * workgroups and then its tail in 16-table workgroups (hidden units split over the waves) are
+ * evaluated; results equal spl_policy_act on each image. */
 int64_t spl_policy_group_scratch_bytes(int32_t n, int32_t n_images);
 int spl_policy_act_grouped(const void *images, int64_t image_bytes, int32_t n_images, const int32_t *group_of,
                            void *scratch, int32_t n, const spl_act_args_t *args, void *stream);

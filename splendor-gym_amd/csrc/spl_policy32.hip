@@ -419,14 +419,15 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
 // workgroup of every network (the group's tail) used to spill into a third round that took a whole
 // round's time (each wave's MFMA chain is latency-bound, however few tables it carries).  A group's
 // full 128-table workgroups stay in k_act32; its tail runs here in wave-tiles of 16 tables, ONE
-// wave-tile per workgroup, the 16 output tiles of each hidden layer split over the 8 waves (wave w:
-// tiles w and w + 8), the weights read straight from the image (L2-resident, shared by every
+// wave-tile per 16-wave workgroup, the 16 output tiles of each hidden layer split over the waves
+// (wave w: tile w), the weights read straight from the image (L2-resident, shared by every
 // workgroup of the network) with a deeper software prefetch than the LDS ring needs, and each
-// layer's outputs exchanged through LDS.  A tail wave-tile takes ~1/8 of a full workgroup's time.
+// layer's outputs exchanged through LDS.  A tail wave-tile takes a small fraction of a full
+// workgroup's time (3 tile chains instead of 35).
 template <int KS, int NB>
 __device__ __forceinline__ f32x4 tile_mma_global(const uint8_t *chunk, const float (&B)[NB], int lane) {
     static_assert(KS <= NB && KS % 4 == 0, "B fragments");
-    constexpr int NG = KS / 4, D = 6, NR = D + 1;  // A fragments 6 groups (24 MFMAs) ahead: an L2 round trip
+    constexpr int NG = KS / 4, D = 10, NR = D + 1;  // A fragments 10 groups (40 MFMAs) ahead: an L2 round trip
     const float *bias = reinterpret_cast<const float *>(chunk + kBiasOff) + 4 * (lane >> 4);
     f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
     const f32x4 *A = reinterpret_cast<const f32x4 *>(chunk) + lane;
@@ -442,14 +443,15 @@ __device__ __forceinline__ f32x4 tile_mma_global(const uint8_t *chunk, const flo
     return acc;
 }
 
-// one hidden layer split over the 8 waves: tiles wave and wave + 8, then every wave gathers all
-// 16 tiles' tanh outputs (its next layer's B fragments) from LDS
+constexpr int kNarrowWaves = kTiles;  // one hidden-layer tile per wave
+
+// one hidden layer split over the waves (wave w: tile w), then every wave gathers all 16 tiles'
+// tanh outputs (its next layer's B fragments) from LDS
 template <int KS, int NB>
 __device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const float (&B)[NB], float (&H)[kKs2],
                                              float *xbuf, int wave, int lane) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int t = wave + 8 * h;
+    {
+        const int t = wave;
         const f32x4 acc = tile_mma_global<KS>(W + (size_t)(chunk0 + t) * kChunk, B, lane);
 #pragma unroll
         for (int i = 0; i < 4; ++i) xbuf[(4 * t + i) * 64 + lane] = tanh_f32(acc[i]);
@@ -461,7 +463,7 @@ __device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const
 }
 
 template <bool kSample>
-__global__ __launch_bounds__(512) void k_act32_narrow(const uint8_t *__restrict__ Wbase, ActArgs a) {
+__global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_t *__restrict__ Wbase, ActArgs a) {
     __shared__ __attribute__((aligned(16))) float xbuf[kTiles * 4 * 64];  // 16 KB: one layer's outputs
     __shared__ float lg[kRowsPerWave * kLogitRow];
     __shared__ uint8_t ms[kMaskWave];
@@ -563,9 +565,11 @@ __global__ __launch_bounds__(64) void k_group_scan(int G, int32_t *counts, int32
         ntab[g] = nw;
         gtab[G + 1 + g] = pos;
         cursor[g] = pos;
-        wg += counts[g] / kRowsPerBlock;
-        nw += (counts[g] % kRowsPerBlock + kRowsPerWave - 1) / kRowsPerWave;
-        pos += counts[g];
+        const int c = counts[g];
+        counts[g] = 0;  // ready for the next call's k_group_count (no memset launch)
+        wg += c / kRowsPerBlock;
+        nw += (c % kRowsPerBlock + kRowsPerWave - 1) / kRowsPerWave;
+        pos += c;
     }
     gtab[G] = wg;
     ntab[G] = nw;
@@ -611,8 +615,6 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
         int32_t *counts = static_cast<int32_t *>(scratch), *cursor = counts + groups, *gtab = cursor + groups;
         int32_t *order = gtab + 2 * groups + 2 + groups + 1;
         const hipStream_t s = (hipStream_t)stream;
-        if (hipMemsetAsync(counts, 0, sizeof(int32_t) * groups, s) != hipSuccess)
-            return spl_fail(SPL_E_HIP, "group scratch clear");
         const dim3 g256((unsigned)((n + 255) / 256));
         hipLaunchKernelGGL(k_group_count, g256, dim3(256), 0, s, n, groups, group_of, counts);
         hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(64), 0, s, groups, counts, cursor, gtab);
@@ -635,11 +637,11 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
     else
         hipLaunchKernelGGL((k_act32<false, false>), grid, block, 0, s, W, a);
     if (groups > 0) {  // the groups' tails: at most 8 wave-tiles of 16 tables per group
-        const dim3 ngrid((unsigned)(groups * (kRowsPerBlock / kRowsPerWave)));
+        const dim3 ngrid((unsigned)(groups * (kRowsPerBlock / kRowsPerWave))), nblock(kNarrowWaves * 64);
         if (sample)
-            hipLaunchKernelGGL((k_act32_narrow<true>), ngrid, block, 0, s, W, a);
+            hipLaunchKernelGGL((k_act32_narrow<true>), ngrid, nblock, 0, s, W, a);
         else
-            hipLaunchKernelGGL((k_act32_narrow<false>), ngrid, block, 0, s, W, a);
+            hipLaunchKernelGGL((k_act32_narrow<false>), ngrid, nblock, 0, s, W, a);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return spl_fail(SPL_E_HIP, std::string("k_act32 launch: ") + hipGetErrorString(e));

@@ -254,8 +254,8 @@ class OpponentPool:
         if obs.dtype != t.int32 or not obs.is_contiguous() or mask.dtype != t.int8 or not mask.is_contiguous():
             raise ValueError("obs int32 [n, 297] and mask int8 [n, 45], contiguous")
         nbytes = int(self.lib.spl_policy_group_scratch_bytes(n, self.n_images))
-        if self._scratch is None or self._scratch.numel() < nbytes:
-            self._scratch = t.empty(nbytes, dtype=t.uint8, device=self.device)
+        if self._scratch is None or self._scratch.numel() < nbytes:  # zero-filled once (spl_policy_act_grouped)
+            self._scratch = t.zeros(nbytes, dtype=t.uint8, device=self.device)
         action = out if out is not None else t.empty(n, dtype=t.int32, device=self.device)
         a = ActArgs(obs=obs.data_ptr(), mask=mask.data_ptr(), action=action.data_ptr(), logprob=None, entropy=None,
                     value=None, logits=None, seed=0, ply=0, ply_base=None, table0=0, mode=ACT_GREEDY,

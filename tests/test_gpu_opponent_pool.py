@@ -96,7 +96,7 @@ def test_grouped_sampling_and_logits_equal_each_network(n):
     ent = torch.empty(n, dtype=torch.float32, device=obs.device)
     lg = torch.empty(n, 45, dtype=torch.float32, device=obs.device)
     nb = int(pool.lib.spl_policy_group_scratch_bytes(n, pool.n_images))
-    scratch = torch.empty(nb, dtype=torch.uint8, device=obs.device)
+    scratch = torch.zeros(nb, dtype=torch.uint8, device=obs.device)
     a = _native.ActArgs(obs=obs.data_ptr(), mask=mask.data_ptr(), action=act.data_ptr(), logprob=lp.data_ptr(),
                         entropy=ent.data_ptr(), value=None, logits=lg.data_ptr(), seed=41, ply=3, ply_base=None,
                         table0=0, mode=_native.ACT_SAMPLE, image=_native.PREC_FP32 << 1)
