@@ -419,39 +419,40 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
 // workgroup of every network (the group's tail) used to spill into a third round that took a whole
 // round's time (each wave's MFMA chain is latency-bound, however few tables it carries).  A group's
 // full 128-table workgroups stay in k_act32; its tail runs here in wave-tiles of 16 tables, ONE
-// wave-tile per 16-wave workgroup, the 16 output tiles of each hidden layer split over the waves
-// (wave w: tile w), the weights read straight from the image (L2-resident, shared by every
-// workgroup of the network) with a deeper software prefetch than the LDS ring needs, and each
+// wave-tile per 8-wave workgroup, the 16 output tiles of each hidden layer split over the waves
+// (wave w: tiles w, w + 8), the weights read straight from the image (L2-resident, shared by every
+// workgroup of the network), a whole tile's A fragments in flight at once, and each
 // layer's outputs exchanged through LDS.  A tail wave-tile takes a small fraction of a full
-// workgroup's time (3 tile chains instead of 35).
+// workgroup's time (5 tile chains per wave instead of 35).
 template <int KS, int NB>
 __device__ __forceinline__ f32x4 tile_mma_global(const uint8_t *chunk, const float (&B)[NB], int lane) {
     static_assert(KS <= NB && KS % 4 == 0, "B fragments");
-    constexpr int NG = KS / 4, D = 10, NR = D + 1;  // A fragments 10 groups (40 MFMAs) ahead: an L2 round trip
+    // the whole tile's A fragments in flight at once (one L2 round trip per tile, not one per group:
+    // 19 x 16 B per lane in layer 1), then the MFMA chain
+    constexpr int NG = KS / 4;
     const float *bias = reinterpret_cast<const float *>(chunk + kBiasOff) + 4 * (lane >> 4);
-    f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
     const f32x4 *A = reinterpret_cast<const f32x4 *>(chunk) + lane;
-    f32x4 af[NR];
+    f32x4 af[NG];
 #pragma unroll
-    for (int q = 0; q < D; ++q) af[q] = A[q * 64];
+    for (int q = 0; q < NG; ++q) af[q] = A[q * 64];
+    f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
 #pragma unroll
-    for (int q = 0; q < NG; ++q) {
-        if (q + D < NG) af[(q + D) % NR] = A[(q + D) * 64];
+    for (int q = 0; q < NG; ++q)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[q % NR][j], B[4 * q + j], acc, 0, 0, 0);
-    }
+        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[q][j], B[4 * q + j], acc, 0, 0, 0);
     return acc;
 }
 
-constexpr int kNarrowWaves = kTiles;  // one hidden-layer tile per wave
+constexpr int kNarrowWaves = 8;  // two hidden-layer tiles per wave (2 waves per SIMD: room for the A fragments)
 
-// one hidden layer split over the waves (wave w: tile w), then every wave gathers all 16 tiles'
-// tanh outputs (its next layer's B fragments) from LDS
+// one hidden layer split over the waves (wave w: tiles w and w + 8), then every wave gathers all
+// 16 tiles' tanh outputs (its next layer's B fragments) from LDS
 template <int KS, int NB>
 __device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const float (&B)[NB], float (&H)[kKs2],
                                              float *xbuf, int wave, int lane) {
-    {
-        const int t = wave;
+#pragma unroll
+    for (int h = 0; h < kTiles / kNarrowWaves; ++h) {
+        const int t = wave + kNarrowWaves * h;
         const f32x4 acc = tile_mma_global<KS>(W + (size_t)(chunk0 + t) * kChunk, B, lane);
 #pragma unroll
         for (int i = 0; i < 4; ++i) xbuf[(4 * t + i) * 64 + lane] = tanh_f32(acc[i]);
