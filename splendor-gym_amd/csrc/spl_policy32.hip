@@ -598,31 +598,6 @@ __global__ __launch_bounds__(256) void k_group_scatter(int n, int G, const int32
 
 constexpr int kMaxGroups = 64;
 
-// The grouped evaluation's side stream (per device, created on first use, highest priority so the
-// tails' few workgroups are dispatched as soon as CUs free up) and its fork / join events.
-static int side_stream(hipStream_t *side, hipEvent_t *fork, hipEvent_t *join) {
-    struct Side {
-        hipStream_t s = nullptr;
-        hipEvent_t f = nullptr, j = nullptr;
-    };
-    static Side per_dev[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return spl_fail(SPL_E_HIP, "grouped act: device");
-    Side &d = per_dev[dev];
-    if (!d.s) {
-        int lo = 0, hi = 0;
-        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
-        if (hipStreamCreateWithPriority(&d.s, hipStreamNonBlocking, hi) != hipSuccess ||
-            hipEventCreateWithFlags(&d.f, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&d.j, hipEventDisableTiming) != hipSuccess)
-            return spl_fail(SPL_E_HIP, "grouped act: side stream");
-    }
-    *side = d.s;
-    *fork = d.f;
-    *join = d.j;
-    return SPL_OK;
-}
-
 int64_t splp32_group_scratch(int32_t n, int32_t groups) { return 4 * ((int64_t)5 * groups + 3 + n); }
 
 // image: a packed fp32 image (full when has_critic); critic: evaluate the critic (SAMPLE with value)
@@ -654,22 +629,6 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
     const hipStream_t s = (hipStream_t)stream;
     const uint8_t *W = img;
     if (has_critic && !critic) W += (size_t)kCriticChunks * kChunk;  // the actor part of a full image
-    // grouped: the tails' narrow workgroups run on a side stream beside the full workgroups (forked
-    // after the sort, joined before the caller's next work), so they take CUs as the full
-    // workgroups leave them instead of adding their time after the last full round
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-    if (groups > 0) {
-        if (int r = side_stream(&side, &fork, &join)) return r;
-        if (hipEventRecord(fork, s) != hipSuccess || hipStreamWaitEvent(side, fork, 0) != hipSuccess)
-            return spl_fail(SPL_E_HIP, "grouped act: fork of the tail stream");
-        const dim3 ngrid((unsigned)(groups * (kRowsPerBlock / kRowsPerWave))), nblock(kNarrowWaves * 64);
-        if (sample)
-            hipLaunchKernelGGL((k_act32_narrow<true>), ngrid, nblock, 0, side, W, a);
-        else
-            hipLaunchKernelGGL((k_act32_narrow<false>), ngrid, nblock, 0, side, W, a);
-        if (hipEventRecord(join, side) != hipSuccess) return spl_fail(SPL_E_HIP, "grouped act: tail stream join");
-    }
     if (critic && sample)
         hipLaunchKernelGGL((k_act32<true, true>), grid, block, 0, s, W, a);
     else if (critic)  // get_value
@@ -678,8 +637,13 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
         hipLaunchKernelGGL((k_act32<false, true>), grid, block, 0, s, W, a);
     else
         hipLaunchKernelGGL((k_act32<false, false>), grid, block, 0, s, W, a);
-    if (groups > 0 && hipStreamWaitEvent(s, join, 0) != hipSuccess)
-        return spl_fail(SPL_E_HIP, "grouped act: tail stream join");
+    if (groups > 0) {  // the groups' tails: at most 8 wave-tiles of 16 tables per group
+        const dim3 ngrid((unsigned)(groups * (kRowsPerBlock / kRowsPerWave))), nblock(kNarrowWaves * 64);
+        if (sample)
+            hipLaunchKernelGGL((k_act32_narrow<true>), ngrid, nblock, 0, s, W, a);
+        else
+            hipLaunchKernelGGL((k_act32_narrow<false>), ngrid, nblock, 0, s, W, a);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return spl_fail(SPL_E_HIP, std::string("k_act32 launch: ") + hipGetErrorString(e));
     return SPL_OK;
