@@ -928,6 +928,24 @@ __device__ __forceinline__ void encode_row(const Tab<P> &T, uint8_t *rows_base, 
     if (o0 == 0u) dst[74] = R[74];
 }
 
+// Half of encode_row: staged dwords [0, kRowHalf) (Half 0) or [kRowHalf, 75) (Half 1) of every
+// lane's row, so two waves of a workgroup encode one block in parallel.  build_row is inlined
+// with constant indices, so each half computes only the row bytes its dwords take.
+constexpr int kRowHalf = 37;
+template <int Half, int P>
+__device__ __forceinline__ void encode_row_half(const Tab<P> &T, uint8_t *rows_base, const Consts &L) {
+    uint32_t R[76];
+    build_row(T, L, R);
+    if (Half == 1) R[74] |= (uint32_t)__shfl_down((int)R[0], 1) << 8;
+    const int lane = lane_id();
+    const uint32_t o0 = (4u - ((uint32_t)lane & 3u)) & 3u;
+    uint32_t *dst = reinterpret_cast<uint32_t *>(rows_base + kObsDim * lane + o0);
+    constexpr int j0 = Half == 0 ? 0 : kRowHalf, j1 = Half == 0 ? kRowHalf : 74;
+#pragma unroll
+    for (int j = j0; j < j1; ++j) dst[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], o0);
+    if (Half == 1 && o0 == 0u) dst[74] = R[74];
+}
+
 // Observation of table T written by its own lane straight to dst[0..296] (int32; 297 dword
 // stores): the rare path for terminal rows that do not fit the pipelined kernel's hand-off.
 template <int P>
@@ -1970,6 +1988,11 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         for (int w = 0; w < kW; ++w) L.st[w][lane] = tab_word(T, w);
         STAMP(3);
         ws_sync();  // hand-off 1: state words (deal scratch in `rows` free again)
+        // Without terminal rows left to the output wave (the usual case) this wave encodes the first
+        // half of every row while the output wave encodes the second (encode 2.7 -> ~1.4 us before
+        // the obs stores start); otherwise the output wave encodes whole rows after its terminal ones.
+        if (fin == 0ull) encode_row_half<0>(T, L.rows, L);
+        ws_sync();  // hand-off 2: first row halves staged
         STAMP(4);
         if (fin_rules) {  // info["final_observation"] rows, compacted in trow, stored row by row
             Tab<P> F;
@@ -2030,6 +2053,9 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
 #pragma unroll
         for (int w = 0; w < kW; ++w) set_tab_word(T, w, L.st[w][lane]);
         const uint64_t fin = L.fin;
+        if (fin == 0ull) encode_row_half<1>(T, L.rows, L);
+        ws_sync();  // hand-off 2
+        STAMP(4);
         if (fin) {  // terminal rows (info["final_observation"]) first, through the same staging rows
             const bool mine = (fin >> lane) & 1ull;
             Tab<P> F = T;
@@ -2045,10 +2071,9 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
                 if (mine && get_moves(F.sw) > 255) S.final_obs[(size_t)t * kObsDim + 295] = get_moves(F.sw);
             }
             wave_lds_sync();  // the terminal rows' LDS reads are done
+            encode_row(T, L.rows, L);
+            wave_lds_sync();
         }
-        STAMP(4);
-        encode_row(T, L.rows, L);
-        wave_lds_sync();
         STAMP(5);
         store_obs_block<64, SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
         STAMP(6);

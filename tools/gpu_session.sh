@@ -2,7 +2,7 @@
 # One GPU session (round 3).  Steps by name, run in order; each GPU step has its own time limit and
 # the chain stops at the first failure.
 #   tools/gpu_session.sh TAG step [step ...]
-# steps: tests smoke driver prof deleg profc4 pmcc4 multi pmc2p pmcmulti selfplay vec policy
+# steps: tests smoke driver prof deleg profc4 pmcc4 multi pmc2p pmcmulti pmcstep stamps selfplay vec policy stepmode
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -47,6 +47,8 @@ for step in "$@"; do
     pmcmulti) bash tools/pmc.sh ${TAG}_3p 3 65536 store traffic || exit 1
               bash tools/pmc.sh ${TAG}_4p 4 65536 store traffic || exit 1
               bash tools/pmc.sh ${TAG}_4p_32768 4 32768 store all || exit 1 ;;
+    pmcstep) bash tools/pmc.sh ${TAG}_2p_step 2 65536 step all || exit 1 ;;
+    stamps) run stamps 300 python3 tools/stamps.py --run ;;
     selfplay) run sp_pool 300 python tools/bench_selfplay.py
               run sp_frozen 300 python tools/bench_selfplay.py --opponent frozen ;;
     bench) run bench_default 600 python3 bench.py ;;

@@ -15,9 +15,9 @@ LIB = os.environ.get("STAMP_LIB", os.path.join(REPO, "splendor-gym_amd", "ablate
 NAMES = ["start", "loaded+prefetched", "pre-apply", "applied", "step logic", "final obs", "reset done",
          "encoded", "barrier", "obs stored", "mask+final stored", "end"]
 # k_step_ws (the default spl_step kernel): stamps per wave, wave 0 = rules, wave 1 = output
-WS_RULES = ["start", "past hand-off 0", "rules done", "state to LDS (reset done)", "past hand-off 1", "legal mask",
+WS_RULES = ["start", "past hand-off 0", "rules done", "state to LDS (reset done)", "past hand-off 2 (row halves)", "legal mask",
             "end (mask, small outputs, state stored)"]
-WS_OUT = ["start", "tables staged", "past hand-off 0", "past hand-off 1", "final rows done", "encoded",
+WS_OUT = ["start", "tables staged", "past hand-off 0", "past hand-off 1", "past hand-off 2 (rows encoded)", "final rows done",
           "obs stores issued", "end", "early board stores issued"]
 
 CHILD = r'''
@@ -84,7 +84,7 @@ def main():
             print(f"{i:2d} {nm:26s} {np.median(col):10.2f} {np.percentile(col, 90):8.2f} {col.max():8.2f}")
     if ws:  # per XCC (workgroup i runs on XCC i % 8): the rules wave's hand-off 1 and the output wave's end
         wg = np.arange(a.shape[1] // 2) % 8
-        for title, idx, ph in (("rules: past hand-off 1", 0, 4), ("output: end", 1, len(WS_OUT) - 1)):
+        for title, idx, ph in (("rules: past hand-off 1", 0, 4), ("output: end", 1, WS_OUT.index("end"))):
             v = a[:, idx::2, ph]
             print(f"{title} by XCC median/p99: " + " | ".join(
                 f"{np.nanmedian(v[:, wg == x]):.1f}/{np.nanpercentile(v[:, wg == x], 99):.1f}" for x in range(8)))
