@@ -2,7 +2,8 @@
 # One GPU session (round 3).  Steps by name, run in order; each GPU step has its own time limit and
 # the chain stops at the first failure.
 #   tools/gpu_session.sh TAG step [step ...]
-# steps: tests smoke driver prof deleg profc4 pmcc4 multi pmc2p pmcmulti pmcstep stamps selfplay vec policy stepmode
+# steps: tests steptests smoke driver prof deleg profc4 pmcc4 multi pmc2p pmcmulti pmcstep stamps selfplay spprof
+#        poolsize vec policy stepmode rank2 bench
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -47,6 +48,10 @@ for step in "$@"; do
     pmcmulti) bash tools/pmc.sh ${TAG}_3p 3 65536 store traffic || exit 1
               bash tools/pmc.sh ${TAG}_4p 4 65536 store traffic || exit 1
               bash tools/pmc.sh ${TAG}_4p_32768 4 32768 store all || exit 1 ;;
+    steptests) run pytest_step 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_env_api.py \
+                   tests/test_gpu_opponent_pool.py -x -v --timeout 200 --timeout-method thread ;;
+    spprof) bash tools/gpu_sp_prof.sh || exit 1 ;;
+    poolsize) for ps in 0 1 3 6 12; do run sps_$ps 200 python3 tools/bench_selfplay.py --opponent pool --pool-size $ps; done ;;
     pmcstep) bash tools/pmc.sh ${TAG}_2p_step 2 65536 step all || exit 1 ;;
     stamps) run stamps 300 python3 tools/stamps.py --run ;;
     selfplay) run sp_pool 300 python tools/bench_selfplay.py
