@@ -233,7 +233,7 @@ def selfplay_line(dev, rank, world, N, iters, warmup):
     return {"metric": f"env-steps/sec (whole node), 2p self-play, on-device fp32 ActorCritic, {N} tables/GPU",
             "value": round(2 * N * world * iters / el, 1), "unit": "env-steps/s",
             "ms_per_dual_step": round(el / iters * 1e3, 4), "iters": iters, "dtype": "fp32",
-            "config": {"workload": "BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused fp32 MFMA) + "
+            "config": {"workload": "BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused, fp32-accurate split-bf16 MFMA) + "
                                    "DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of 12 frozen "
                                    "snapshots per episode, greedy), reset after done; hipGraph replays",
                        "tables_per_gpu": N, "weights": "reference checkpoint runs/ppo_splendor/ppo_splendor_latest.pt"}}

@@ -9,8 +9,9 @@
  * for opponents.  These entry points evaluate that network for a whole batch of tables in one
  * launch: observations (int32 [n][297]) and masks (int8 [n][45]) straight from the engine, tanh /
  * softmax / sampling fused.  Two precisions:
- *   SPL_PREC_FP32 (default)  the reference's fp32: exact fp32 products and accumulation on
- *                            v_mfma_f32_16x16x4_f32 (spl_policy32.hip), tanhf
+ *   SPL_PREC_FP32 (default)  the reference's fp32: fp32-accurate products (three bf16 planes per
+ *                            operand, six plane products accumulated in fp32 on
+ *                            v_mfma_f32_16x16x32_bf16; spl_policy32.hip), fp32 tanh
  *   SPL_PREC_BF16 (opt-in)   bf16 MFMA (v_mfma_f32_32x32x16_bf16) with fp32 accumulation (spl_policy.hip)
  *
  *   spl_policy_bytes   size of a packed weight image (actor only, or actor + critic; per precision)

@@ -1,22 +1,31 @@
-// spl_policy32.hip — the fused ActorCritic forward at fp32 (the reference's precision) on MI355X.
+// spl_policy32.hip — the fused ActorCritic forward at fp32 accuracy (the reference's precision) on MI355X.
 //
 // Same network and epilogue as spl_policy.hip's bf16 kernel (ppo_splendor.py:27-59: actor and
 // critic Linear(297,256)-Tanh-Linear(256,256)-Tanh-Linear(256,{45|1}); masked_categorical sample,
-// log_prob, entropy, critic value; or the greedy masked argmax of training_utils.py:263-276), but
-// every product is an exact fp32 FMA: v_mfma_f32_16x16x4_f32 (fp32 in, fp32 accumulate — the chip's
-// fp32 matrix peak, bitwise an fmaf chain), tanh to a few ulp (tanh_f32).  Logits and
-// values therefore agree with torch's fp32 nn.Linear stack to summation-order rounding.
-//
-//   * a wave = 16 tables = the 16 columns of every 16x16x4 tile; a workgroup = 8 waves = 128 tables
+// log_prob, entropy, critic value; or the greedy masked argmax of training_utils.py:263-276), with
+// fp32-accurate products on the bf16 matrix cores (gfx950 has no xf32 MFMA, and its fp32 MFMA runs
+// at 1/16 of the bf16 rate):
+//   * every fp32 operand x is split into three bf16 planes x = x0 + x1 + x2 (x0 = bf16(x),
+//     x1 = bf16(x - x0), x2 = bf16(x - x0 - x1): 3 x 8 significand bits, so x is represented to
+//     ~2^-25 relative; each residual is exact in fp32).  A weight-times-activation product is the
+//     six plane products of order <= 2, a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0, accumulated in
+//     fp32 by v_mfma_f32_16x16x32_bf16 (bf16 x bf16 products are exact in fp32); the three dropped
+//     terms are <= 3 x 2^-24 of |ab|, the size of an fp32 rounding.  Layer 1's operand is the
+//     observation, small integers exact in bf16: three products (a0 b + a1 b + a2 b).
+//     Smallest terms first into the accumulator.  6 (3) bf16 MFMAs per 32 inputs against 8 fp32
+//     v_mfma_f32_16x16x4_f32 of twice the cycles each: ~2.7x (5.3x) fewer matrix cycles.
+//   * a wave = 16 tables = the 16 columns of every 16x16x32 tile; a workgroup = 8 waves = 128 tables
 //     (two waves per SIMD).  Activations are TRANSPOSED (hidden unit on the accumulator row, table
-//     on the lane): accumulator register i of lane group g holds unit 16t + 4g + i of tile t, which
-//     is exactly lane group g's B operand of k-step 4t + i of the next layer — no LDS round trip
-//     between layers (the packed weights carry the matching input-unit order).
-//   * the observation (int32 -> fp32, exact) loads into registers as the 76 layer-1 B fragments
-//     and stays there through both networks' layer 1; hidden layers hold 64 fp32 per lane.
-//   * weights stream once per workgroup through the same 6-slot LDS ring as the bf16 kernel
-//     (20-KB chunks = one 16-row output tile of one layer, [k-step/4][lane][4 fp32] + bias,
-//     global_load_lds, 5 chunks in flight), shared by the 8 waves.
+//     on the lane): accumulator register i of lane group g holds unit 16t + 4g + i of tile t, and
+//     tiles 2s, 2s+1 are lane group g's B elements of k-step s of the next layer (element e = unit
+//     16(2s + e/4) + 4g + e%4) — no LDS round trip between layers; the packed weights carry the
+//     matching input-unit order.  tanh runs in fp32 (tanh_f32) before the split.
+//   * the observation (int32 -> bf16, exact) loads into registers as the 10 layer-1 B fragments
+//     and stays there through both networks' layer 1; a hidden layer's output is 3 planes x 8
+//     k-steps x 8 bf16 per lane.
+//   * weights stream once per workgroup through a 4-slot LDS ring (31-KB chunks = one 16-row
+//     output tile of one layer, [k-step][plane][lane][8 bf16] + bias, global_load_lds, 3 chunks in
+//     flight), shared by the 8 waves.
 //   * the critic's one-unit output layer is a per-lane fp32 FMA chain over its layer-2 tiles.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -45,27 +54,32 @@ namespace splp32 {
 
 using spl::philox4x32;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kObs = 297, kAct = 45, kHid = 256;
-constexpr int kKs1 = 76;  // layer-1 k-steps of 4: 297 inputs padded to 304
-constexpr int kKs2 = 64;  // layers 2 and 3: 256 inputs
-constexpr int kChunk = 20480;
-constexpr int kBiasOff = kKs1 * 256;  // 19 456: after the largest weight block
-constexpr int kTiles = kHid / 16;     // 16 output tiles of 16 rows per hidden layer
-constexpr int kActTiles = 3;          // 48 rows >= 45 logits
+constexpr int kKs1 = 10;    // layer-1 k-steps of 32: 297 inputs padded to 320
+constexpr int kKs2 = 8;     // layers 2 and 3: 256 inputs
+constexpr int kPlanes = 3;  // bf16 planes of a split fp32 operand
+constexpr int kFrag = 1024;                       // one plane of one k-step: [lane][8 bf16]
+constexpr int kBiasOff = kKs1 * kPlanes * kFrag;  // 30 720: after the largest weight block
+constexpr int kChunk = 31 * 1024;                 // + the tile's 16 fp32 biases, in 1-KB blocks
+constexpr int kTiles = kHid / 16;                 // 16 output tiles of 16 rows per hidden layer
+constexpr int kActTiles = 3;                      // 48 rows >= 45 logits
 constexpr int kActorChunks = 2 * kTiles + kActTiles, kCriticChunks = 2 * kTiles;  // 35, 32
 constexpr int kAllChunks = kActorChunks + kCriticChunks;                          // 67
 constexpr int kCriticTail = 272 * 4;  // fp32 critic output layer: w3 [256], b3, padding
 
 constexpr int kWaves = 8, kRowsPerWave = 16, kRowsPerBlock = kWaves * kRowsPerWave;  // 128 tables
-constexpr int kSlots = 6;
+constexpr int kSlots = 4;
 constexpr int kMaskWave = kRowsPerWave * kAct;  // 720 B
 constexpr int kLogitRow = 49;                   // floats per staged logit row (odd: conflict-free)
 constexpr int kLdsMask = kSlots * kChunk;
-constexpr int kLds = kLdsMask + kWaves * kMaskWave;  // 128 640 B
+constexpr int kLds = kLdsMask + kWaves * kMaskWave;  // 132 736 B
 static_assert(kWaves * kRowsPerWave * kLogitRow * 4 <= kLdsMask, "logits reuse the weight ring");
 static_assert(kLds <= 160 * 1024, "LDS");
-static_assert(kKs1 % 4 == 0 && kKs2 % 4 == 0, "k-steps in groups of four");
+static_assert(kBiasOff + 64 <= kChunk, "bias");
 
 // chunk order of an image (the order a forward pass consumes them): with a critic
 // [critic L1 x16][critic L2 x16], then [actor L1 x16][actor L2 x16][actor L3 x3]; the actor part of
@@ -76,13 +90,22 @@ struct PackNet {
     int out;
 };
 
-// input unit fed by lane group g at k-step s: natural order in layer 1 (the observation), the
-// accumulator order of the previous layer's tiles in layers 2-3 (k-step 4t + i <- tile t, reg i)
-__device__ __forceinline__ int unit_of(int layer, int s, int g) {
-    return layer == 1 ? 4 * s + g : 16 * (s >> 2) + 4 * g + (s & 3);
+// input unit of lane group g, element e at k-step s: natural order in layer 1 (the observation),
+// the accumulator order of the previous layer's tiles in layers 2-3 (tile 2s + e/4, register e%4)
+__device__ __forceinline__ int unit_of(int layer, int s, int g, int e) {
+    return layer == 1 ? 32 * s + 8 * g + e : 16 * (2 * s + (e >> 2)) + 4 * g + (e & 3);
 }
 
-// one block per physical chunk
+// x = x0 + x1 + x2 in bf16 (round to nearest even; x - x0 and x - x0 - x1 are exact in fp32)
+__device__ __forceinline__ void split3(float x, __bf16 &x0, __bf16 &x1, __bf16 &x2) {
+    x0 = (__bf16)x;
+    const float r = x - (float)x0;
+    x1 = (__bf16)r;
+    x2 = (__bf16)(r - (float)x1);
+}
+
+// one block per physical chunk: [k-step s][plane p][lane][8 bf16], lane l = (g = l >> 4, r = l & 15)
+// holds W[row 16*tile + r][unit_of(layer, s, g, e)] split into planes 0..2; then 16 fp32 biases
 __global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, int with_critic, uint8_t *dst) {
     const int ch = blockIdx.x;
     const int net = with_critic && ch < kCriticChunks ? 1 : 0;  // 0 actor, 1 critic
@@ -94,18 +117,28 @@ __global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, i
     const float *B = layer == 1 ? P.b1 : layer == 2 ? P.b2 : P.b3;
     const int in = layer == 1 ? kObs : kHid, rows = layer == 3 ? P.out : kHid;
     const int ks = layer == 1 ? kKs1 : kKs2;
-    float *out = reinterpret_cast<float *>(dst + (size_t)ch * kChunk);
-    // [k-step group q][lane][4]: lane l = (g = l >> 4, r = l & 15) holds W[row 16*tile + r][unit(4q + j, g)]
-    for (int v = threadIdx.x; v < (ks / 4) * 64 * 4; v += blockDim.x) {
-        const int j = v & 3, lane = (v >> 2) & 63, q = v >> 8;
-        const int r = lane & 15, g = lane >> 4, row = 16 * tile + r, k = unit_of(layer, 4 * q + j, g);
-        out[v] = (row < rows && k < in) ? W[(size_t)row * in + k] : 0.f;
+    uint8_t *out = dst + (size_t)ch * kChunk;
+    __bf16 *o = reinterpret_cast<__bf16 *>(out);
+    for (int v = threadIdx.x; v < ks * 64 * 8; v += blockDim.x) {
+        const int e = v & 7, lane = (v >> 3) & 63, s = v >> 9;
+        const int r = lane & 15, g = lane >> 4, row = 16 * tile + r, k = unit_of(layer, s, g, e);
+        const float w = (row < rows && k < in) ? W[(size_t)row * in + k] : 0.f;
+        __bf16 w0, w1, w2;
+        split3(w, w0, w1, w2);
+        const size_t base = ((size_t)(s * kPlanes) * 64 + lane) * 8 + e;
+        o[base] = w0;
+        o[base + 64 * 8] = w1;
+        o[base + 2 * 64 * 8] = w2;
     }
-    for (int v = (ks / 4) * 256 + threadIdx.x; v < kBiasOff / 4; v += blockDim.x) out[v] = 0.f;
-    if (threadIdx.x < 16) {  // bias in row order
+    for (int v = ks * kPlanes * kFrag + 4 * threadIdx.x; v < kBiasOff; v += 4 * blockDim.x)
+        *reinterpret_cast<uint32_t *>(out + v) = 0u;
+    float *bias = reinterpret_cast<float *>(out + kBiasOff);
+    if (threadIdx.x < 16) {  // bias in row order, then zero padding to the end of the chunk
         const int row = 16 * tile + threadIdx.x;
-        out[kBiasOff / 4 + threadIdx.x] = row < rows ? B[row] : 0.f;
+        bias[threadIdx.x] = row < rows ? B[row] : 0.f;
     }
+    for (int v = kBiasOff + 64 + 4 * threadIdx.x; v < kChunk; v += 4 * blockDim.x)
+        *reinterpret_cast<uint32_t *>(out + v) = 0u;
     if (net == 1 && layer == 2 && tile == 0) {  // the critic's output layer as fp32 (evaluated on VALU)
         float *tail = reinterpret_cast<float *>(dst + (size_t)kAllChunks * kChunk);
         for (int k = threadIdx.x; k < 272; k += blockDim.x) tail[k] = k < kHid ? P.w3[k] : k == kHid ? P.b3[0] : 0.f;
@@ -164,52 +197,119 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int kChunkBlocks = kChunk / 1024;  // 20
+constexpr int kChunkBlocks = kChunk / 1024;  // 31: blocks w, w + 8, w + 16, w + 24 of wave w
+constexpr int kBlocksPerWave = (kChunkBlocks + kWaves - 1) / kWaves;  // 4 (3 for the last wave)
 __device__ __forceinline__ void issue_chunk(const uint8_t *W, int chunk, uint8_t *slot, int wave, int lane) {
     const uint8_t *src = W + (size_t)chunk * kChunk + lane * 16;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < kBlocksPerWave; ++i) {
         const int blk = wave + kWaves * i;
         if (blk < kChunkBlocks)
             __builtin_amdgcn_global_load_lds(src + blk * 1024, (lds_void *)(slot + blk * 1024), 16, 0, 0);
     }
 }
 
-// one 16-row output tile: bias + sum over KS k-steps; B fragments (one fp32 per lane and k-step) in
-// registers, A fragments read from the ring slot four k-steps per 16-byte LDS read, one group ahead
-template <int KS, int NB>
-__device__ __forceinline__ f32x4 tile_mma(const uint8_t *slot, const float (&B)[NB], int lane) {
-    static_assert(KS <= NB && KS % 4 == 0, "B fragments");
-    constexpr int NG = KS / 4;
-    const float *bias = reinterpret_cast<const float *>(slot + kBiasOff) + 4 * (lane >> 4);
+__device__ __forceinline__ f32x4 mma(const bf16x8 &a, const bf16x8 &b, const f32x4 &c) {
+#if SPL_POL_ABL & 8
+    return c + (float)a[0] * (float)b[1];
+#else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+
+// one 16-row output tile: bias + sum over KS k-steps of 32 inputs.  B: NB planes of the layer's
+// input (1: the observation, exact in bf16; 3: a split hidden layer), in registers.  A: the tile's
+// three weight planes per k-step from `src` (the LDS ring slot, or the image in global memory for
+// the narrow kernel), D k-steps ahead of the MFMAs that use them.
+template <int KS, int NB, int D>
+__device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const bf16x8 (&B)[NB][KS], int lane) {
+    static_assert(NB == 1 || NB == 3, "planes");
+    const float *bias = reinterpret_cast<const float *>(src + kBiasOff) + 4 * (lane >> 4);
     f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
-    const f32x4 *A = reinterpret_cast<const f32x4 *>(slot) + lane;
-    // A fragments SPL_AF_AHEAD groups ahead (a group's four MFMAs take ~128 cycles, about one LDS
-    // round trip with eight waves reading the ring)
-    constexpr int D = SPL_AF_AHEAD, NR = D + 1;
-    f32x4 af[NR];
+    const bf16x8 *A = reinterpret_cast<const bf16x8 *>(src) + lane;  // k-step s, plane p at A[(3s + p) * 64]
+    constexpr int NR = D + 1;
+    bf16x8 af[NR][kPlanes];
 #pragma unroll
-    for (int q = 0; q < D; ++q) af[q] = A[q * 64];
+    for (int q = 0; q < D && q < KS; ++q)
 #pragma unroll
-    for (int q = 0; q < NG; ++q) {
-        if (!(SPL_POL_ABL & 4) && q + D < NG) af[(q + D) % NR] = A[(q + D) * 64];
+        for (int p = 0; p < kPlanes; ++p) af[q][p] = A[(kPlanes * q + p) * 64];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[(SPL_POL_ABL & 4) ? q % D : q % NR][j], B[4 * q + j], acc, 0, 0, 0);
-        if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    for (int s = 0; s < KS; ++s) {
+        if (!(SPL_POL_ABL & 4) && s + D < KS) {
+#pragma unroll
+            for (int p = 0; p < kPlanes; ++p) af[(s + D) % NR][p] = A[(kPlanes * (s + D) + p) * 64];
+        }
+        const bf16x8 *a = af[(SPL_POL_ABL & 4) ? s % D : s % NR];
+        if constexpr (NB == 1) {  // exact B: a2 b + a1 b + a0 b
+            acc = mma(a[2], B[0][s], acc);
+            acc = mma(a[1], B[0][s], acc);
+            acc = mma(a[0], B[0][s], acc);
+        } else {  // the six products of order <= 2, smallest first
+            acc = mma(a[2], B[0][s], acc);
+            acc = mma(a[1], B[1][s], acc);
+            acc = mma(a[0], B[2][s], acc);
+            acc = mma(a[1], B[0][s], acc);
+            acc = mma(a[0], B[1][s], acc);
+            acc = mma(a[0], B[0][s], acc);
+        }
+        if (NB == 3 || (s & 1) == 1) __builtin_amdgcn_sched_barrier(0);
     }
     return acc;
 }
 
-// a hidden layer: 16 tiles, each tile's tanh is the next layer's B fragments 4t..4t+3
-template <int KS, int NB, typename Enter>
-__device__ __forceinline__ void layer_tanh(Enter &enter, const float (&B)[NB], float (&H)[kKs2], int lane) {
+// planes of a bf16x8 as dwords: element e in dword e / 2 (even e in the low half)
+__device__ __forceinline__ uint32_t pk2(__bf16 lo, __bf16 hi) {
+    const bf16x2 v = {lo, hi};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+// the four fp32 outputs h[0..3] of tile t (units 16t + 4g + i) -> elements 4(t & 1) .. +3 of
+// k-step t / 2 of the next layer's three B planes
+__device__ __forceinline__ void put_split(bf16x8 (&H)[kPlanes][kKs2], int t, const float (&h)[4]) {
+    __bf16 x[4][kPlanes];
 #pragma unroll
-    for (int t = 0; t < kTiles; ++t) {
-        const f32x4 acc = tile_mma<KS>(enter(), B, lane);
+    for (int i = 0; i < 4; ++i) split3(h[i], x[i][0], x[i][1], x[i][2]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) H[4 * t + i] = tanh_f32(acc[i]);
+    for (int p = 0; p < kPlanes; ++p) {
+        u32x4 w = __builtin_bit_cast(u32x4, H[p][t >> 1]);
+        w[2 * (t & 1)] = pk2(x[0][p], x[1][p]);
+        w[2 * (t & 1) + 1] = pk2(x[2][p], x[3][p]);
+        H[p][t >> 1] = __builtin_bit_cast(bf16x8, w);
     }
 }
+
+// a hidden layer: 16 tiles, each tile's tanh split into the next layer's B planes
+template <int KS, int NB, int D, typename Enter>
+__device__ __forceinline__ void layer_tanh(Enter &enter, const bf16x8 (&B)[NB][KS], bf16x8 (&H)[kPlanes][kKs2],
+                                           int lane) {
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) {
+        const f32x4 acc = tile_mma<KS, NB, D>(enter(), B, lane);
+        float h[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[i] = tanh_f32(acc[i]);
+        put_split(H, t, h);
+    }
+}
+
+// the observation's B fragments: lane (r, g), k-step s, element e = obs[table r][32s + 8g + e]
+// (integers < 256: exact in bf16)
+__device__ __forceinline__ void load_obs(const int32_t *xrow, int g, bf16x8 (&X)[1][kKs1]) {
+#pragma unroll
+    for (int s = 0; s < kKs1; ++s) {
+        int v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = 32 * s + 8 * g + e;
+            v[e] = k < kObs ? xrow[k < kObs ? k : 0] : 0;
+        }
+        const u32x4 w = {pk2((__bf16)(float)v[0], (__bf16)(float)v[1]), pk2((__bf16)(float)v[2], (__bf16)(float)v[3]),
+                         pk2((__bf16)(float)v[4], (__bf16)(float)v[5]), pk2((__bf16)(float)v[6], (__bf16)(float)v[7])};
+        X[0][s] = __builtin_bit_cast(bf16x8, w);
+    }
+}
+
+constexpr int kAheadL1 = 2, kAheadHid = 1;  // A-plane prefetch depth (k-steps) in the ring kernel
 
 // The per-table epilogue over one table's 45 logits (`row`) and mask bytes: greedy masked argmax
 // (training_utils.py:263-276) or masked_categorical's sample, log-prob and entropy, plus the critic
@@ -307,15 +407,10 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
 
     // grouped rows: the wave's table ids, one load (lane i < valid holds row i's), then shuffles
     const int32_t tid_own = (a.order && lane < valid) ? a.order[tbase + lane] : 0;
-    // observation B fragments: lane (r, g), k-step s = obs[table r][4s + g] (exact in fp32)
+    // observation B fragments (load_obs)
     const int64_t xt = valid > 0 ? (a.order ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : tbase + (r < valid ? r : 0)) : 0;
-    const int32_t *xrow = a.obs + (size_t)xt * kObs;
-    float X[kKs1];
-#pragma unroll
-    for (int s = 0; s < kKs1; ++s) {
-        const int k = 4 * s + g;
-        X[s] = k < kObs ? (float)xrow[k < kObs ? k : 0] : 0.f;
-    }
+    bf16x8 X[1][kKs1];
+    load_obs(a.obs + (size_t)xt * kObs, g, X);
     if constexpr (!kActor) {
         // get_value: no mask
     } else if (a.order) {
@@ -353,8 +448,8 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         return ring;
 #endif
         // this wave's part of chunk c landed (later chunks' loads may stay outstanding)
-        if (wave < kChunkBlocks - 2 * kWaves) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if (wave < kChunkBlocks - (kBlocksPerWave - 1) * kWaves) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // everyone's part landed; slot c-1 is free
         asm volatile("" ::: "memory");
         const int nxt = c + kSlots - 1 < kTotal ? c + kSlots - 1 : kTotal - 1;  // past the end: harmless reload
@@ -363,16 +458,16 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         ++c;
         return slot;
     };
-    static_assert((kSlots - 2) * 3 == 12 && (kSlots - 2) * 2 == 8, "vmcnt immediates");
+    static_assert((kSlots - 2) * kBlocksPerWave == 8 && (kSlots - 2) * (kBlocksPerWave - 1) == 6, "vmcnt immediates");
 
-    float H1[kKs2];
+    bf16x8 H1[kPlanes][kKs2];
     float value = 0.f;
     if constexpr (kCritic) {
-        layer_tanh<kKs1>(enter, X, H1, lane);
+        layer_tanh<kKs1, 1, kAheadL1>(enter, X, H1, lane);
         // layer 2 tile t -> tanh -> its units' share of the fp32 output unit, on the spot
 #pragma unroll 1
         for (int t = 0; t < kTiles; ++t) {
-            const f32x4 acc = tile_mma<kKs2>(enter(), H1, lane);
+            const f32x4 acc = tile_mma<kKs2, kPlanes, kAheadHid>(enter(), H1, lane);
             const float4 w = *reinterpret_cast<const float4 *>(a.critic_out + 16 * t + 4 * g);
             value = __builtin_fmaf(w.x, tanh_f32(acc[0]), value);
             value = __builtin_fmaf(w.y, tanh_f32(acc[1]), value);
@@ -388,12 +483,12 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         if (g == 0 && r < valid) a.value[table_of(r)] = value;
         return;
     }
-    layer_tanh<kKs1>(enter, X, H1, lane);
-    float H2[kKs2];
-    layer_tanh<kKs2>(enter, H1, H2, lane);
+    layer_tanh<kKs1, 1, kAheadL1>(enter, X, H1, lane);
+    bf16x8 H2[kPlanes][kKs2];
+    layer_tanh<kKs2, kPlanes, kAheadHid>(enter, H1, H2, lane);
     f32x4 L[kActTiles];
 #pragma unroll
-    for (int t = 0; t < kActTiles; ++t) L[t] = tile_mma<kKs2>(enter(), H2, lane);
+    for (int t = 0; t < kActTiles; ++t) L[t] = tile_mma<kKs2, kPlanes, kAheadHid>(enter(), H2, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing reloads
     __builtin_amdgcn_s_barrier();                      // every wave is done with the ring
 
@@ -421,45 +516,33 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
 // full 128-table workgroups stay in k_act32; its tail runs here in wave-tiles of 16 tables, ONE
 // wave-tile per 8-wave workgroup, the 16 output tiles of each hidden layer split over the waves
 // (wave w: tiles w, w + 8), the weights read straight from the image (L2-resident, shared by every
-// workgroup of the network), a whole tile's A fragments in flight at once, and each
+// workgroup of the network; tile_mma with the A planes kAheadGlobal k-steps ahead), and each
 // layer's outputs exchanged through LDS.  A tail wave-tile takes a small fraction of a full
 // workgroup's time (5 tile chains per wave instead of 35).
-template <int KS, int NB>
-__device__ __forceinline__ f32x4 tile_mma_global(const uint8_t *chunk, const float (&B)[NB], int lane) {
-    static_assert(KS <= NB && KS % 4 == 0, "B fragments");
-    // the whole tile's A fragments in flight at once (one L2 round trip per tile, not one per group:
-    // 19 x 16 B per lane in layer 1), then the MFMA chain
-    constexpr int NG = KS / 4;
-    const float *bias = reinterpret_cast<const float *>(chunk + kBiasOff) + 4 * (lane >> 4);
-    const f32x4 *A = reinterpret_cast<const f32x4 *>(chunk) + lane;
-    f32x4 af[NG];
-#pragma unroll
-    for (int q = 0; q < NG; ++q) af[q] = A[q * 64];
-    f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
-#pragma unroll
-    for (int q = 0; q < NG; ++q)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(af[q][j], B[4 * q + j], acc, 0, 0, 0);
-    return acc;
-}
+constexpr int kAheadGlobal = 3;
 
 constexpr int kNarrowWaves = 8;  // two hidden-layer tiles per wave (2 waves per SIMD: room for the A fragments)
 
 // one hidden layer split over the waves (wave w: tiles w and w + 8), then every wave gathers all
 // 16 tiles' tanh outputs (its next layer's B fragments) from LDS
 template <int KS, int NB>
-__device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const float (&B)[NB], float (&H)[kKs2],
-                                             float *xbuf, int wave, int lane) {
+__device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const bf16x8 (&B)[NB][KS],
+                                             bf16x8 (&H)[kPlanes][kKs2], float *xbuf, int wave, int lane) {
 #pragma unroll
     for (int h = 0; h < kTiles / kNarrowWaves; ++h) {
         const int t = wave + kNarrowWaves * h;
-        const f32x4 acc = tile_mma_global<KS>(W + (size_t)(chunk0 + t) * kChunk, B, lane);
+        const f32x4 acc = tile_mma<KS, NB, kAheadGlobal>(W + (size_t)(chunk0 + t) * kChunk, B, lane);
 #pragma unroll
         for (int i = 0; i < 4; ++i) xbuf[(4 * t + i) * 64 + lane] = tanh_f32(acc[i]);
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kKs2; ++k) H[k] = xbuf[k * 64 + lane];
+    for (int t = 0; t < kTiles; ++t) {
+        float h[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[i] = xbuf[(4 * t + i) * 64 + lane];
+        put_split(H, t, h);
+    }
     __syncthreads();  // xbuf is written again by the next layer
 }
 
@@ -480,13 +563,8 @@ __global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_
     const int valid = (int)max<int64_t>(0, min<int64_t>(kRowsPerWave, gend - tbase));
     const int32_t tid_own = lane < valid ? a.order[tbase + lane] : 0;
     const int64_t xt = valid > 0 ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : 0;
-    const int32_t *xrow = a.obs + (size_t)xt * kObs;
-    float X[kKs1];
-#pragma unroll
-    for (int s = 0; s < kKs1; ++s) {
-        const int k = 4 * s + g;
-        X[s] = k < kObs ? (float)xrow[k < kObs ? k : 0] : 0.f;
-    }
+    bf16x8 X[1][kKs1];
+    load_obs(a.obs + (size_t)xt * kObs, g, X);
     if (wave == 0) {  // the wave-tile's mask bytes (gathered rows), for the epilogue
         constexpr int kMI = (kMaskWave + 63) / 64;
         uint32_t mv[kMI];
@@ -502,11 +580,11 @@ __global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_
             if (e < valid * kAct) ms[e] = (uint8_t)mv[i];
         }
     }
-    float H1[kKs2], H2[kKs2];
-    narrow_layer<kKs1>(W, 0, X, H1, xbuf, wave, lane);
-    narrow_layer<kKs2>(W, kTiles, H1, H2, xbuf, wave, lane);
+    bf16x8 H1[kPlanes][kKs2], H2[kPlanes][kKs2];
+    narrow_layer(W, 0, X, H1, xbuf, wave, lane);
+    narrow_layer(W, kTiles, H1, H2, xbuf, wave, lane);
     if (wave < kActTiles) {  // logits: waves 0..2 take one 16-row tile each
-        const f32x4 L = tile_mma_global<kKs2>(W + (size_t)(2 * kTiles + wave) * kChunk, H2, lane);
+        const f32x4 L = tile_mma<kKs2, kPlanes, kAheadGlobal>(W + (size_t)(2 * kTiles + wave) * kChunk, H2, lane);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int act = 16 * wave + 4 * g + i;

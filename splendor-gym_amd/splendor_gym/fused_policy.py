@@ -14,9 +14,10 @@ tables in one HIP launch straight from the engine's int32 observations and int8 
   * ``get_value(obs)`` = ``model.get_value(obs.float())`` (ppo_splendor.py:51, the bootstrap value
     of ppo_splendor.py:302): the critic alone, fp32.
 
-precision="fp32" (default, the reference's precision): exact fp32 products and accumulation on
-v_mfma_f32_16x16x4_f32 — logits and values equal the fp32 module's to summation-order rounding
-(tests/test_gpu_policy.py: 1e-5 relative).  precision="bf16" (opt-in): bf16 MFMA with fp32
+precision="fp32" (default, the reference's precision): fp32-accurate products — every operand split
+into three bf16 planes, the six plane products of order <= 2 accumulated in fp32 on
+v_mfma_f32_16x16x32_bf16 (csrc/spl_policy32.hip) — so logits and values equal the fp32 module's to
+summation-order rounding (tests/test_gpu_policy.py: 1e-5 relative).  precision="bf16" (opt-in): bf16 MFMA with fp32
 accumulation, logits to bf16 accuracy.  Call ``refresh()`` after the module's weights change (e.g.
 after each PPO update).
 """

@@ -1,7 +1,8 @@
 """Fused ActorCritic forward (include/splendor_policy.h) against the torch fp32 module it replaces
 (ppo_splendor.py:27-59 ActorCritic / masked_categorical; training_utils.py:263-276 greedy).
 
-fp32 kernel (the default, the reference's precision; exact fp32 products on v_mfma_f32_16x16x4_f32):
+fp32 kernel (the default, the reference's precision; fp32-accurate products: three bf16 planes per
+operand, six plane products accumulated in fp32 on v_mfma_f32_16x16x32_bf16):
   * |logit - ref| <= 1e-5 * (|ref| + 1) and |value - ref| <= 1e-5 * (|ref| + 1) against the plain
     fp32 module (what is left is summation order and the kernel's few-ulp tanh vs torch's, ~1e-7);
   * greedy actions EQUAL torch's argmax on every row whose top two legal logits are more than

@@ -37,7 +37,7 @@ def main():
     obs, mask = e.obs, e.mask
     torch.manual_seed(0)
     m = ActorCritic().to(e.device).eval()
-    f = FusedActorCritic(m)                       # fp32 (exact products, v_mfma_f32_16x16x4_f32)
+    f = FusedActorCritic(m)                       # fp32 (fp32-accurate split-bf16 products)
     f16 = FusedActorCritic(m, precision="bf16")   # opt-in bf16 MFMA
 
     def timeit(fn):

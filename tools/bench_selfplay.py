@@ -30,7 +30,7 @@ def main():
                     help="opt-in reduced precision: the fused kernel's bf16 MFMA image, or the torch actor under bf16 "
                          "autocast (default fp32, the reference's precision)")
     ap.add_argument("--actor", choices=["fused", "torch"], default="fused",
-                    help="fused: spl_policy_act (fp32 MFMA kernel, bf16 with --bf16) for agent and opponent; "
+                    help="fused: spl_policy_act (fp32-accurate split-bf16 kernel, bf16 with --bf16) for agent and opponent; "
                          "torch: the nn.Module")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--opponent", choices=["pool", "frozen"], default="pool",
@@ -144,7 +144,7 @@ def main():
                                       if fused and args.opponent == "pool" else
                                       "(greedy frozen-ActorCritic opponent, reset after done)"),
                        "weights": args.weights, "tables_per_gpu": N, "players": 2, "launch": "hipGraph replay" if graph is not None else "eager",
-                       "actor": (f"spl_policy_act (fused, {'bf16' if args.bf16 else 'fp32'} MFMA)" if fused
+                       "actor": (f"spl_policy_act (fused, {'bf16 MFMA' if args.bf16 else 'fp32-accurate split-bf16 MFMA'})" if fused
                                  else "torch nn.Module" + (" (bf16 autocast)" if args.bf16 else ""))},
             "env_only": {"value": round(steps / env_only, 1), "ms_per_dual_step": round(env_only / args.iters * 1e3, 4),
                          "note": "same loop with the agent's forward replaced by device uniform sampling (eager)"},
