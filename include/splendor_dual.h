@@ -59,6 +59,20 @@ int spl_dual_finish(int32_t n, const spl_dual_io_t *io, void *stream);
 int spl_dual_draw_opponents(int32_t n, const uint8_t *draw, uint32_t *episode, int32_t *group_of,
                             const int32_t *pool_slots, int32_t pool_len, float p_current, uint64_t seed, int64_t table0,
                             void *stream);
+/* spl_dual_finish, then in the same launch spl_dual_draw_opponents with draw = io->done (the tables
+ * re-dealt in this dual step), group_prev[t] = group_of[t] before the draw (the opponent that played
+ * the finished episode; NULL = skip): one launch instead of three (finish, copy, draw). */
+typedef struct {
+    uint32_t *episode;
+    int32_t *group_of;
+    int32_t *group_prev;
+    const int32_t *pool_slots;
+    int32_t pool_len;
+    float p_current;
+    uint64_t seed;
+    int64_t table0;
+} spl_dual_draw_t;
+int spl_dual_finish_draw(int32_t n, const spl_dual_io_t *io, const spl_dual_draw_t *draw, void *stream);
 
 #ifdef __cplusplus
 }

@@ -22,6 +22,38 @@ __global__ __launch_bounds__(256) void k_dual_gate(int n, const uint8_t *__restr
     if (!passed) opp[i] = -1;
 }
 
+// ppo_splendor.py:137-143 opponent_supplier for table i starting an episode
+__device__ __forceinline__ void draw_one(int i, uint32_t *__restrict__ episode, int32_t *__restrict__ group_of,
+                                         const int32_t *__restrict__ pool_slots, int pool_len, float p_current,
+                                         uint64_t seed, int64_t table0) {
+    const uint32_t ep = episode[i];
+    episode[i] = ep + 1;
+    const uint64_t t = (uint64_t)(table0 + i);
+    const uint4 r = spl::philox4x32(make_uint4((uint32_t)t, (uint32_t)(t >> 32), ep, 0x6F70706Fu),
+                                    make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    const float u = (float)(r.x >> 8) * (1.f / 16777216.f);
+    group_of[i] = (pool_len <= 0 || u < p_current) ? 0 : pool_slots[(uint32_t)(((uint64_t)r.y * (uint32_t)pool_len) >> 32)];
+}
+
+__global__ __launch_bounds__(256) void k_draw_opponents(int n, const uint8_t *__restrict__ draw,
+                                                        uint32_t *__restrict__ episode, int32_t *__restrict__ group_of,
+                                                        const int32_t *__restrict__ pool_slots, int pool_len,
+                                                        float p_current, uint64_t seed, int64_t table0) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || (draw && draw[i] == 0)) return;
+    draw_one(i, episode, group_of, pool_slots, pool_len, p_current, seed, table0);
+}
+
+struct Draw {
+    uint32_t *episode;
+    int32_t *group_of, *group_prev;
+    const int32_t *pool_slots;
+    int pool_len;
+    float p_current;
+    uint64_t seed;
+    int64_t table0;
+};
+
 // final_rewards[player] of a finished game (envs/splendor_env.py:92-115): +-1 for the winner /
 // loser; without a winner -0.1 after the turn limit, else 0 (the no-legal-move draw reports none)
 __device__ __forceinline__ float final_reward(int player, int winner, uint8_t flags) {
@@ -39,7 +71,8 @@ struct Io {
     uint8_t *info;
 };
 
-__global__ __launch_bounds__(256) void k_dual_finish(int n, Io io) {
+template <bool kDraw>
+__global__ __launch_bounds__(256) void k_dual_finish(int n, Io io, Draw d) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint8_t ta = io.ta[i], fa = io.fa[i], fb = io.fb[i];
@@ -51,6 +84,10 @@ __global__ __launch_bounds__(256) void k_dual_finish(int n, Io io) {
     io.ended_on[i] = ended_a ? 1 : ended_b ? 2 : 0;
     io.info[i] = ((fa & SPL_F_ILLEGAL) ? SPL_DUAL_ILLEGAL : 0) | (((fa | fb) & SPL_F_DRAW) ? SPL_DUAL_DRAW : 0) |
                  (((fa | fb) & SPL_F_TURN_LIMIT) ? SPL_DUAL_TURN_LIMIT : 0);
+    if constexpr (kDraw) {
+        if (d.group_prev) d.group_prev[i] = d.group_of[i];
+        if (ended_a || ended_b) draw_one(i, d.episode, d.group_of, d.pool_slots, d.pool_len, d.p_current, d.seed, d.table0);
+    }
 }
 
 // opponent_obs = done ? final_obs : obs, 16 bytes per thread (rows are 297 int32: a 16-byte
@@ -80,21 +117,7 @@ __global__ __launch_bounds__(256) void k_dual_opp_obs(int n, const uint8_t *__re
     }
 }
 
-// ppo_splendor.py:137-143 opponent_supplier for every table starting an episode
-__global__ __launch_bounds__(256) void k_draw_opponents(int n, const uint8_t *__restrict__ draw,
-                                                        uint32_t *__restrict__ episode, int32_t *__restrict__ group_of,
-                                                        const int32_t *__restrict__ pool_slots, int pool_len,
-                                                        float p_current, uint64_t seed, int64_t table0) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || (draw && draw[i] == 0)) return;
-    const uint32_t ep = episode[i];
-    episode[i] = ep + 1;
-    const uint64_t t = (uint64_t)(table0 + i);
-    const uint4 r = spl::philox4x32(make_uint4((uint32_t)t, (uint32_t)(t >> 32), ep, 0x6F70706Fu),
-                                    make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
-    const float u = (float)(r.x >> 8) * (1.f / 16777216.f);
-    group_of[i] = (pool_len <= 0 || u < p_current) ? 0 : pool_slots[(uint32_t)(((uint64_t)r.y * (uint32_t)pool_len) >> 32)];
-}
+
 
 }  // namespace spld
 
@@ -111,8 +134,11 @@ int spl_dual_gate(int32_t n, const uint8_t *terminated_a, const uint8_t *flags_a
     return e == hipSuccess ? SPL_OK : spl_fail(SPL_E_HIP, std::string("k_dual_gate: ") + hipGetErrorString(e));
 }
 
-int spl_dual_finish(int32_t n, const spl_dual_io_t *io, void *stream) {
+static int dual_finish(int32_t n, const spl_dual_io_t *io, const spl_dual_draw_t *draw, void *stream) {
     if (n <= 0) return spl_fail(SPL_E_ARG, "n must be positive");
+    if (draw && (!draw->episode || !draw->group_of || (draw->pool_len > 0 && !draw->pool_slots)))
+        return spl_fail(SPL_E_ARG, "null buffer");
+    if (draw && !(draw->p_current >= 0.f && draw->p_current <= 1.f)) return spl_fail(SPL_E_ARG, "p_current must be in [0, 1]");
     if (!io || !io->reward_a || !io->reward_b || !io->terminated_a || !io->terminated_b || !io->flags_a ||
         !io->flags_b || !io->winner_a || !io->winner_b || !io->agent_reward || !io->opp_reward || !io->done ||
         !io->game_ended_on || !io->info_flags)
@@ -123,7 +149,13 @@ int spl_dual_finish(int32_t n, const spl_dual_io_t *io, void *stream) {
     const hipStream_t s = (hipStream_t)stream;
     const Io k{io->reward_a, io->reward_b, io->terminated_a, io->terminated_b, io->flags_a, io->flags_b, io->winner_a,
                io->winner_b, io->agent_reward, io->opp_reward, io->done, io->game_ended_on, io->info_flags};
-    hipLaunchKernelGGL(k_dual_finish, dim3((n + 255) / 256), dim3(256), 0, s, n, k);
+    if (draw) {
+        const Draw d{draw->episode, draw->group_of, draw->group_prev, draw->pool_slots, draw->pool_len, draw->p_current,
+                     draw->seed, draw->table0};
+        hipLaunchKernelGGL(k_dual_finish<true>, dim3((n + 255) / 256), dim3(256), 0, s, n, k, d);
+    } else {
+        hipLaunchKernelGGL(k_dual_finish<false>, dim3((n + 255) / 256), dim3(256), 0, s, n, k, Draw{});
+    }
     if (io->opp_obs) {
         const int64_t quads = ((int64_t)n * 297 + 3) / 4;
         hipLaunchKernelGGL(k_dual_opp_obs, dim3((unsigned)((quads + 255) / 256)), dim3(256), 0, s, n, io->terminated_a,
@@ -132,6 +164,13 @@ int spl_dual_finish(int32_t n, const spl_dual_io_t *io, void *stream) {
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? SPL_OK : spl_fail(SPL_E_HIP, std::string("k_dual_finish: ") + hipGetErrorString(e));
+}
+
+int spl_dual_finish(int32_t n, const spl_dual_io_t *io, void *stream) { return dual_finish(n, io, nullptr, stream); }
+
+int spl_dual_finish_draw(int32_t n, const spl_dual_io_t *io, const spl_dual_draw_t *draw, void *stream) {
+    if (!draw) return spl_fail(SPL_E_ARG, "null draw arguments");
+    return dual_finish(n, io, draw, stream);
 }
 
 int spl_dual_draw_opponents(int32_t n, const uint8_t *draw, uint32_t *episode, int32_t *group_of,

@@ -63,6 +63,12 @@ class DualIo(ctypes.Structure):
                                         "game_ended_on", "info_flags", "obs", "final_obs", "opp_obs")]
 
 
+class DualDraw(ctypes.Structure):
+    """spl_dual_draw_t (include/splendor_dual.h)"""
+    _fields_ = [("episode", c_void_p), ("group_of", c_void_p), ("group_prev", c_void_p), ("pool_slots", c_void_p),
+                ("pool_len", c_int32), ("p_current", ctypes.c_float), ("seed", c_uint64), ("table0", c_int64)]
+
+
 DUAL_ILLEGAL, DUAL_DRAW, DUAL_TURN_LIMIT = 0x01, 0x02, 0x04  # SPL_DUAL_*
 
 
@@ -116,6 +122,7 @@ SIGNATURES = {
     # include/splendor_dual.h
     "spl_dual_gate": ([c_int32, c_void_p, c_void_p, c_void_p, c_void_p], c_int32),
     "spl_dual_finish": ([c_int32, ctypes.POINTER(DualIo), c_void_p], c_int32),
+    "spl_dual_finish_draw": ([c_int32, ctypes.POINTER(DualIo), ctypes.POINTER(DualDraw), c_void_p], c_int32),
     "spl_dual_draw_opponents": ([c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, ctypes.c_float, c_uint64,
                                  c_int64, c_void_p], c_int32),
     "spl_policy_group_scratch_bytes": ([c_int32, c_int32], c_int64),

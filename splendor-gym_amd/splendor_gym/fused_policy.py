@@ -248,6 +248,17 @@ class OpponentPool:
                 group_of.numel(), ptr(draw_mask), episode.data_ptr(), group_of.data_ptr(), self.slots.data_ptr(),
                 len(self.pool), ctypes.c_float(self.p_current), self.seed & (2**64 - 1), int(table0), self._stream()))
 
+    def finish_draw(self, io, group_of, episode, group_prev, table0=0):
+        """spl_dual_finish of a dual step (io: a DualIo) fused with draw(group_of, episode,
+        io.done): the tables that finished draw their next opponent; group_prev receives each
+        table's opponent before the draw.  One launch (include/splendor_dual.h)."""
+        d = _native.DualDraw(episode=episode.data_ptr(), group_of=group_of.data_ptr(), group_prev=group_prev.data_ptr(),
+                             pool_slots=self.slots.data_ptr(), pool_len=len(self.pool), p_current=self.p_current,
+                             seed=self.seed & (2**64 - 1), table0=int(table0))
+        with self.torch.cuda.device(self.device):
+            check(self.lib, self.lib.spl_dual_finish_draw(group_of.numel(), ctypes.byref(io), ctypes.byref(d),
+                                                          self._stream()))
+
     def act(self, obs, mask, group_of, out=None):
         """Greedy action of each table's network: int32 [n]."""
         t = self.torch

@@ -92,6 +92,7 @@ class DualStepVectorEnv:
         if self.pool is not None:  # per-table opponent of the current episode, and each table's episode count
             self.opp_group = z(t.int32)
             self.episode = z(t.int32)
+            self.ep_opp = z(t.int32)  # info["episode_opponent_index"]: the opponent before this step's draw
             self.pool.track(self.opp_group)  # slots still in play are not overwritten by add_snapshot
         e = self.eng
         ra, ta, fa, wa = self.small_a
@@ -148,13 +149,15 @@ class DualStepVectorEnv:
             e.step(opp, autoreset=2, final_obs=True)
             io = self._io
             io.opp_obs = self.opp_obs.data_ptr() if self.want_opp_obs else None
-            _native.check(lib, lib.spl_dual_finish(self.num_envs, ctypes.byref(io), stream))
+            if self.pool is not None:  # finish + the finished tables' next-opponent draw, one launch
+                self.pool.finish_draw(io, self.opp_group, self.episode, self.ep_opp, self.eng.table0)
+            else:
+                _native.check(lib, lib.spl_dual_finish(self.num_envs, ctypes.byref(io), stream))
         base = {"action_mask": e.mask, "to_play": e.obs[:, 294], "final_observation": e.final_obs,
                 "opponent_action": opp, "game_ended_on": self.game_ended_on, "agent_step_reward": ra}
         if self.pool is not None:
             # the opponent that played this step's episode, then the next episode's for re-dealt tables
-            base["episode_opponent_index"] = self.opp_group.clone()
-            self.pool.draw(self.opp_group, self.episode, self.done, self.eng.table0)
+            base["episode_opponent_index"] = self.ep_opp
             base["opponent_index"] = self.opp_group
         info = DualInfo(base, self.info_flags)
         return e.obs, self.agent_reward, self.opp_obs, self.opp_reward, self.done, info
