@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 4
+#define SPL_ABI_VERSION 5  /* 5: spl_step_args_t.obs_u8 (compact observation) */
 
 /* ---- per-table flag bits (uint8) --------------------------------------------------- */
 #define SPL_F_ILLEGAL 0x01        /* info["illegal_action"]      envs/splendor_env.py:64-66 */
@@ -108,6 +108,11 @@ typedef struct spl_step_args_s {
     uint64_t *errors;        /* [1] or NULL (spl_step only): += the number of tables whose flags
                                 carry SPL_F_OOB or SPL_F_AFTER_TERMINAL (the reference's
                                 ValueError / RuntimeError cases, envs/splendor_env.py:53-63)   */
+    uint8_t *obs_u8;         /* [n][300] or NULL (spl_step only): the observation as bytes for a
+                                device consumer (spl_act_args_t.obs_u8), a quarter of obs's bytes:
+                                bytes 0..296 = obs (every value < 256 but move_count, byte 295 =
+                                move_count mod 256), byte 297 = move_count >> 8, 298-299 = 0.
+                                With obs_u8 set, obs may be NULL (then only the bytes are written) */
 } spl_step_args_t;
 
 int spl_abi_version(void);

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SPL_POLICY_ABI 2  /* 2: precision argument, args->image describes the image */
+#define SPL_POLICY_ABI 3  /* 2: precision argument, args->image describes the image; 3: obs_u8 */
 
 #define SPL_PREC_FP32 0
 #define SPL_PREC_BF16 1
@@ -65,6 +65,8 @@ typedef struct {
     int32_t mode;        /* SPL_ACT_*                                                            */
     int32_t image;       /* how the image was packed: SPL_IMG_CRITIC if with a critic | precision << 1;
                             packed_bytes must equal spl_policy_bytes(critic, precision)              */
+    const uint8_t *obs_u8; /* [n][300] or NULL: the observation as spl_step's obs_u8 bytes, read
+                            instead of obs (fp32 images only); obs may then be NULL              */
 } spl_act_args_t;
 
 /* bytes of a packed image: with_critic 0 = actor only (greedy opponents), 1 = actor + critic;

@@ -60,6 +60,7 @@ struct KStep {
     float *ep_return;
     uint32_t *ep_count;
     uint8_t *info;             // nullable: [4][n] info planes + truncated (spl_step)
+    uint8_t *obs_u8;           // nullable: [n][300] compact observation instead of obs (k_step_ws)
     unsigned long long *errors;  // nullable: running count of tables with an error flag (spl_step)
     const uint64_t *ply_base;  // nullable: device counter added to `ply` (graph replays)
     uint64_t policy_seed;
@@ -70,6 +71,7 @@ struct KStep {
 };
 
 constexpr int kObsDim = 297;
+constexpr int kObsU8 = 300;  // compact observation row (spl_step_args_t.obs_u8): 297 bytes + move_count >> 8 + 2 zero
 
 // Ablation switches for profiling builds only (tools/ablate.py); the product build defines none.
 #ifndef SPL_ABL
@@ -946,6 +948,20 @@ __device__ __forceinline__ void encode_row_half(const Tab<P> &T, uint8_t *rows_b
     if (Half == 1 && o0 == 0u) dst[74] = R[74];
 }
 
+// The compact observation row (spl_step_args_t.obs_u8) of table T at rows_base[300*lane ...]:
+// the row's 297 bytes, move_count >> 8, two zero bytes — 75 aligned dwords per row (no
+// neighbouring-lane bytes).  Part 0: dwords [0, kRowHalf), 1: [kRowHalf, 75), 2: all.
+template <int Part, int P>
+__device__ __forceinline__ void encode_row_u8(const Tab<P> &T, uint8_t *rows_base, const Consts &L) {
+    uint32_t R[76];
+    build_row(T, L, R);
+    R[74] = (R[74] & 0xFFu) | ((uint32_t)(get_moves(T.sw) >> 8) << 8);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(rows_base + kObsU8 * lane_id());
+    constexpr int j0 = Part == 1 ? kRowHalf : 0, j1 = Part == 0 ? kRowHalf : 75;
+#pragma unroll
+    for (int j = j0; j < j1; ++j) dst[j] = R[j];
+}
+
 // Observation of table T written by its own lane straight to dst[0..296] (int32; 297 dword
 // stores): the rare path for terminal rows that do not fit the pipelined kernel's hand-off.
 template <int P>
@@ -1036,6 +1052,18 @@ __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int row
     }
     for (; d < full; d += 64) st_v4<NT>(out + d, expand4(src[d]));
     for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) dst[b] = (int32_t)rows_lds[b];
+}
+
+// Block store of `rows` compact rows (300 bytes each) staged in LDS to dst (16-byte aligned).
+__device__ __forceinline__ void store_obs_u8_block(const uint8_t *rows_lds, int rows, uint8_t *dst) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
+    const int words = rows * (kObsU8 / 4), chunks = words >> 2;
+    v4i *out = reinterpret_cast<v4i *>(dst);
+    for (int c = lane_id(); c < chunks; c += 64) {
+        const v4i v = {(int)src[4 * c], (int)src[4 * c + 1], (int)src[4 * c + 2], (int)src[4 * c + 3]};
+        out[c] = v;
+    }
+    for (int w = 4 * chunks + lane_id(); w < words; w += 64) reinterpret_cast<uint32_t *>(dst)[w] = src[w];
 }
 
 // Block store of this wave's masks: mask[t0 .. t0+rows) as int8 [rows][45].  The 64 x 45 mask
@@ -1930,7 +1958,9 @@ struct __align__(16) StepWsLDS : Consts {
     uint64_t fin;          // terminal rows left to the output wave (beyond kTermRows)
     uint32_t mbits[96];
     uint32_t trow[kTermRows][75];  // the rules wave's terminal rows, compacted (297 bytes in 75 dwords)
-    uint8_t rows[64 * kObsDim];  // observation staging; before hand-off 1 the rules wave's deal scratch + LaneMT
+    // observation staging (rows of 297 bytes, or 300 for obs_u8); before hand-off 1 the rules wave's
+    // deal scratch + LaneMT
+    alignas(16) uint8_t rows[64 * kObsU8];
 };
 static_assert(sizeof(StepWsLDS<4>) <= 40960, "k_step_ws_* needs four workgroups per CU");
 
@@ -1944,6 +1974,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
     const bool valid = t < A.n;
     const int rows = min(64, A.n - t0);
     const bool want_final = S.autoreset && S.final_obs != nullptr;
+    const bool compact = S.obs_u8 != nullptr;  // obs_u8 rows instead of int32 obs rows
     STAMP(0);
     if (rules_wave) {
         __builtin_amdgcn_s_setprio(SPL_WS_PRIO);  // as in the rollout: 27.9 -> 27.3 us
@@ -1991,7 +2022,10 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         // Without terminal rows left to the output wave (the usual case) this wave encodes the first
         // half of every row while the output wave encodes the second (encode 2.7 -> ~1.4 us before
         // the obs stores start); otherwise the output wave encodes whole rows after its terminal ones.
-        if (fin == 0ull) encode_row_half<0>(T, L.rows, L);
+        if (fin == 0ull) {
+            if (compact) encode_row_u8<0>(T, L.rows, L);
+            else encode_row_half<0>(T, L.rows, L);
+        }
         ws_sync();  // hand-off 2: first row halves staged
         STAMP(4);
         if (fin_rules) {  // info["final_observation"] rows, compacted in trow, stored row by row
@@ -2053,7 +2087,10 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
 #pragma unroll
         for (int w = 0; w < kW; ++w) set_tab_word(T, w, L.st[w][lane]);
         const uint64_t fin = L.fin;
-        if (fin == 0ull) encode_row_half<1>(T, L.rows, L);
+        if (fin == 0ull) {
+            if (compact) encode_row_u8<1>(T, L.rows, L);
+            else encode_row_half<1>(T, L.rows, L);
+        }
         ws_sync();  // hand-off 2
         STAMP(4);
         if (fin) {  // terminal rows (info["final_observation"]) first, through the same staging rows
@@ -2071,10 +2108,16 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
                 if (mine && get_moves(F.sw) > 255) S.final_obs[(size_t)t * kObsDim + 295] = get_moves(F.sw);
             }
             wave_lds_sync();  // the terminal rows' LDS reads are done
-            encode_row(T, L.rows, L);
+            if (compact) encode_row_u8<2>(T, L.rows, L);
+            else encode_row(T, L.rows, L);
             wave_lds_sync();
         }
         STAMP(5);
+        if (compact) {
+            store_obs_u8_block(L.rows, rows, S.obs_u8 + (size_t)t0 * kObsU8);
+            STAMP(6);
+            return;
+        }
         store_obs_block<64, SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
         STAMP(6);
         if (__any(valid && get_moves(T.sw) > 255)) {  // patch after this wave's block stores of the same dwords
@@ -3288,8 +3331,10 @@ int spl_refill(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
 }
 
 static int check_step_args(const spl_step_args_t *a) {
-    if (!a || !a->actions || !a->obs || !a->mask || !a->reward || !a->terminated || !a->flags)
+    if (!a || !a->actions || !(a->obs || a->obs_u8) || !a->mask || !a->reward || !a->terminated || !a->flags)
         return fail(SPL_E_ARG, "actions/obs/mask/reward/terminated/flags are required");
+    if (a->obs && a->obs_u8) return fail(SPL_E_ARG, "obs and obs_u8 are exclusive");
+    if ((uintptr_t)a->obs_u8 & 15u) return fail(SPL_E_ARG, "obs_u8 must be 16-byte aligned");
     if (a->autoreset < 0 || a->autoreset > 2) return fail(SPL_E_ARG, "autoreset must be 0, 1 or 2");
     if (a->policy < SPL_POLICY_UNIFORM || a->policy > SPL_POLICY_BASIC_PRIORITY) return fail(SPL_E_ARG, "unknown policy");
     if (((uintptr_t)a->obs & 15u) || (a->final_obs && ((uintptr_t)a->final_obs & 3u)))
@@ -3312,6 +3357,7 @@ static KStep kstep(const spl_step_args_t *a) {
     S.ep_return = a->ep_return;
     S.ep_count = a->ep_count;
     S.info = a->info;
+    S.obs_u8 = a->obs_u8;
     S.errors = reinterpret_cast<unsigned long long *>(a->errors);
     S.ply_base = a->ply_base;
     S.policy_seed = a->policy_seed;
@@ -3325,6 +3371,7 @@ static KStep kstep(const spl_step_args_t *a) {
 int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void *stream) {
     if (int r = check_arena(ctx, arena)) return r;
     if (int r = check_step_args(a)) return r;
+    if (a->obs_u8 && !kStepWs) return fail(SPL_E_ARG, "obs_u8 needs the two-wave step kernel");
     const KStep S = kstep(a);
     const KArena A = karena(arena);
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -3380,6 +3427,7 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
                 void *stream) {
     if (int r = check_arena(ctx, arena)) return r;
     if (int r = check_step_args(a)) return r;
+    if (!a->obs) return fail(SPL_E_ARG, "spl_rollout writes int32 obs (obs_u8 is spl_step only)");
     if (steps < 1) return fail(SPL_E_ARG, "spl_rollout: steps must be >= 1");
     if (per_step_outputs && (arena->n & 3))
         return fail(SPL_E_ARG, "spl_rollout: per-step outputs need a table count divisible by 4 (16-byte obs blocks)");

@@ -505,6 +505,18 @@ int spl_policy_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, int32_t pre
     return SPL_OK;
 }
 
+// the observation: int32 obs (16-byte aligned), or (fp32 images) the compact obs_u8 rows
+static int check_obs(const spl_act_args_t *args, int precision) {
+    if (args->obs_u8) {
+        if (args->obs) return spl_fail(SPL_E_ARG, "obs and obs_u8 are exclusive");
+        if (precision != SPL_PREC_FP32) return spl_fail(SPL_E_ARG, "obs_u8 is read by the fp32 kernels");
+        if ((uintptr_t)args->obs_u8 & 3u) return spl_fail(SPL_E_ARG, "obs_u8 must be 4-byte aligned");
+        return SPL_OK;
+    }
+    if (!args->obs || ((uintptr_t)args->obs & 15u)) return spl_fail(SPL_E_ARG, "obs must be 16-byte aligned");
+    return SPL_OK;
+}
+
 int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const spl_act_args_t *args, void *stream) {
     if (!args) return spl_fail(SPL_E_ARG, "null args");
     if (!packed || ((uintptr_t)packed & 255u)) return spl_fail(SPL_E_ARG, "packed image must be 256-byte aligned");
@@ -516,7 +528,7 @@ int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const sp
     if (packed_bytes != spl_policy_bytes(has_critic ? 1 : 0, precision))
         return spl_fail(SPL_E_ARG, "packed_bytes does not match the image described by args->image");
     if (n <= 0) return spl_fail(SPL_E_ARG, "n must be positive");
-    if (!args->obs || ((uintptr_t)args->obs & 15u)) return spl_fail(SPL_E_ARG, "obs must be 16-byte aligned");
+    if (int r = check_obs(args, precision)) return r;
     if (args->mode == SPL_ACT_VALUE) {  // ActorCritic.get_value (ppo_splendor.py:51): the critic alone
         if (!has_critic || !args->value) return spl_fail(SPL_E_ARG, "VALUE needs an image with a critic and a value output");
         if (precision != SPL_PREC_FP32) return spl_fail(SPL_E_ARG, "VALUE is implemented for fp32 images");
@@ -567,7 +579,7 @@ int spl_policy_act_grouped(const void *images, int64_t image_bytes, int32_t n_im
     if (has_critic) return spl_fail(SPL_E_ARG, "grouped evaluation serves actor-only images");
     if (image_bytes < spl_policy_bytes(0, precision)) return spl_fail(SPL_E_ARG, "image_bytes smaller than an image");
     if (n <= 0) return spl_fail(SPL_E_ARG, "n must be positive");
-    if (!args->obs || ((uintptr_t)args->obs & 15u)) return spl_fail(SPL_E_ARG, "obs must be 16-byte aligned");
+    if (int r = check_obs(args, precision)) return r;
     if (!args->mask || !args->action) return spl_fail(SPL_E_ARG, "mask / action missing");
     if (args->mode != SPL_ACT_SAMPLE && args->mode != SPL_ACT_GREEDY) return spl_fail(SPL_E_ARG, "unknown mode");
     if (args->value) return spl_fail(SPL_E_ARG, "grouped evaluation has no critic");

@@ -147,6 +147,7 @@ __global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, i
 
 struct ActArgs {
     const int32_t *obs;
+    const uint8_t *obs_u8;  // compact rows instead of obs (spl_step_args_t.obs_u8), or NULL
     const int8_t *mask;
     int32_t *action;
     float *logprob, *entropy, *value, *logits;
@@ -292,6 +293,33 @@ __device__ __forceinline__ void layer_tanh(Enter &enter, const bf16x8 (&B)[NB][K
     }
 }
 
+// the same B fragments from a compact row (spl_step_args_t.obs_u8: 300 bytes, move_count >> 8 at
+// byte 297): 8 bytes per k-step as two dword loads, k = 296 alone, k >= 297 zero
+__device__ __forceinline__ void load_obs_u8(const uint8_t *xrow, int g, bf16x8 (&X)[1][kKs1]) {
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(xrow);
+#pragma unroll
+    for (int s = 0; s < kKs1; ++s) {
+        const int k0 = 32 * s + 8 * g;
+        uint32_t lo = 0u, hi = 0u;
+        if (k0 + 7 < kObs) {
+            lo = w[k0 >> 2];
+            hi = w[(k0 >> 2) + 1];
+        } else if (k0 < kObs) {  // k0 = 296 (s = 9, g = 1): byte 296 only
+            lo = w[k0 >> 2] & 0xFFu;
+        }
+        int v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            v[e] = (int)((lo >> (8 * e)) & 0xFFu);
+            v[4 + e] = (int)((hi >> (8 * e)) & 0xFFu);
+        }
+        if (k0 == 288) v[7] += 256 * (int)((w[74] >> 8) & 0xFFu);  // k = 295: move_count
+        const u32x4 q = {pk2((__bf16)(float)v[0], (__bf16)(float)v[1]), pk2((__bf16)(float)v[2], (__bf16)(float)v[3]),
+                         pk2((__bf16)(float)v[4], (__bf16)(float)v[5]), pk2((__bf16)(float)v[6], (__bf16)(float)v[7])};
+        X[0][s] = __builtin_bit_cast(bf16x8, q);
+    }
+}
+
 // the observation's B fragments: lane (r, g), k-step s, element e = obs[table r][32s + 8g + e]
 // (integers < 256: exact in bf16)
 __device__ __forceinline__ void load_obs(const int32_t *xrow, int g, bf16x8 (&X)[1][kKs1]) {
@@ -309,7 +337,13 @@ __device__ __forceinline__ void load_obs(const int32_t *xrow, int g, bf16x8 (&X)
     }
 }
 
-constexpr int kAheadL1 = 2, kAheadHid = 1;  // A-plane prefetch depth (k-steps) in the ring kernel
+#ifndef SPL_P32_AHEAD1
+#define SPL_P32_AHEAD1 2
+#endif
+#ifndef SPL_P32_AHEAD2
+#define SPL_P32_AHEAD2 1
+#endif
+constexpr int kAheadL1 = SPL_P32_AHEAD1, kAheadHid = SPL_P32_AHEAD2;  // A-plane prefetch depth (k-steps) in the ring kernel
 
 // The per-table epilogue over one table's 45 logits (`row`) and mask bytes: greedy masked argmax
 // (training_utils.py:263-276) or masked_categorical's sample, log-prob and entropy, plus the critic
@@ -410,7 +444,8 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
     // observation B fragments (load_obs)
     const int64_t xt = valid > 0 ? (a.order ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : tbase + (r < valid ? r : 0)) : 0;
     bf16x8 X[1][kKs1];
-    load_obs(a.obs + (size_t)xt * kObs, g, X);
+    if (a.obs_u8) load_obs_u8(a.obs_u8 + (size_t)xt * 300, g, X);
+    else load_obs(a.obs + (size_t)xt * kObs, g, X);
     if constexpr (!kActor) {
         // get_value: no mask
     } else if (a.order) {
@@ -564,7 +599,8 @@ __global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_
     const int32_t tid_own = lane < valid ? a.order[tbase + lane] : 0;
     const int64_t xt = valid > 0 ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : 0;
     bf16x8 X[1][kKs1];
-    load_obs(a.obs + (size_t)xt * kObs, g, X);
+    if (a.obs_u8) load_obs_u8(a.obs_u8 + (size_t)xt * 300, g, X);
+    else load_obs(a.obs + (size_t)xt * kObs, g, X);
     if (wave == 0) {  // the wave-tile's mask bytes (gathered rows), for the epilogue
         constexpr int kMI = (kMaskWave + 63) / 64;
         uint32_t mv[kMI];
@@ -683,9 +719,9 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
                void *stream, int groups = 0, int64_t image_stride = 0, const int32_t *group_of = nullptr,
                void *scratch = nullptr) {
     const float *critic_out = has_critic ? reinterpret_cast<const float *>(img + (size_t)kAllChunks * kChunk) : nullptr;
-    ActArgs a{args->obs,      args->mask,   args->action, args->logprob, args->entropy, args->value,  args->logits,
-              critic_out,     args->seed,   args->ply,    args->ply_base, args->table0,  n,           nullptr,
-              nullptr,        0,            0};
+    ActArgs a{args->obs,    args->obs_u8, args->mask,     args->action, args->logprob, args->entropy, args->value,
+              args->logits, critic_out,   args->seed,     args->ply,    args->ply_base, args->table0, n,
+              nullptr,      nullptr,      0,              0};
     dim3 grid((unsigned)((n + kRowsPerBlock - 1) / kRowsPerBlock)), block(kWaves * 64);
     if (groups > 0) {  // sort the tables by network, then one workgroup per 128 tables of one group
         if (groups > kMaxGroups) return spl_fail(SPL_E_ARG, "at most 64 networks per grouped call");

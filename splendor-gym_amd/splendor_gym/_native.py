@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 LIB_NAME = "libsplendor_amd.so"
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # per-table flag bits (include/splendor_amd.h)
 POLICY_UNIFORM, POLICY_GREEDY_V1, POLICY_BASIC_PRIORITY = 0, 1, 2  # SPL_POLICY_* (device next_actions)
@@ -18,6 +18,7 @@ F_ILLEGAL, F_DRAW, F_TURN_LIMIT = 0x01, 0x02, 0x04
 F_AFTER_TERMINAL, F_OOB, F_RESET, F_RNG_LIMIT = 0x08, 0x10, 0x20, 0x40
 
 OBS_DIM = 297
+OBS_U8 = 300  # spl_step_args_t.obs_u8 row: the 297 observation bytes, move_count >> 8, two zero bytes
 NUM_ACTIONS = 45
 
 c_void_p, c_int32, c_int64, c_uint64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
@@ -35,7 +36,8 @@ class StepArgs(ctypes.Structure):
                 ("terminated", c_void_p), ("flags", c_void_p), ("winner", c_void_p),
                 ("final_obs", c_void_p), ("autoreset", c_int32), ("policy", c_int32), ("next_actions", c_void_p),
                 ("ply_base", c_void_p), ("policy_seed", c_uint64), ("ply", c_uint64), ("table0", c_int64),
-                ("ep_return", c_void_p), ("ep_count", c_void_p), ("info", c_void_p), ("errors", c_void_p)]
+                ("ep_return", c_void_p), ("ep_count", c_void_p), ("info", c_void_p), ("errors", c_void_p),
+                ("obs_u8", c_void_p)]
 
 
 class MlpDesc(ctypes.Structure):
@@ -48,7 +50,8 @@ class ActArgs(ctypes.Structure):
     """spl_act_args_t (include/splendor_policy.h)"""
     _fields_ = [("obs", c_void_p), ("mask", c_void_p), ("action", c_void_p), ("logprob", c_void_p),
                 ("entropy", c_void_p), ("value", c_void_p), ("logits", c_void_p), ("seed", c_uint64),
-                ("ply", c_uint64), ("ply_base", c_void_p), ("table0", c_int64), ("mode", c_int32), ("image", c_int32)]
+                ("ply", c_uint64), ("ply_base", c_void_p), ("table0", c_int64), ("mode", c_int32), ("image", c_int32),
+                ("obs_u8", c_void_p)]
 
 
 ACT_SAMPLE, ACT_GREEDY, ACT_VALUE = 0, 1, 2  # SPL_ACT_*

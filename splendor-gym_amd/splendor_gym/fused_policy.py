@@ -24,7 +24,7 @@ after each PPO update).
 import ctypes
 
 from . import _native
-from ._native import (ACT_GREEDY, ACT_SAMPLE, ACT_VALUE, IMG_CRITIC, NUM_ACTIONS, OBS_DIM, PREC_BF16, PREC_FP32, ActArgs, MlpDesc,
+from ._native import (ACT_GREEDY, ACT_SAMPLE, ACT_VALUE, IMG_CRITIC, NUM_ACTIONS, OBS_DIM, OBS_U8, PREC_BF16, PREC_FP32, ActArgs, MlpDesc,
                       check, ptr)
 
 _PRECISIONS = {"fp32": PREC_FP32, "bf16": PREC_BF16}
@@ -86,8 +86,10 @@ class FusedActorCritic:
 
     def _check_inputs(self, obs, mask):
         t = self.torch
-        if obs.dtype != t.int32 or obs.dim() != 2 or obs.shape[1] != OBS_DIM or not obs.is_contiguous():
-            raise ValueError("obs must be a contiguous int32 [n, 297] device tensor")
+        u8 = obs.dtype == t.uint8 and self.precision == "fp32"  # compact rows (Engine.step obs_u8)
+        if (obs.dtype != t.int32 and not u8) or obs.dim() != 2 or obs.shape[1] != (OBS_U8 if u8 else OBS_DIM) \
+                or not obs.is_contiguous():
+            raise ValueError("obs must be a contiguous int32 [n, 297] device tensor (fp32: or uint8 [n, 300] rows)")
         if mask.dtype not in (t.int8, t.uint8, t.bool) or tuple(mask.shape) != (obs.shape[0], NUM_ACTIONS) or \
                 not mask.is_contiguous():
             raise ValueError("mask must be a contiguous int8 [n, 45] device tensor")
@@ -98,7 +100,8 @@ class FusedActorCritic:
     def _run(self, obs, mask, mode, action, logprob=None, entropy=None, value=None, logits=None, seed=0, ply=0,
              table0=0, ply_base=None):
         n = self._check_inputs(obs, mask) if mask is not None else obs.shape[0]
-        a = ActArgs(obs=obs.data_ptr(), mask=ptr(mask), action=ptr(action), logprob=ptr(logprob),
+        u8 = obs.dtype == self.torch.uint8
+        a = ActArgs(obs=None if u8 else obs.data_ptr(), obs_u8=obs.data_ptr() if u8 else None, mask=ptr(mask), action=ptr(action), logprob=ptr(logprob),
                     entropy=ptr(entropy), value=ptr(value), logits=ptr(logits), seed=int(seed) & (2**64 - 1),
                     ply=int(ply) & (2**64 - 1), ply_base=ptr(ply_base), table0=int(table0), mode=mode, image=self._image_flags)
         with self.torch.cuda.device(self.device):
@@ -143,8 +146,17 @@ class FusedActorCritic:
         return value
 
     def opponent(self):
-        """A batched opponent for DualStepVectorEnv: (obs, mask) -> int32 actions."""
-        return lambda obs, mask: self.greedy(obs, mask)
+        """A batched opponent for DualStepVectorEnv: (obs, mask) -> int32 actions.  An fp32 one also
+        takes the compact uint8 rows (accepts_u8), which the dual step then writes for it."""
+        f = self
+
+        class _Opponent:
+            accepts_u8 = f.precision == "fp32"
+
+            def __call__(self, obs, mask):
+                return f.greedy(obs, mask)
+
+        return _Opponent()
 
 
 class OpponentPool:
@@ -260,18 +272,21 @@ class OpponentPool:
                                                           self._stream()))
 
     def act(self, obs, mask, group_of, out=None):
-        """Greedy action of each table's network: int32 [n]."""
+        """Greedy action of each table's network: int32 [n].  obs: int32 [n, 297], or the compact
+        uint8 [n, 300] rows of Engine.step(obs_u8=...)."""
         t = self.torch
         n = obs.shape[0]
-        if obs.dtype != t.int32 or not obs.is_contiguous() or mask.dtype != t.int8 or not mask.is_contiguous():
-            raise ValueError("obs int32 [n, 297] and mask int8 [n, 45], contiguous")
+        u8 = obs.dtype == t.uint8
+        if (obs.dtype not in (t.int32, t.uint8) or obs.shape[1] != (OBS_U8 if u8 else OBS_DIM) or not obs.is_contiguous()
+                or mask.dtype != t.int8 or not mask.is_contiguous()):
+            raise ValueError("obs int32 [n, 297] (or uint8 [n, 300] compact rows) and mask int8 [n, 45], contiguous")
         nbytes = int(self.lib.spl_policy_group_scratch_bytes(n, self.n_images))
         if self._scratch is None or self._scratch.numel() < nbytes:  # zero-filled once (spl_policy_act_grouped)
             self._scratch = t.zeros(nbytes, dtype=t.uint8, device=self.device)
         action = out if out is not None else t.empty(n, dtype=t.int32, device=self.device)
-        a = ActArgs(obs=obs.data_ptr(), mask=mask.data_ptr(), action=action.data_ptr(), logprob=None, entropy=None,
-                    value=None, logits=None, seed=0, ply=0, ply_base=None, table0=0, mode=ACT_GREEDY,
-                    image=PREC_FP32 << 1)
+        a = ActArgs(obs=None if u8 else obs.data_ptr(), obs_u8=obs.data_ptr() if u8 else None, mask=mask.data_ptr(),
+                    action=action.data_ptr(), logprob=None, entropy=None, value=None, logits=None, seed=0, ply=0,
+                    ply_base=None, table0=0, mode=ACT_GREEDY, image=PREC_FP32 << 1)
         with t.cuda.device(self.device):
             check(self.lib, self.lib.spl_policy_act_grouped(self.images.data_ptr(), self.image_bytes, self.n_images,
                                                             group_of.data_ptr(), self._scratch.data_ptr(), n,

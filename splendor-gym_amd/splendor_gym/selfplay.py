@@ -94,6 +94,12 @@ class DualStepVectorEnv:
             self.episode = z(t.int32)
             self.ep_opp = z(t.int32)  # info["episode_opponent_index"]: the opponent before this step's draw
             self.pool.track(self.opp_group)  # slots still in play are not overwritten by add_snapshot
+        # the agent's move writes the opponent's observation as compact bytes for a fused fp32 opponent
+        # (the pool kernel, FusedActorCritic.opponent(): Engine.step obs_u8): a quarter of the int32
+        # rows' bytes to store and to read back
+        self.opp_obs_u8 = None
+        if self.pool is not None or getattr(opponent, "accepts_u8", False):
+            self.opp_obs_u8 = t.zeros(n, _native.OBS_U8, dtype=t.uint8, device=dev)
         e = self.eng
         ra, ta, fa, wa = self.small_a
         p = lambda x: None if x is None else x.data_ptr()
@@ -130,13 +136,14 @@ class DualStepVectorEnv:
         e.step(actions, autoreset=False, final_obs=False, small=self.small_a,
                next_actions=self.opp_actions if device_opp else None,
                policy=_DEVICE_POLICIES[self.opponent] if device_opp else 0,
-               policy_seed=self.policy_seed, ply=self._ply)
+               policy_seed=self.policy_seed, ply=self._ply,
+               obs_u8=None if device_opp else self.opp_obs_u8)
         if device_opp:
             opp = self.opp_actions
         elif self.pool is not None:
-            opp = self.pool.act(e.obs, e.mask, self.opp_group, out=self.opp_actions)
+            opp = self.pool.act(self.opp_obs_u8, e.mask, self.opp_group, out=self.opp_actions)
         else:
-            opp = self.opponent(e.obs, e.mask)
+            opp = self.opponent(e.obs if self.opp_obs_u8 is None else self.opp_obs_u8, e.mask)
             if not (isinstance(opp, torch.Tensor) and opp.dtype == torch.int32 and opp.is_contiguous()
                     and opp.device == self.device):
                 opp = torch.as_tensor(opp, device=self.device).to(torch.int32).contiguous()
