@@ -71,8 +71,14 @@ constexpr int kActorChunks = 2 * kTiles + kActTiles, kCriticChunks = 2 * kTiles;
 constexpr int kAllChunks = kActorChunks + kCriticChunks;                          // 67
 constexpr int kCriticTail = 272 * 4;  // fp32 critic output layer: w3 [256], b3, padding
 
-constexpr int kWaves = 8, kRowsPerWave = 16, kRowsPerBlock = kWaves * kRowsPerWave;  // 128 tables
-constexpr int kSlots = 4;
+#ifndef SPL_P32_WAVES
+#define SPL_P32_WAVES 8  // waves per k_act32 workgroup (16 tables each)
+#endif
+#ifndef SPL_P32_RING
+#define SPL_P32_RING 4  // ring slots (SPL_P32_RING - 1 chunks in flight)
+#endif
+constexpr int kWaves = SPL_P32_WAVES, kRowsPerWave = 16, kRowsPerBlock = kWaves * kRowsPerWave;  // 128 tables
+constexpr int kSlots = SPL_P32_RING;
 constexpr int kMaskWave = kRowsPerWave * kAct;  // 720 B
 constexpr int kLogitRow = 49;                   // floats per staged logit row (odd: conflict-free)
 constexpr int kLdsMask = kSlots * kChunk;
@@ -209,6 +215,11 @@ __device__ __forceinline__ void issue_chunk(const uint8_t *W, int chunk, uint8_t
             __builtin_amdgcn_global_load_lds(src + blk * 1024, (lds_void *)(slot + blk * 1024), 16, 0, 0);
     }
 }
+
+// s_waitcnt immediate for vmcnt(n) alone (gfx9: vmcnt[3:0] in bits 3:0, vmcnt[5:4] in 15:14)
+constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
+// a wave's loads of the chunks after chunk c that may stay in flight when it enters chunk c
+constexpr int kWaitMost = (kSlots - 2) * kBlocksPerWave, kWaitLast = (kSlots - 2) * (kBlocksPerWave - 1);
 
 __device__ __forceinline__ f32x4 mma(const bf16x8 &a, const bf16x8 &b, const f32x4 &c) {
 #if SPL_POL_ABL & 8
@@ -411,7 +422,7 @@ __device__ __forceinline__ void act_epilogue(const ActArgs &a, const float *row,
 // <false, false> greedy actor, <false, true> sampling actor, <true, true> critic + sampling actor
 // (get_action_and_value), <true, false> critic only (ActorCritic.get_value, ppo_splendor.py:51)
 template <bool kCritic, bool kSample>
-__global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, ActArgs a) {
+__global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict__ W, ActArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
     constexpr bool kActor = kSample || !kCritic;
     constexpr int kTotal = kCritic ? (kActor ? kAllChunks : kCriticChunks) : kActorChunks;
@@ -483,8 +494,8 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         return ring;
 #endif
         // this wave's part of chunk c landed (later chunks' loads may stay outstanding)
-        if (wave < kChunkBlocks - (kBlocksPerWave - 1) * kWaves) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        if (wave < kChunkBlocks - (kBlocksPerWave - 1) * kWaves) __builtin_amdgcn_s_waitcnt(vmcnt_imm(kWaitMost));
+        else __builtin_amdgcn_s_waitcnt(vmcnt_imm(kWaitLast));
         __builtin_amdgcn_s_barrier();  // everyone's part landed; slot c-1 is free
         asm volatile("" ::: "memory");
         const int nxt = c + kSlots - 1 < kTotal ? c + kSlots - 1 : kTotal - 1;  // past the end: harmless reload
@@ -493,7 +504,7 @@ __global__ __launch_bounds__(512) void k_act32(const uint8_t *__restrict__ W, Ac
         ++c;
         return slot;
     };
-    static_assert((kSlots - 2) * kBlocksPerWave == 8 && (kSlots - 2) * (kBlocksPerWave - 1) == 6, "vmcnt immediates");
+    static_assert(kWaitMost <= 63, "vmcnt range");
 
     bf16x8 H1[kPlanes][kKs2];
     float value = 0.f;
