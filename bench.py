@@ -17,7 +17,10 @@ trajectories and write the same per-step outputs (tests/test_gpu_parity.py::test
                   captured HIP graphs of whole refill periods
 The mode not selected is measured too ("other_mode"), and the rollout kernel is measured a second
 time writing every step into the same [T, ...] block ("in_place_l3": that ~81 MB block stays
-resident in the Infinity Cache, so it is NOT an HBM figure and is never the headline).
+resident in the Infinity Cache, so it is NOT an HBM figure and is never the headline).  Two more
+secondary lines: "config5_selfplay" (BASELINE config 5 per GPU: fused fp32 ActorCritic + batched
+dual step with the opponent pool, hipGraph replays) and "config4_share" (BASELINE config 4's
+per-GPU share: 4 players x 32768 tables, the same per-step rollout store, 8 launches timed).
 
 --steps / --warmup are rounded UP to whole plan units (step_plan): a unit is two launches (the
 action buffers alternate) and whole pool-refill periods; "steps" in the JSON line is the number
@@ -239,6 +242,77 @@ def selfplay_line(dev, rank, world, N, iters, warmup):
                        "tables_per_gpu": N, "weights": "reference checkpoint runs/ppo_splendor/ppo_splendor_latest.pt"}}
 
 
+def c4_share_line(dev, rank, world, T, launches, warmup):
+    """BASELINE config 4's per-GPU share (262 144 4-player tables over 8 GPUs = 32 768 per GPU) on
+    this rank: the same per-step rollout store as the headline (spl_rollout, 128 steps per launch,
+    every step's obs/mask/reward/terminated/flags/winner into [128, T, ...]), `launches` launches
+    timed with HIP events around each (after `warmup`), barrier + synchronize around the timed
+    region, max over ranks; roofline bytes as the headline's."""
+    import torch
+    from splendor_gym.device import Engine
+    from splendor_gym.parallel import barrier, max_over_ranks
+    P, K = 4, ROLLOUT_K
+    table0 = rank * T
+    eng = Engine(T, P, device=dev, refill_period=REFILL_EVERY[P], table0=table0)
+    eng.reset(seeds=range(table0, table0 + T))
+    out = dict(obs=torch.zeros((K, T, 297), dtype=torch.int32, device=dev),
+               mask=torch.zeros((K, T, 45), dtype=torch.int8, device=dev),
+               reward=torch.zeros((K, T), dtype=torch.float32, device=dev),
+               terminated=torch.zeros((K, T), dtype=torch.uint8, device=dev),
+               flags=torch.zeros((K, T), dtype=torch.uint8, device=dev),
+               winner=torch.zeros((K, T), dtype=torch.int8, device=dev),
+               final_obs=torch.zeros((K, T, 297), dtype=torch.int32, device=dev))
+    acts = [torch.zeros(T, dtype=torch.int32, device=dev) for _ in range(2)]
+    eng.sample_uniform(out=acts[0], seed=3, ply=0)
+    ep_cnt = torch.zeros(T, dtype=torch.int32, device=dev)
+    ply = 1
+
+    def launch(i):
+        nonlocal ply
+        eng.rollout(K, actions=acts[i & 1], next_actions=acts[(i & 1) ^ 1], policy_seed=3, ply=ply, out=out,
+                    ep_count=ep_cnt)
+        ply += K
+
+    for i in range(warmup):
+        launch(i)
+    strm = torch.cuda.current_stream(dev)
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(launches)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(launches)]
+    for e in ev0 + ev1:  # created on first record, outside the timed region
+        e.record(strm)
+    torch.cuda.synchronize(dev)
+    eps0 = int(ep_cnt.sum().item())
+    barrier(dev)
+    t0 = time.perf_counter()
+    for i in range(launches):
+        ev0[i].record(strm)
+        launch(warmup + i)
+        ev1[i].record(strm)
+    torch.cuda.synchronize(dev)
+    barrier(dev)
+    el = max_over_ranks(time.perf_counter() - t0, device=dev)
+    launch_s = sum(ev0[i].elapsed_time(ev1[i]) for i in range(launches)) / launches / 1e3
+    term = (int(ep_cnt.sum().item()) - eps0) / launches
+    algo = (2 * STATE_BYTES[P] + 8) * T + OUT_BYTES * T * K + OBS_ROW * term
+    name = eng.rollout_kernel_name(per_step=True)
+    traffic, src = load_pmc_traffic(name, T, K)
+    eng.close()
+    achieved = algo / launch_s / 1e9
+    return {"metric": f"env-steps/sec (whole node), 4p {T} tables/GPU (BASELINE config 4's per-GPU share)",
+            "value": round(T * world * K * launches / el, 1), "unit": "env-steps/s",
+            "ms_per_step": round(el / (K * launches) * 1e3, 4), "steps": K * launches, "warmup_launches": warmup,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": name, "steps_per_launch": K,
+                         "kernel_avg_us": round(launch_s * 1e6, 2),
+                         "kernel_timing": f"HIP events around each of {launches} eager launches in the timed region",
+                         "algo_bytes_per_launch": round(algo),
+                         "algo_bytes_note": f"as the headline's, 4 players ({term:.0f} terminal rows per launch)",
+                         "traffic": traffic, "traffic_source": src,
+                         "traffic_over_algo": None if traffic is None else round(traffic / algo, 4)},
+            "config": {"workload": "4-player SplendorEnv.step, device uniform-random policy, same-step autoreset, "
+                                   "per-step rollout store [128, T, ...]", "tables_per_gpu": T, "players": P}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -271,6 +345,8 @@ def main():
     ap.add_argument("--sp-tables", type=int, default=65536,
                     help="tables per GPU of the config-5 self-play line (0 = skip it)")
     ap.add_argument("--sp-iters", type=int, default=64, help="timed dual steps of the config-5 line")
+    ap.add_argument("--c4-tables", type=int, default=32768,
+                    help="tables per GPU of the config-4 share line (4 players; 0 = skip)")
     ap.add_argument("--delegation", type=int, default=0,
                     help="rollout store: every n-th step the odd-XCC workgroups' rows are stored by their "
                          "even-XCC partners (0 = off, the library default: a 1.5 %% gain, "
@@ -452,6 +528,9 @@ def main():
     sp = None
     if args.sp_tables > 0 and not args.only:
         sp = selfplay_line(dev, rank, world, args.sp_tables, args.sp_iters, warmup=8)
+    c4 = None
+    if args.c4_tables > 0 and not args.only and args.players == 2:
+        c4 = c4_share_line(dev, rank, world, args.c4_tables, launches=8, warmup=2)
     # correctness canaries on the measured run: no error flags, episodes completed
     bad = int(((eng.flags & (_native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT)) != 0).sum().item())
     rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
@@ -539,6 +618,8 @@ def main():
             out["in_place_l3" if v == "rollout_inplace" else ("other_mode" if v == "step" else v)] = s
         if sp is not None:
             out["config5_selfplay"] = sp
+        if c4 is not None:
+            out["config4_share"] = c4
         print(json.dumps(out))
     eng.close()
     if world > 1:
