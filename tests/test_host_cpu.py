@@ -74,6 +74,31 @@ def test_policy_abi_host_side_errors():
     args.image = 0
     args.value, args.mode = None, 7
     assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0, 0), 1, ctypes.byref(args), None) == -1
+    # compact rows (policy ABI 3): exclusive with obs, fp32 images only, 4-byte aligned
+    args.mode, args.obs_u8 = 1, 512
+    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0, 0), 1, ctypes.byref(args), None) == -1
+    assert b"exclusive" in lib.spl_last_error()
+    args.obs, args.image = None, 2  # bf16 image
+    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0, 1), 1, ctypes.byref(args), None) == -1
+    assert b"fp32" in lib.spl_last_error()
+    args.image, args.obs_u8 = 0, 514
+    assert lib.spl_policy_act(ctypes.c_void_p(4096), lib.spl_policy_bytes(0, 0), 1, ctypes.byref(args), None) == -1
+    assert b"aligned" in lib.spl_last_error()
+
+
+def test_dual_abi_host_side_errors():
+    """spl_dual_* argument checks (include/splendor_dual.h) run before any launch."""
+    from splendor_gym import _native
+    lib = _native.load_library()
+    io = _native.DualIo()
+    assert lib.spl_dual_finish(0, ctypes.byref(io), None) == -1
+    assert lib.spl_dual_finish(8, ctypes.byref(io), None) == -1 and b"null" in lib.spl_last_error()
+    assert lib.spl_dual_finish_draw(8, ctypes.byref(io), None, None) == -1 and b"draw" in lib.spl_last_error()
+    d = _native.DualDraw(episode=256, group_of=256, pool_len=3, p_current=0.25)  # pool slots missing
+    assert lib.spl_dual_finish_draw(8, ctypes.byref(io), ctypes.byref(d), None) == -1
+    d.pool_slots, d.p_current = 256, 1.5
+    assert lib.spl_dual_finish_draw(8, ctypes.byref(io), ctypes.byref(d), None) == -1
+    assert b"p_current" in lib.spl_last_error()
 
 
 def test_arena_layout_sizes():
