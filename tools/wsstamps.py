@@ -2,6 +2,7 @@
 s_memrealtime stamps (diagnostic build -DSPL_STAMPS; not the product library).
 
     python tools/wsstamps.py [--build-only | --run] [--inplace] [--lib PATH]
+    (WS_P / WS_T: players and tables, default 2 and 65536; 4 x 32768 runs the dealer variant)
 Rules wave stamps per step: 0 start, 1 rules done, 2 hand-off written, 3 past the barrier.
 Output wave: 0 past the barrier, 1 rows encoded (incl. terminal rows), 2 obs stores issued,
 3 mask + small outputs issued.  Medians over workgroups and launches, microseconds.
@@ -21,8 +22,8 @@ import torch
 from splendor_gym import _native
 from splendor_gym.device import Engine
 inplace = sys.argv[2] == "1"
-T, K = 65536, 64
-e = Engine(T, 2, device="cuda:0", refill_period=64)
+T, K, P = int(os.environ.get("WS_T", "65536")), 64, int(os.environ.get("WS_P", "2"))
+e = Engine(T, P, device="cuda:0", refill_period={2: 64, 3: 32, 4: 16}[P])
 e.lib.spl_debug_set_ws_stamps.argtypes = [ctypes.c_void_p]
 e.reset(seeds=range(T))
 buf = [torch.zeros(T, dtype=torch.int32, device=e.device) for _ in range(2)]
