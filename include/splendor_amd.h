@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 5  /* 5: spl_step_args_t.obs_u8 (compact observation) */
+#define SPL_ABI_VERSION 5  /* 5: spl_step_args_t.obs_u8 (compact observation), gate_terminated / gate_flags */
 
 /* ---- per-table flag bits (uint8) --------------------------------------------------- */
 #define SPL_F_ILLEGAL 0x01        /* info["illegal_action"]      envs/splendor_env.py:64-66 */
@@ -112,7 +112,13 @@ typedef struct spl_step_args_s {
                                 device consumer (spl_act_args_t.obs_u8), a quarter of obs's bytes:
                                 bytes 0..296 = obs (every value < 256 but move_count, byte 295 =
                                 move_count mod 256), byte 297 = move_count >> 8, 298-299 = 0.
-                                With obs_u8 set, obs may be NULL (then only the bytes are written) */
+                                With obs_u8 set, obs must be NULL (only the bytes are written)     */
+    const uint8_t *gate_terminated; /* [n] or NULL (spl_step only, with gate_flags): the dual step's
+                                gate fused into the opponent's move — where gate_terminated[t] != 0
+                                or gate_flags[t] has SPL_F_ILLEGAL / SPL_F_OOB (the agent's move
+                                ended the game or was not applied) actions[t] becomes -1 (written
+                                back) and the table is not moved (spl_dual_gate + spl_step) */
+    const uint8_t *gate_flags;
 } spl_step_args_t;
 
 int spl_abi_version(void);

@@ -61,6 +61,7 @@ struct KStep {
     uint32_t *ep_count;
     uint8_t *info;             // nullable: [4][n] info planes + truncated (spl_step)
     uint8_t *obs_u8;           // nullable: [n][300] compact observation instead of obs (k_step_ws)
+    const uint8_t *gate_terminated, *gate_flags;  // nullable: the dual step's gate (spl_step_args_t)
     unsigned long long *errors;  // nullable: running count of tables with an error flag (spl_step)
     const uint64_t *ply_base;  // nullable: device counter added to `ply` (graph replays)
     uint64_t policy_seed;
@@ -1576,6 +1577,18 @@ __device__ __forceinline__ void store_final_rows(const uint8_t *rows_lds, uint64
     }
 }
 
+// spl_step_args_t.gate_*: the dual step's opponent moves only where the agent's move was applied
+// and left the game running (wrappers/dual_step_native.py:120-140, spl_dual_gate); elsewhere its
+// action becomes -1 (out of range: no move), written back so the caller sees the gated action.
+__device__ __forceinline__ int gated_action(const KStep &S, int t) {
+    int action = S.actions[t];
+    if (S.gate_terminated && (S.gate_terminated[t] != 0 || (S.gate_flags[t] & (SPL_F_ILLEGAL | SPL_F_OOB)) != 0)) {
+        action = -1;
+        const_cast<int32_t *>(S.actions)[t] = -1;
+    }
+    return action;
+}
+
 // spl_step's gymnasium info planes (illegal_action, draw, turn_limit as 0/1 bytes; truncated = 0) and the running
 // count of tables whose flags carry the reference's exceptions (out-of-range action, step after
 // termination): one atomic per wave that has any.  Wave-uniform call (the ballot).
@@ -1627,7 +1640,7 @@ __global__ __launch_bounds__(64 * W) void k_step(KArena A, KTables Tb, KStep S) 
     Deal pool = empty_deal();
     if (valid && !abl(ABL_LOAD)) {
         load_tab(T, A, t);
-        action = S.actions[t];
+        action = gated_action(S, t);
         if (S.autoreset) pool = load_pool(A, t);
     } else {
         fresh_state(T, 0u, empty_deal());
@@ -1983,7 +1996,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         Deal pool = empty_deal();
         if (valid) {
             load_tab(T, A, t);
-            action = S.actions[t];
+            action = gated_action(S, t);
             if (S.autoreset) pool = load_pool(A, t);
         } else {
             fresh_state(T, 0u, empty_deal());
@@ -3335,6 +3348,7 @@ static int check_step_args(const spl_step_args_t *a) {
         return fail(SPL_E_ARG, "actions/obs/mask/reward/terminated/flags are required");
     if (a->obs && a->obs_u8) return fail(SPL_E_ARG, "obs and obs_u8 are exclusive");
     if ((uintptr_t)a->obs_u8 & 15u) return fail(SPL_E_ARG, "obs_u8 must be 16-byte aligned");
+    if (!a->gate_terminated != !a->gate_flags) return fail(SPL_E_ARG, "gate_terminated and gate_flags go together");
     if (a->autoreset < 0 || a->autoreset > 2) return fail(SPL_E_ARG, "autoreset must be 0, 1 or 2");
     if (a->policy < SPL_POLICY_UNIFORM || a->policy > SPL_POLICY_BASIC_PRIORITY) return fail(SPL_E_ARG, "unknown policy");
     if (((uintptr_t)a->obs & 15u) || (a->final_obs && ((uintptr_t)a->final_obs & 3u)))
@@ -3358,6 +3372,8 @@ static KStep kstep(const spl_step_args_t *a) {
     S.ep_count = a->ep_count;
     S.info = a->info;
     S.obs_u8 = a->obs_u8;
+    S.gate_terminated = a->gate_terminated;
+    S.gate_flags = a->gate_flags;
     S.errors = reinterpret_cast<unsigned long long *>(a->errors);
     S.ply_base = a->ply_base;
     S.policy_seed = a->policy_seed;
@@ -3428,6 +3444,7 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     if (int r = check_arena(ctx, arena)) return r;
     if (int r = check_step_args(a)) return r;
     if (!a->obs) return fail(SPL_E_ARG, "spl_rollout writes int32 obs (obs_u8 is spl_step only)");
+    if (a->gate_terminated || a->gate_flags) return fail(SPL_E_ARG, "the gate is spl_step only");
     if (steps < 1) return fail(SPL_E_ARG, "spl_rollout: steps must be >= 1");
     if (per_step_outputs && (arena->n & 3))
         return fail(SPL_E_ARG, "spl_rollout: per-step outputs need a table count divisible by 4 (16-byte obs blocks)");

@@ -37,7 +37,7 @@ class StepArgs(ctypes.Structure):
                 ("final_obs", c_void_p), ("autoreset", c_int32), ("policy", c_int32), ("next_actions", c_void_p),
                 ("ply_base", c_void_p), ("policy_seed", c_uint64), ("ply", c_uint64), ("table0", c_int64),
                 ("ep_return", c_void_p), ("ep_count", c_void_p), ("info", c_void_p), ("errors", c_void_p),
-                ("obs_u8", c_void_p)]
+                ("obs_u8", c_void_p), ("gate_terminated", c_void_p), ("gate_flags", c_void_p)]
 
 
 class MlpDesc(ctypes.Structure):

@@ -176,14 +176,17 @@ class Engine:
         return self.obs, self.mask
 
     def step(self, actions=None, autoreset=True, final_obs=True, next_actions=None, policy_seed=0, ply=0,
-             ep_return=None, ep_count=None, ply_base=None, policy=0, small=None, obs_u8=None):
+             ep_return=None, ep_count=None, ply_base=None, policy=0, small=None, obs_u8=None, gate=None):
         """One env step on every table (SplendorEnv.step semantics per table).  autoreset: False,
         True (same-step autoreset) or 2 (also re-deal tables terminal on entry, without a move).
         next_actions (optional int32 tensor) receives `policy`'s action (_native.POLICY_*) over
         the new state.  small: optional (reward, terminated, flags, winner) tensors that receive
         those outputs instead of self.reward/terminated/flags/winner.  obs_u8: optional uint8
         [n, 300] tensor that receives the compact observation (spl_step_args_t.obs_u8) INSTEAD of
-        self.obs (a device policy's input at a quarter of the bytes; self.obs is left as it was)."""
+        self.obs (a device policy's input at a quarter of the bytes; self.obs is left as it was).
+        gate: optional (terminated, flags) uint8 tensors of the agent's move in a dual step — tables
+        where it ended the game or was not applied get action -1 (written into `actions`) and are not
+        moved (spl_step_args_t.gate_*; spl_dual_gate fused into this launch)."""
         torch = self.torch
         if actions is None:
             actions = self.actions
@@ -217,6 +220,8 @@ class Engine:
         a.ply = int(ply) & (2**64 - 1)
         a.ep_return = None if ep_return is None else ep_return.data_ptr()
         a.ep_count = None if ep_count is None else ep_count.data_ptr()
+        a.gate_terminated = None if gate is None else gate[0].data_ptr()
+        a.gate_flags = None if gate is None else gate[1].data_ptr()
         if torch.cuda.current_device() == self.device.index:
             check(self.lib, self.lib.spl_step(self.ctx, ctypes.byref(self.desc), ctypes.byref(a), self.stream()))
         else:

@@ -127,7 +127,8 @@ class DualStepVectorEnv:
 
     def dual_step(self, actions):
         """wrappers/dual_step_native.py:90-193 on every table: spl_step (agent) -> opponent
-        actions -> spl_dual_gate -> spl_step (opponent, autoreset 2) -> spl_dual_finish."""
+        actions -> spl_step (opponent, autoreset 2, gated by the agent's move in the same launch) ->
+        spl_dual_finish."""
         e, lib = self.eng, self.eng.lib
         device_opp = isinstance(self.opponent, str)
         self._ply += 1
@@ -150,10 +151,10 @@ class DualStepVectorEnv:
             self._opp_keep = opp
         stream = e.stream()
         with torch.cuda.device(self.device):
-            # -1 (out of range: no move) where the agent's move was not applied or ended the game
-            _native.check(lib, lib.spl_dual_gate(self.num_envs, ta.data_ptr(), fa.data_ptr(), opp.data_ptr(), stream))
-            # phase B: the opponent's move; autoreset 2 also re-deals tables that ended on the agent's move
-            e.step(opp, autoreset=2, final_obs=True)
+            # phase B: the opponent's move, gated in the same launch (-1, no move, where the agent's move
+            # was not applied or ended the game); autoreset 2 also re-deals the tables that ended on
+            # the agent's move
+            e.step(opp, autoreset=2, final_obs=True, gate=(ta, fa))
             io = self._io
             io.opp_obs = self.opp_obs.data_ptr() if self.want_opp_obs else None
             if self.pool is not None:  # finish + the finished tables' next-opponent draw, one launch

@@ -484,7 +484,7 @@ def test_dual_step_vector_env_matches_per_env_wrappers():
 
 
 def test_dual_step_callable_opponent_and_illegal_actions():
-    """The callable-opponent path (spl_dual_gate / spl_dual_finish around two spl_step launches)
+    """The callable-opponent path (two spl_step launches, the second gated, then spl_dual_finish)
     equals the fused device-opponent path table for table, including illegal and out-of-range
     agent actions: those leave the table unchanged, the opponent does not move, and info reports
     illegal_action with the -0.01 step reward (envs/splendor_env.py:62-66)."""
@@ -591,3 +591,45 @@ def test_device_scripted_policies(orc, policy):
                                if len(legal[(legal >= lo) & (legal <= hi)]))
             assert got[i] in allowed, (k, i, got[i], allowed)
         e.sample_uniform(out=a, seed=11, ply=k)  # keep the tables moving with uniform play
+
+
+def test_fused_gate_equals_spl_dual_gate():
+    """spl_step_args_t.gate_* (the dual step's gate inside the opponent's spl_step) equals
+    spl_dual_gate followed by a plain spl_step: the same gated actions written back, the same
+    outputs and table states, with ended, illegal and out-of-range agent moves mixed in."""
+    import ctypes
+    import torch
+    from splendor_gym import _native
+    n, seed = 1000, 21
+    a, b = engine(n, 2), engine(n, 2)
+    a.reset(seeds=range(seed, seed + n))
+    b.reset(seeds=range(seed, seed + n))
+    dev = a.device
+    rs = np.random.default_rng(4)
+    z = lambda dt: torch.zeros(n, dtype=dt, device=dev)
+    small_a, small_b = (z(torch.float32), z(torch.uint8), z(torch.uint8), z(torch.int8)), \
+        (z(torch.float32), z(torch.uint8), z(torch.uint8), z(torch.int8))
+    gated = 0
+    for k in range(80):
+        mask = a.mask.cpu().numpy()
+        acts = [int(rs.choice(np.flatnonzero(m))) if m.any() and rs.random() > 0.1 else int(rs.integers(-2, 50))
+                for m in mask]
+        act = torch.tensor(acts, dtype=torch.int32, device=dev)
+        a.step(act, autoreset=False, final_obs=False, small=small_a)
+        b.step(act.clone(), autoreset=False, final_obs=False, small=small_b)
+        opp = torch.tensor([int(rs.choice(np.flatnonzero(m))) if m.any() else 0 for m in a.mask.cpu().numpy()],
+                           dtype=torch.int32, device=dev)
+        oa, ob = opp.clone(), opp.clone()
+        with torch.cuda.device(dev):
+            _native.check(b.lib, b.lib.spl_dual_gate(n, small_b[1].data_ptr(), small_b[2].data_ptr(), ob.data_ptr(),
+                                                     b.stream()))
+        b.step(ob, autoreset=2, final_obs=True)
+        a.step(oa, autoreset=2, final_obs=True, gate=(small_a[1], small_a[2]))
+        assert torch.equal(oa, ob), k
+        gated += int((oa == -1).sum())
+        for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), (k, name)
+        term = a.terminated.bool()
+        assert torch.equal(a.final_obs[term], b.final_obs[term]), k
+    assert a.download().tobytes() == b.download().tobytes()
+    assert gated > 100
