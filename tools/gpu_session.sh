@@ -3,7 +3,7 @@
 # the chain stops at the first failure.
 #   tools/gpu_session.sh TAG step [step ...]
 # steps: tests steptests smoke driver prof deleg profc4 pmcc4 multi pmc2p pmcmulti pmcstep stamps selfplay spprof
-#        poolsize vec policy stepmode rank2 bench
+#        poolsize vec policy stepmode rank2 bench poltests abl32
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -70,6 +70,11 @@ for step in "$@"; do
          run prof_vec 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_vec_$TAG -o run -- python3 tools/bench_vec_step.py
          cp $O/prof_vec_$TAG/run_kernel_stats.csv $O/kernel_stats_vec_$TAG.csv; head -6 $O/kernel_stats_vec_$TAG.csv | cut -c1-200 ;;
     policy) run policy 300 python tools/bench_policy.py --iters 20 ;;
+    poltests)  # the actor, pool, compact-row and dual-step GPU tests
+      run pytest_pol 500 python -u -m pytest tests/test_gpu_policy.py tests/test_gpu_opponent_pool.py \
+          tests/test_gpu_compact_obs.py tests/test_gpu_headline.py tests/test_gpu_parity.py tests/test_wrappers.py \
+          -x -v --timeout 200 --timeout-method thread ;;
+    abl32) bash tools/ablate_policy32.sh || exit 1 ;;  # k_act32 timing ablations (BUILD=1 here first)
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
