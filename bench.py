@@ -235,7 +235,8 @@ def selfplay_line(dev, rank, world, N, iters, warmup):
     env.close()
     return {"metric": f"env-steps/sec (whole node), 2p self-play, on-device fp32 ActorCritic, {N} tables/GPU",
             "value": round(2 * N * world * iters / el, 1), "unit": "env-steps/s",
-            "ms_per_dual_step": round(el / iters * 1e3, 4), "iters": iters, "dtype": "fp32",
+            "ms_per_dual_step": round(el / iters * 1e3, 4), "iters": iters,
+            "dtype": "fp32 (fp32 operands as three bf16 planes, six plane products accumulated in fp32; torch fp32 tolerance 1e-5)",
             "config": {"workload": "BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused, fp32-accurate split-bf16 MFMA) + "
                                    "DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of 12 frozen "
                                    "snapshots per episode, greedy), reset after done; hipGraph replays",

@@ -135,7 +135,7 @@ def main():
             "metric": f"env-steps/sec (whole node), 2p self-play with on-device ActorCritic actor, {N} tables/GPU",
             "value": round(steps / full, 1), "unit": "env-steps/s", "n_gpus": world, "iters": args.iters,
             "ms_per_dual_step": round(full / args.iters * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-            "dtype": "bf16" if args.bf16 else "fp32", "data": ("synthetic: seeded deals; ActorCritic weights from the reference checkpoint "
+            "dtype": "bf16" if args.bf16 else "fp32 (three bf16 planes per operand, fp32 accumulation)", "data": ("synthetic: seeded deals; ActorCritic weights from the reference checkpoint "
                      "runs/ppo_splendor/ppo_splendor_latest.pt (agent, opponent, every pool snapshot)"
                      if args.weights == "trained" else "synthetic: seeded deals, random-init ActorCritic"),
             "config": {"workload": "PPO rollout step: ActorCritic.get_action_and_value + DualStepVectorEnv.dual_step "
