@@ -172,6 +172,20 @@ constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 // that would pay for a cross-XCC hand-off in the headline kernel
 #define SPL_DELEG_EVERY 0
 #endif
+#ifndef SPL_XCD_MAP
+#define SPL_XCD_MAP 1
+#endif
+// Workgroup -> 64-table block, XCD-contiguous.  The dispatcher hands workgroup b to XCD b % 8, so
+// with the identity map every XCD writes every eighth 76 KB chunk of a step's rollout-store block;
+// mapped, XCD x's workgroups own tables [x n/8, (x+1) n/8) and each XCD streams one contiguous eighth
+// of the block (store-only pattern: 880 -> 844-862 us per 64 steps on one box,
+// tools/microbench_hbm_store.hip rows_x).  Only which workgroup steps which tables changes: every
+// table's chain is its own, so results are identical (A/B build switch SPL_XCD_MAP=0).
+__device__ __forceinline__ int wg_block() {
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    if (!SPL_XCD_MAP || (nb & 7u)) return (int)b;
+    return (int)((b & 7u) * (nb >> 3) + (b >> 3));
+}
 #ifndef SPL_STEP_OBS_NT
 #define SPL_STEP_OBS_NT false  // k_step_ws observation stores non-temporal (A/B switch)
 #endif
@@ -1982,7 +1996,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
     constexpr int kW = StepWsLDS<P>::kW;
     const int lane = lane_id();
     const bool rules_wave = threadIdx.x < 64;
-    const int t0 = blockIdx.x * 64;
+    const int t0 = wg_block() * 64;
     const int t = t0 + lane;
     const bool valid = t < A.n;
     const int rows = min(64, A.n - t0);
@@ -2405,7 +2419,9 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
     constexpr int kW = WsLDS<P>::kW;
     const int lane = lane_id();
     const bool rules_wave = threadIdx.x < 64;
-    const int t0 = blockIdx.x * TPW;
+    // delegation pairs neighbouring workgroups (blockIdx b and b + 1 on adjacent XCCs): identity map
+    const bool deleg_shape = TPW == 64 && kStore && !kDealer && deleg_every >= 4;
+    const int t0 = (deleg_shape ? (int)blockIdx.x : wg_block()) * TPW;
     const int t = t0 + lane;
     const bool valid = lane < TPW && t < A.n;
     const int rows = min(TPW, A.n - t0);
@@ -2545,7 +2561,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
 #endif
         // delegation: both workgroups of a full pair take part (the same test on both sides)
         Deleg dl{false, false, (int)(blockIdx.x >> 1), deleg_every, 0u};
-        if (TPW == 64 && kStore && !kDealer && deleg_every >= 4 && (int)(blockIdx.x | 1u) * 64 + 64 <= A.n) {
+        if (deleg_shape && (int)(blockIdx.x | 1u) * 64 + 64 <= A.n) {
             dl.on = true;
             dl.producer = (blockIdx.x & 1u) != 0;
             uint32_t *ep = A.dflags + (size_t)dl.pair * kDelegFlagWords + (dl.producer ? DF_PROD_EPOCH : DF_CONS_EPOCH) * kFlagLine;

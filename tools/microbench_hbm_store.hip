@@ -101,6 +101,27 @@ __global__ __launch_bounds__(256) void k_rows_r(v4i *out, v4i *mask, int T, int 
     }
 }
 
+// XCD-aware placement of the same [K][T] rows: the dispatcher hands workgroup b to XCD b % 8, so
+// wave b writes block slot (b % 8) * (nw / 8) + b / 8 — each XCD's waves then cover one contiguous
+// eighth of every step's 78 MB block instead of every eighth 76 KB chunk
+template <bool NT, int R>
+__global__ __launch_bounds__(64) void k_rows_x(v4i *out, int T, int K) {
+    constexpr int RV4 = R * OBS / 4;
+    const int lane = threadIdx.x;
+    const size_t nw = gridDim.x;
+    const size_t wave = (blockIdx.x % 8) * (nw / 8) + blockIdx.x / 8;
+    const size_t blk = (size_t)T * OBS / 4;
+    for (int k = 0; k < K; ++k) {
+        v4i *dst = out + (size_t)k * blk + wave * RV4;
+        int d = lane;
+        for (; d + 64 * 4 < RV4; d += 64 * 5) {
+#pragma unroll
+            for (int u = 0; u < 5; ++u) st<NT>(dst + d + 64 * u, v4i{k, d, u, 0});
+        }
+        for (; d < RV4; d += 64) st<NT>(dst + d, v4i{k, d, 0, 0});
+    }
+}
+
 // read + write copy (the guide's 6.29 TB/s float4 copy)
 __global__ __launch_bounds__(256) void k_copy(const v4i *in, v4i *out, size_t n4) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x)
@@ -156,6 +177,11 @@ int main() {
     rep("rows_r R=32 2 waves/WG (2048 waves)", timeit([&] { k_rows_r<false, 32, false><<<nb, 128>>>(out, mk, T, K); }, 5), bytes);
     rep("rows_r R=32 NT 1 wave/WG", timeit([&] { k_rows_r<true, 32, false><<<2 * nb, 64>>>(out, mk, T, K); }, 5), bytes);
     rep("rows_r R=16 1 wave/WG (4096 waves)", timeit([&] { k_rows_r<false, 16, false><<<4 * nb, 64>>>(out, mk, T, K); }, 5), bytes);
+    rep("rows_x R=64 XCD-contiguous (1024 waves)", timeit([&] { k_rows_x<false, 64><<<nb, 64>>>(out, T, K); }, 5), bytes);
+    rep("rows_x R=64 XCD-contiguous NT", timeit([&] { k_rows_x<true, 64><<<nb, 64>>>(out, T, K); }, 5), bytes);
+    rep("rows_x R=32 XCD-contiguous (2048 waves)", timeit([&] { k_rows_x<false, 32><<<2 * nb, 64>>>(out, T, K); }, 5), bytes);
+    rep("rows_r R=64 1 wave/WG again (same-box A/B)", timeit([&] { k_rows_r<false, 64, false><<<nb, 64>>>(out, mk, T, K); }, 5), bytes);
+    rep("rows_x R=64 XCD-contiguous again", timeit([&] { k_rows_x<false, 64><<<nb, 64>>>(out, T, K); }, 5), bytes);
     const double mb = bytes + (double)K * T * 45;
     rep("rows_r R=64 + mask stream", timeit([&] { k_rows_r<false, 64, true><<<nb, 64>>>(out, mk, T, K); }, 5), mb);
     rep("rows_r R=64 + mask stream NT", timeit([&] { k_rows_r<true, 64, true><<<nb, 64>>>(out, mk, T, K); }, 5), mb);
