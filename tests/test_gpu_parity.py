@@ -119,6 +119,61 @@ def test_trajectories_c2_2000_plies(orc):
     assert resets > 4096 * 2000 // 90  # ~one episode per 77 plies per table
 
 
+@pytest.mark.parametrize("n", [984, 1000, 520, 4104])
+def test_xcd_map_ragged_grids(orc, n):
+    """The XCD-contiguous workgroup map (spl_engine.hip wg_block) on grids whose workgroup
+    count is a multiple of 8 with a partial last block (984, 1000: 16 workgroups, the last one 24 / 40
+    tables; 4104: 72 workgroups at 32 tables per workgroup) and on one that is not (520: 9 workgroups,
+    identity map): every ply of k_step_ws bit-compared with the oracle, then a 48-step rollout store
+    launch (each rollout kernel shape: auto, two-wave at 64 and 32 tables per workgroup, dealer)
+    against the same chain of steps replayed by the oracle."""
+    import torch
+    run_parity(orc, 2, n, 40, 8, 77 + n, True, check_state_every=20)
+    for pipeline in (True, "always", "half", "dealer"):
+        e = engine(n, 2, refill_period=16, pipeline=pipeline)
+        seeds = [5 + i for i in range(n)]
+        e.reset(seeds=seeds)
+        vec = OracleVec(orc, n, 2, seeds)
+        a = torch.zeros(n, dtype=torch.int32, device=e.device)
+        e.sample_uniform(out=a, seed=3, ply=0)
+        K = 48
+        out = {"obs": torch.empty((K, n, 297), dtype=torch.int32, device=e.device),
+               "mask": torch.empty((K, n, 45), dtype=torch.int8, device=e.device),
+               "reward": torch.empty((K, n), dtype=torch.float32, device=e.device),
+               "terminated": torch.empty((K, n), dtype=torch.uint8, device=e.device),
+               "flags": torch.empty((K, n), dtype=torch.uint8, device=e.device),
+               "winner": torch.empty((K, n), dtype=torch.int8, device=e.device),
+               "final_obs": torch.zeros((K, n, 297), dtype=torch.int32, device=e.device)}
+        acts = torch.empty((K, n), dtype=torch.int32, device=e.device)
+        # the actions each step takes are the previous step's next_actions: record them by re-running
+        # the device policy stream through a step chain on a twin engine
+        twin = engine(n, 2, refill_period=16)
+        twin.reset(seeds=seeds)
+        ta = a.clone()
+        for k in range(K):
+            acts[k] = ta
+            na = torch.empty_like(ta)
+            twin.step(ta, next_actions=na, policy_seed=3, ply=1 + k)
+            ta = na
+        na = torch.empty_like(a)
+        e.rollout(K, actions=a, next_actions=na, policy_seed=3, ply=1, out=out)
+        assert torch.equal(na, ta), pipeline
+        A = acts.cpu().numpy()
+        for k in range(K):
+            ref = vec.step(A[k], want_final=True)
+            np.testing.assert_array_equal(out["obs"][k].cpu().numpy(), ref["obs"], err_msg=f"{pipeline} obs {k}")
+            np.testing.assert_array_equal(bits_of(out["mask"][k].cpu().numpy()), ref["mask"],
+                                          err_msg=f"{pipeline} mask {k}")
+            np.testing.assert_array_equal(out["reward"][k].cpu().numpy(), ref["reward"], err_msg=f"{pipeline} rew {k}")
+            np.testing.assert_array_equal(out["terminated"][k].cpu().numpy(), ref["terminated"])
+            rows = np.flatnonzero(ref["terminated"])
+            if len(rows):
+                np.testing.assert_array_equal(out["final_obs"][k].cpu().numpy()[rows], ref["final_obs"][rows])
+        recs = e.download()
+        for t in range(n):
+            assert canon(table_to_view(recs[t])) == canon(vec.table(t)), (pipeline, t)
+
+
 @pytest.mark.parametrize("P", [3, 4])
 def test_trajectories_multiplayer(orc, P):
     resets = run_parity(orc, P, 1024, 200, 8, 99 * P, False)
