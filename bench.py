@@ -133,14 +133,38 @@ def _cpu_leg(players, procs, steps_per_proc):
     return (sum(r[0] for r in res), wall, sum(r[0] / r[1] for r in res) / len(res), sum(r[2] for r in res))
 
 
+def cgroup_cpu_quota():
+    """CPUs the cgroup CPU quota grants this process (cgroup v2 /sys/fs/cgroup/cpu.max "quota period",
+    or v1 cpu.cfs_quota_us / cpu.cfs_period_us), with the file it came from; (None, source) when the
+    quota is unlimited or not readable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return (None if q == "max" else int(q) / int(per)), "/sys/fs/cgroup/cpu.max: " + q + " " + per
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return (None if q <= 0 else q / per), f"/sys/fs/cgroup/cpu/cpu.cfs_quota_us: {q} / {per}"
+    except (OSError, ValueError):
+        return None, "no cgroup cpu quota file"
+
+
 def cpu_share():
-    """CPUs this process may use: the affinity set, capped at the 16 CPUs a one-GPU box grants per
-    GPU (os.cpu_count() and the affinity set show the whole host there)."""
+    """(processes to run, affinity CPUs, quota CPUs or None, how the count was chosen): the cgroup CPU
+    quota when one is set, else the affinity set capped at the 16 CPUs a one-GPU box grants per GPU
+    (os.cpu_count() and the affinity set show the whole host there)."""
     try:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count() or 1
-    return min(16, aff), aff
+    quota, src = cgroup_cpu_quota()
+    if quota is not None:
+        return max(1, min(aff, int(quota))), aff, quota, f"cgroup quota ({src})"
+    return min(16, aff), aff, None, f"affinity set capped at 16 ({src}: unlimited or absent)"
 
 
 def cpu_baseline(players, procs, steps_per_proc):
@@ -149,16 +173,26 @@ def cpu_baseline(players, procs, steps_per_proc):
     leg (`procs` processes, one per core of the box's share)."""
     n1, w1, _, _ = _cpu_leg(players, 1, steps_per_proc)
     n, wall, per_core, eps = _cpu_leg(players, procs, steps_per_proc)
-    _, aff = cpu_share()
+    _, aff, quota, how = cpu_share()
     return {"value": round(n / wall, 1), "unit": "env-steps/s", "cores": procs, "kind": "port",
             "one_core": round(n1 / w1, 1), "per_core_mean_all_core_leg": round(per_core, 1),
-            "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+            "os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cgroup_quota_cpus": quota, "cores_source": how,
             "sample": (f"C oracle (port of engine/rules.py + envs/splendor_env.py step), {players}p, 1 env per "
                        f"process, uniform-random legal policy with autoreset: all-core leg {procs} processes x "
                        f"{steps_per_proc} env steps ({eps} episodes) = value; 1-core leg 1 process x "
-                       f"{steps_per_proc} steps = one_core.  cores = the box's CPU share (16 per GPU; "
-                       "os_cpu_count is the whole host's).  Reference Python engine: 5.4k steps/s/core, "
+                       f"{steps_per_proc} steps = one_core.  cores = processes run (cores_source says how the "
+                       "count was chosen; os_cpu_count is the whole host's).  Reference Python engine: 5.4k steps/s/core, "
                        "SURVEY.md §6")}
+
+
+def launch_spread(times):
+    """min / median / max / mean of per-launch times (seconds) -> microseconds, and the median in s."""
+    xs = sorted(times)
+    n = len(xs)
+    med = xs[n // 2] if n % 2 else 0.5 * (xs[n // 2 - 1] + xs[n // 2])
+    return {"median_s": med, "us": {"min": round(xs[0] * 1e6, 2), "median": round(med * 1e6, 2),
+                                    "max": round(xs[-1] * 1e6, 2), "mean": round(sum(xs) / n * 1e6, 2),
+                                    "launches": n}}
 
 
 def load_pmc_traffic(kernel, tables, steps_per_launch):
@@ -250,6 +284,7 @@ def c4_share_line(dev, rank, world, T, launches, warmup):
     timed with HIP events around each (after `warmup`), barrier + synchronize around the timed
     region, max over ranks; roofline bytes as the headline's."""
     import torch
+    from splendor_gym import _native
     from splendor_gym.device import Engine
     from splendor_gym.parallel import barrier, max_over_ranks
     P, K = 4, ROLLOUT_K
@@ -292,24 +327,31 @@ def c4_share_line(dev, rank, world, T, launches, warmup):
     torch.cuda.synchronize(dev)
     barrier(dev)
     el = max_over_ranks(time.perf_counter() - t0, device=dev)
-    launch_s = sum(ev0[i].elapsed_time(ev1[i]) for i in range(launches)) / launches / 1e3
+    times = [ev0[i].elapsed_time(ev1[i]) / 1e3 for i in range(launches)]
+    launch_s = sum(times) / launches
+    spread = launch_spread(times)
     term = (int(ep_cnt.sum().item()) - eps0) / launches
     algo = (2 * STATE_BYTES[P] + 8) * T + OUT_BYTES * T * K + OBS_ROW * term
     name = eng.rollout_kernel_name(per_step=True)
     traffic, src = load_pmc_traffic(name, T, K)
+    # the dealer kernel's hand-off faults (spl_ctx_faults) and error flags of the last launch's steps
+    faults = eng.faults()
+    bad = int(((out["flags"] & (_native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_FAULT)) != 0).sum().item())
     eng.close()
-    achieved = algo / launch_s / 1e9
+    achieved = algo / spread["median_s"] / 1e9
     return {"metric": f"env-steps/sec (whole node), 4p {T} tables/GPU (BASELINE config 4's per-GPU share)",
             "value": round(T * world * K * launches / el, 1), "unit": "env-steps/s",
             "ms_per_step": round(el / (K * launches) * 1e3, 4), "steps": K * launches, "warmup_launches": warmup,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": name, "steps_per_launch": K,
-                         "kernel_avg_us": round(launch_s * 1e6, 2),
-                         "kernel_timing": f"HIP events around each of {launches} eager launches in the timed region",
+                         "kernel_avg_us": round(launch_s * 1e6, 2), "kernel_us": spread["us"],
+                         "kernel_timing": f"HIP events around each of {launches} eager launches in the timed region; "
+                                          "frac from the median launch",
                          "algo_bytes_per_launch": round(algo),
                          "algo_bytes_note": f"as the headline's, 4 players ({term:.0f} terminal rows per launch)",
                          "traffic": traffic, "traffic_source": src,
                          "traffic_over_algo": None if traffic is None else round(traffic / algo, 4)},
+            "error_flags": bad, "launch_faults": faults,
             "config": {"workload": "4-player SplendorEnv.step, device uniform-random policy, same-step autoreset, "
                                    "per-step rollout store [128, T, ...]", "tables_per_gpu": T, "players": P}}
 
@@ -323,7 +365,7 @@ def main():
     ap.add_argument("--players", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = the cgroup CPU quota, else min(16, affinity CPUs)")
     ap.add_argument("--cpu-steps", type=int, default=1_000_000, help="env steps per CPU process")
     ap.add_argument("--graph-steps", type=int, default=128,
                     help="step mode: steps per captured HIP graph (rounded to whole plan units); 0 = eager")
@@ -504,7 +546,8 @@ def main():
             # inter-kernel gaps included); HIP events around each launch of an eager window of the
             # same loop, right after the timed replays, are reported beside it (they also bracket
             # the host dispatch latency of a ~20 us kernel).
-            launch_s = sum(ev[0][i].elapsed_time(ev[1][i]) for i in range(len(ev[0]))) / (K // per) / 1e3
+            times = [ev[0][i].elapsed_time(ev[1][i]) / 1e3 / (G // per) for i in range(len(ev[0]))]
+            launch_s = sum(times) / len(times)
             kt = f"HIP events around each of {K // G} hipGraph replays ({G // per} launches each) in the timed region"
             nwin = plan["unit"] * max(1, -(-64 // plan["unit"]))
             ev = events(nwin // per)
@@ -514,8 +557,9 @@ def main():
             eager_s = sum(ev[0][i].elapsed_time(ev[1][i]) for i in range(len(ev[0]))) / len(ev[0]) / 1e3
             k_next += nwin + 1
         else:
-            launch_s = sum(ev[0][i].elapsed_time(ev[1][i]) for i in range(len(ev[0]))) / len(ev[0]) / 1e3
-        return {"variant": variant, "plan": plan, "elapsed": elapsed, "launch_s": launch_s, "how": how,
+            times = [ev[0][i].elapsed_time(ev[1][i]) / 1e3 for i in range(len(ev[0]))]
+            launch_s = sum(times) / len(times)
+        return {"variant": variant, "plan": plan, "elapsed": elapsed, "launch_s": launch_s, "times": times, "how": how,
                 "kernel_timing": kt, "terminations": terminations, "k_next": k_next, "eager_s": eager_s}
 
     headline = "step" if args.mode == "step" else ("rollout_store" if args.outputs == "store" else "rollout_inplace")
@@ -533,7 +577,11 @@ def main():
     if args.c4_tables > 0 and not args.only and args.players == 2:
         c4 = c4_share_line(dev, rank, world, args.c4_tables, launches=8, warmup=2)
     # correctness canaries on the measured run: no error flags, episodes completed
-    bad = int(((eng.flags & (_native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT)) != 0).sum().item())
+    errs = _native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT | _native.F_FAULT
+    bad = int(((eng.flags & errs) != 0).sum().item())
+    if store is not None:  # every step of the last rollout-store launch
+        bad += int(((store["flags"] & errs) != 0).sum().item())
+    faults = eng.faults()
     rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
     episodes = int(cnts.sum().item())
 
@@ -557,15 +605,25 @@ def main():
             algo_note = (f"2*S_P/{per} + {OUT_BYTES} B per table-step (obs 1188 + mask 45 + reward 4 + terminated/flags/"
                          f"winner 3) + 8 B/table of actions per launch + 1188 B per terminal row "
                          f"({term_per_launch:.0f} per launch, counted in the timed region)")
-        achieved = algo / rec["launch_s"] / 1e9
+        spread = launch_spread(rec["times"])
+        achieved = algo / spread["median_s"] / 1e9  # frac from the median launch
+        if v == "rollout_inplace":
+            # every step overwrites one ~81 MB block that stays in the 256 MiB Infinity Cache: not an
+            # HBM figure, so no HBM fraction
+            bound = {"bound": "l3", "achieved": round(achieved, 1), "peak": None, "unit": "GB/s", "frac": None,
+                     "bound_note": "L3-resident output block (MALL): achieved is algorithmic bytes / median launch, "
+                                   "no HBM fraction"}
+        else:
+            bound = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "frac_of_achievable": round(achieved / HBM_ACHIEVABLE_GBS, 4)}
         return {"variant": v, "value": round(T * world * K / rec["elapsed"], 1),
                 "steps": K, "ms_per_step": round(rec["elapsed"] / K * 1e3, 4),
-                "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(achieved / HBM_PEAK_GBS, 4),
-                             "frac_of_achievable": round(achieved / HBM_ACHIEVABLE_GBS, 4),
+                "roofline": {**bound,
                              "kernel": kernel_name(v), "steps_per_launch": per,
                              "kernel_avg_us": round(rec["launch_s"] * 1e6, 2),
-                             "kernel_timing": rec["kernel_timing"],
+                             "kernel_us": spread["us"],
+                             "kernel_timing": rec["kernel_timing"] + "; frac from the median launch",
                              **({} if rec["eager_s"] is None else
                                 {"eager_launch_us": round(rec["eager_s"] * 1e6, 2)}),
                              "algo_bytes_per_launch": round(algo),
@@ -612,6 +670,7 @@ def main():
             "episodes": episodes,
             "mean_final_reward_p0": round(float(rets.sum().item()) / max(1, episodes), 4),
             "error_flags": bad,
+            "launch_faults": faults,
         }
         for v in variants[1:]:
             s = with_traffic(summary(recs[v]))

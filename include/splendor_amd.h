@@ -44,7 +44,8 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 5  /* 5: spl_step_args_t.obs_u8 (compact observation), gate_terminated / gate_flags */
+#define SPL_ABI_VERSION 6  /* 6: SPL_F_FAULT + spl_ctx_faults (a lost hand-off in a rollout launch is reported);
+                              5: spl_step_args_t.obs_u8 (compact observation), gate_terminated / gate_flags */
 
 /* ---- per-table flag bits (uint8) --------------------------------------------------- */
 #define SPL_F_ILLEGAL 0x01        /* info["illegal_action"]      envs/splendor_env.py:64-66 */
@@ -55,6 +56,8 @@ extern "C" {
 #define SPL_F_RESET 0x20          /* autoreset: obs/mask describe the freshly dealt table   */
 #define SPL_F_RNG_LIMIT 0x40      /* reserved (ABI 2 raised it when a deal or token return   */
                                   /* outran the MT stream; ABI 3 continues the stream instead) */
+#define SPL_F_FAULT 0x80          /* the launch faulted (a lost internal hand-off, spl_ctx_faults):  */
+                                  /* this step's outputs of the table were NOT written (stale rows) */
 
 /* ---- device policies for next_actions (scripts/eval_suite.py opponents) --------------- */
 #define SPL_POLICY_UNIFORM 0         /* uniform over legal (wrappers/selfplay.py:66-73 random_opponent) */
@@ -156,6 +159,20 @@ int spl_ctx_set_rollout_delegation(spl_ctx_t *ctx, int every);
  * of its own, so a rocprofv3 summary row maps to one variant.  NULL (spl_last_error) on bad input. */
 const char *spl_rollout_kernel_name(spl_ctx_t *ctx, int32_t n, int32_t players, int32_t per_step_outputs);
 
+/* Launch faults.  A spl_rollout launch of the three-wave dealer variant whose waves hand off through
+ * LDS counters bounds every wait; a wait that runs out (a lost hand-off: never in a correct run) stops
+ * that workgroup — it stores no more steps and leaves its tables' state as it was, marks SPL_F_FAULT in
+ * the flags of every step it did not store — and writes the launch's serial (spl_ctx_launches at the
+ * time of the call) into the context's fault word.  The word lives in host-mapped memory the kernel
+ * writes through to, so reading it needs no synchronisation: it shows the faults of every launch that
+ * has finished (and of running ones as they happen).  After a fault the tables must be reset.
+ * spl_ctx_faults: *launch = the word (0 = no fault since the last clear); `clear` zeroes it.
+ * spl_ctx_fault_word: the word's host address, for polling without a call (valid until destroy).
+ * spl_ctx_launches: kernel launches through this context so far (spl_step / spl_rollout serials). */
+int spl_ctx_faults(spl_ctx_t *ctx, uint64_t *launch, int clear);
+const volatile uint64_t *spl_ctx_fault_word(spl_ctx_t *ctx);
+uint64_t spl_ctx_launches(spl_ctx_t *ctx);
+
 int64_t spl_arena_bytes(int32_t n, int32_t players);
 /* Zero the arena and mark every table's pool as not dealt (must precede the first spl_reset
  * of a fresh allocation).  A table that was never reset with a seed has no engine-seed stream:
@@ -222,6 +239,11 @@ int spl_table_upload(spl_ctx_t *ctx, spl_arena_t *arena, int32_t first, int32_t 
  * process-wide, current device).  Results are identical for every value: the parity tests lower it
  * to drive every deal and token return through the continuation. */
 int spl_debug_set_stream_limit(int outputs);
+
+/* TEST HOOK: polls after which a dealer-rollout hand-off wait gives up and faults the launch (see
+ * spl_ctx_faults; default and maximum 2^22, a fraction of a second; negative = default).  Process-wide,
+ * current device.  0 makes the first wait that has to wait fault: tests force the fault path with it. */
+int spl_debug_set_spin_limit(int64_t polls);
 
 /* TEST HOOK of the bounds-check build (libsplendor_amd_checked.so, -DSPL_BOUNDS_CHECK): the OR of the
  * invariant violations the kernels recorded (table / slot / deck / token-table / deal-scratch index,

@@ -64,6 +64,8 @@ struct KStep {
     const uint8_t *gate_terminated, *gate_flags;  // nullable: the dual step's gate (spl_step_args_t)
     unsigned long long *errors;  // nullable: running count of tables with an error flag (spl_step)
     const uint64_t *ply_base;  // nullable: device counter added to `ply` (graph replays)
+    uint64_t *fault;           // nullable: the context's host-mapped fault word (spl_ctx_faults)
+    uint64_t fault_tag;        // what a faulting launch writes there (the context's launch serial)
     uint64_t policy_seed;
     uint64_t ply;
     int64_t table0;
@@ -2275,41 +2277,61 @@ __device__ __forceinline__ void lds_publish(uint32_t *p, uint32_t v) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     if (lane_id() == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// Every wait is bounded (~2^22 polls, a fraction of a second; a legitimate wait is one deal, ~0.1 ms):
-// a lost hand-off would corrupt results (and set BC_SPIN in a bounds-check build) rather than leave
-// waves spinning on the GPU, and once one wait has run out the workgroup's later waits return at once.
+// Every wait is bounded (~2^22 polls, a fraction of a second; a legitimate wait is one deal, ~0.1 ms)
+// so that a lost hand-off never leaves waves spinning on the GPU.  A wait that runs out FAULTS the
+// workgroup, loudly, in every build (round 4; was a silent abort in the release library):
+//   * it sets the workgroup's abort word, so every later wait of the three waves returns false at once;
+//   * the rules wave stops stepping and leaves its tables' state unstored, the output wave stops storing
+//     and marks SPL_F_FAULT in the flags of every step it did not store, the dealer stops dealing —
+//     nothing reads or writes through an index taken from an unsettled hand-off;
+//   * the launch's serial goes into the context's host-mapped fault word (signal_fault), which
+//     spl_ctx_faults reads without synchronising (Engine / SplendorVectorEnv / bench.py raise on it).
+// spl_debug_set_spin_limit lowers the limit so a test can force the path (BC_SPIN still marks it in
+// the bounds-check build).
 constexpr uint32_t kSpinLimit = 1u << 22;
-__device__ __forceinline__ void lds_wait_ge(DealerLDS &D, const uint32_t *p, uint32_t v) {
+__device__ uint32_t g_spin_limit = kSpinLimit;
+__device__ __forceinline__ void signal_fault(const KStep &S) {
+    if (S.fault && lane_id() == 0)  // a vector store (system scope: write-through to the host-mapped word)
+        __hip_atomic_store(S.fault, S.fault_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// true once *p >= v; false when the wait ran out or another wave of the workgroup already faulted
+__device__ __forceinline__ bool lds_wait_ge(DealerLDS &D, const uint32_t *p, uint32_t v) {
+    const uint32_t limit = g_spin_limit;
     for (uint32_t spins = 0; lds_poll(p) < v; ++spins) {
-        if (spins > kSpinLimit || lds_poll(&D.abort)) {
+        if (spins >= limit || lds_poll(&D.abort)) {
             SPL_CHECK(false, BC_SPIN);
             if (lane_id() == 0) __hip_atomic_store(&D.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            break;
+            return false;
         }
         __builtin_amdgcn_s_sleep(1);
     }
+    return true;
 }
 __device__ __forceinline__ Deal deal_of_lds(const DealerLDS &D, int lane) {
     return Deal{{D.rdeal[0][lane], D.rdeal[1][lane], D.rdeal[2][lane]}, D.rdeal[3][lane], D.rdeal[4][lane]};
 }
 
-// The dealer wave: batches until the rules wave stops and none is left.
+// The dealer wave: batches until the rules wave stops and none is left.  An idle wait that runs out
+// ends the dealer quietly: a batch posted after that is never dealt, so the rules wave's wait for it
+// runs out and faults the launch (lds_wait_ge).  A faulted workgroup's dealer ends after its batch.
 template <int P>
 __device__ __forceinline__ void dealer_loop(DealerLDS &D, const KArena &A, int t0) {
     const int lane = lane_id();
+    const uint32_t limit = g_spin_limit;
     uint32_t done = 0;
     for (;;) {
         uint32_t req;
         for (uint32_t spins = 0;; ++spins) {
+            if (lds_poll(&D.abort)) return;
             req = lds_poll(&D.dreq);
             if (req != done || lds_poll(&D.stop)) break;
-            if (spins > kSpinLimit || lds_poll(&D.abort)) {
+            if (spins >= limit) {
                 SPL_CHECK(false, BC_SPIN);
                 break;
             }
             __builtin_amdgcn_s_sleep(4);
         }
-        if (req == done) break;  // stopped, nothing pending
+        if (req == done) break;  // stopped (or idle too long), nothing pending
         const int slot = D.rq[lane];
         const int t = t0 + lane;
         if (slot != 0xFF) {
@@ -2336,9 +2358,10 @@ __device__ __forceinline__ void dealer_post(DealerLDS &D, bool want, int slot, u
 // The rules wave's side of the dealer after step_rules (wave-uniform call): settle a finished
 // batch, make sure every table that ended has its next record dealt (waiting for the batch in
 // flight, or posting one for a spent pool), run the same-step autoreset (flip_to_pool without its
-// inline deal), then post a new batch when the dealer is idle.
+// inline deal), then post a new batch when the dealer is idle.  False: a wait for the dealer faulted
+// (lds_wait_ge) and T / pool were left as they were, not filled from an unsettled batch.
 template <int P>
-__device__ __forceinline__ void dealer_step(DealerLDS &D, Tab<P> &T, const KArena &A, int t, bool valid, bool ends,
+__device__ __forceinline__ bool dealer_step(DealerLDS &D, Tab<P> &T, const KArena &A, int t, bool valid, bool ends,
                                             bool autoreset, Deal &pool, bool &pool_dirty, uint32_t &my_req,
                                             uint32_t &infl, bool &pool_stale, StepOut &o) {
     constexpr int kPools = kSlotRecords - 1;
@@ -2360,7 +2383,7 @@ __device__ __forceinline__ void dealer_step(DealerLDS &D, Tab<P> &T, const KAren
     const bool blocked = ends && !spent && (((infl >> nxt) & 1u) != 0u || pool_stale);
     if (__any(spent || blocked)) {
         if (!idle) {
-            lds_wait_ge(D, &D.ddone, my_req);
+            if (!lds_wait_ge(D, &D.ddone, my_req)) return false;
             settle();
             idle = true;
         }
@@ -2371,7 +2394,7 @@ __device__ __forceinline__ void dealer_step(DealerLDS &D, Tab<P> &T, const KAren
                 misc = (misc & ~ST_PEND) | ((uint32_t)pend << ST_PEND_SHIFT);
                 pool_stale = true;
             }
-            lds_wait_ge(D, &D.ddone, my_req);
+            if (!lds_wait_ge(D, &D.ddone, my_req)) return false;
             settle();
         }
     }
@@ -2401,6 +2424,7 @@ __device__ __forceinline__ void dealer_step(DealerLDS &D, Tab<P> &T, const KAren
             if (pend == kPools) pool_stale = true;  // the next record itself is being dealt
         }
     }
+    return true;
 }
 
 // TPW = tables per workgroup: 64, or 32 for grids too small to give every SIMD a wave (e.g. the
@@ -2453,6 +2477,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         // outstanding) and whether `pool` still lacks the next record's words
         uint32_t my_req = 0, infl = 0;
         bool pool_stale = false;
+        bool faulted = false;  // a dealer hand-off ran out (wave-uniform): stop, store nothing more
         Tab<P> T;
         int action = 0;
         Deal pool = empty_deal();
@@ -2476,7 +2501,10 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             const size_t blk = per_step ? (size_t)k * (size_t)A.n : 0;
             WSSTAMP(0, k);
             if constexpr (kDealer) {
-                if (k >= 2) lds_wait_ge(L.dl, &L.dl.odone, (uint32_t)(k - 1));  // slot b: step k-2 is stored
+                if (k >= 2 && !lds_wait_ge(L.dl, &L.dl.odone, (uint32_t)(k - 1))) {  // slot b: step k-2 is stored
+                    faulted = true;
+                    break;
+                }
             }
             // token-return continuation (LaneMT) in this step's free state slot
 #ifdef SPL_STAMPS
@@ -2502,8 +2530,11 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             }
             const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;  // per termination, as k_step
             if constexpr (kDealer) {
-                dealer_step<P>(L.dl, T, A, t, valid, valid && o.term && S.autoreset, S.autoreset != 0, pool, pool_dirty,
-                               my_req, infl, pool_stale, o);
+                if (!dealer_step<P>(L.dl, T, A, t, valid, valid && o.term && S.autoreset, S.autoreset != 0, pool,
+                                    pool_dirty, my_req, infl, pool_stale, o)) {
+                    faulted = true;
+                    break;
+                }
             } else {
                 if (valid && o.term && S.autoreset)
                     autoreset_table(T, A, t, pool, L.scratch(b, lane), L.deal_mtx(b), o, pool_dirty);
@@ -2528,10 +2559,14 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         }
         if constexpr (kDealer) {  // no more batches; the last one lands before the state is stored
             lds_publish(&L.dl.stop, 1u);
-            lds_wait_ge(L.dl, &L.dl.ddone, my_req);
-            if (pool_stale) {
+            if (!faulted && !lds_wait_ge(L.dl, &L.dl.ddone, my_req)) faulted = true;
+            if (pool_stale && !faulted) {
                 pool = deal_of_lds(L.dl, lane);
                 pool_dirty = true;
+            }
+            if (faulted) {  // the tables' state is not stored: the host sees the fault and resets
+                signal_fault(S);
+                return;
             }
         }
 #ifdef SPL_STAMPS
@@ -2576,7 +2611,13 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         uint32_t staged = 0u;        // producer: tasks staged (not stored here)
         for (int k = 0; k < K; ++k) {
             if constexpr (kDealer) {
-                lds_wait_ge(L.dl, &L.dl.rdone, (uint32_t)(k + 1));  // hand-off of step k
+                if (!lds_wait_ge(L.dl, &L.dl.rdone, (uint32_t)(k + 1))) {  // hand-off of step k
+                    // steps k.. are not stored: their flags say so (the blocks keep stale rows)
+                    for (int j = per_step ? k : 0; j < K && (per_step || j == 0); ++j)
+                        if (valid) S.flags[(per_step ? (size_t)j * (size_t)A.n : 0) + t] = (uint8_t)SPL_F_FAULT;
+                    signal_fault(S);
+                    return;
+                }
             } else {
                 ws_sync();  // hand-off of step k
             }
@@ -3066,6 +3107,9 @@ struct spl_ctx_s {
     int ws_resident[5];  // k_rollout_store_<P>p: workgroups resident per device (occupancy x CUs), index P
     int dealer_resident[5];  // k_rollout_store_dealer_<P>p: the same for the three-wave dealer variant
     int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
+    uint64_t *fault_host;  // host-mapped, fine-grained: the serial of a launch that faulted (0 = none), spl_ctx_faults
+    uint64_t *fault_dev;   // its device address (KStep::fault)
+    uint64_t launches;     // launch serial (KStep::fault_tag)
     void *stage;
     size_t stage_bytes;
 };
@@ -3174,6 +3218,13 @@ int spl_debug_set_stream_limit(int outputs) {
     return SPL_OK;
 }
 
+int spl_debug_set_spin_limit(int64_t polls) {
+    if (polls > (int64_t)kSpinLimit) return fail(SPL_E_ARG, "spin limit must be <= 2^22 (negative = default)");
+    const uint32_t v = polls < 0 ? kSpinLimit : (uint32_t)polls;
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_spin_limit), &v, sizeof(v)));
+    return SPL_OK;
+}
+
 const char *spl_last_error(void) { return g_err.c_str(); }
 
 int64_t spl_arena_bytes(int32_t n, int32_t players) {
@@ -3243,6 +3294,15 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         spl_ctx_destroy(c);
         return fail(SPL_E_HIP, "hipMalloc of constant tables failed");
     }
+    // the fault word: host memory the kernels write through to (fine-grained), so the host reads a
+    // launch's fault without synchronising the stream
+    if (hipHostMalloc(reinterpret_cast<void **>(&c->fault_host), sizeof(uint64_t),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void **>(&c->fault_dev), c->fault_host, 0) != hipSuccess) {
+        spl_ctx_destroy(c);
+        return fail(SPL_E_HIP, "hipHostMalloc of the fault word failed");
+    }
+    *c->fault_host = 0;
     HIP_TRY(hipMemcpy(c->cards, crec.data(), sizeof(uint4) * 90, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->nobles, nrec.data(), sizeof(uint2) * 10, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(k_build_lut, dim3(blocks_for(kLutEntries)), dim3(64), 0, 0, c->lut);
@@ -3261,9 +3321,28 @@ int spl_ctx_destroy(spl_ctx_t *ctx) {
     if (ctx->nobles) (void)hipFree(ctx->nobles);
     if (ctx->lut) (void)hipFree(ctx->lut);
     if (ctx->stage) (void)hipFree(ctx->stage);
+    if (ctx->fault_host) (void)hipHostFree(ctx->fault_host);
     delete ctx;
     return SPL_OK;
 }
+
+int spl_ctx_faults(spl_ctx_t *ctx, uint64_t *launch, int clear) {
+    if (!ctx || !launch) return fail(SPL_E_ARG, "null argument");
+    volatile uint64_t *w = ctx->fault_host;
+    *launch = *w;
+    if (clear) *w = 0;
+    return SPL_OK;
+}
+
+const volatile uint64_t *spl_ctx_fault_word(spl_ctx_t *ctx) {
+    if (!ctx) {
+        fail(SPL_E_ARG, "null ctx");
+        return nullptr;
+    }
+    return ctx->fault_host;
+}
+
+uint64_t spl_ctx_launches(spl_ctx_t *ctx) { return ctx ? ctx->launches : 0; }
 
 int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period) {
     if (!ctx || period < 0) return fail(SPL_E_ARG, "bad refill period");
@@ -3373,8 +3452,10 @@ static int check_step_args(const spl_step_args_t *a) {
     return SPL_OK;
 }
 
-static KStep kstep(const spl_step_args_t *a) {
+static KStep kstep(spl_ctx_t *ctx, const spl_step_args_t *a) {
     KStep S;
+    S.fault = ctx->fault_dev;
+    S.fault_tag = ++ctx->launches;
     S.actions = a->actions;
     S.obs = a->obs;
     S.mask = a->mask;
@@ -3404,7 +3485,7 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     if (int r = check_arena(ctx, arena)) return r;
     if (int r = check_step_args(a)) return r;
     if (a->obs_u8 && !kStepWs) return fail(SPL_E_ARG, "obs_u8 needs the two-wave step kernel");
-    const KStep S = kstep(a);
+    const KStep S = kstep(ctx, a);
     const KArena A = karena(arena);
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (kStepWs) {
@@ -3464,7 +3545,7 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     if (steps < 1) return fail(SPL_E_ARG, "spl_rollout: steps must be >= 1");
     if (per_step_outputs && (arena->n & 3))
         return fail(SPL_E_ARG, "spl_rollout: per-step outputs need a table count divisible by 4 (16-byte obs blocks)");
-    const KStep S = kstep(a);
+    const KStep S = kstep(ctx, a);
     const KArena A = karena(arena);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t before = arena->steps;

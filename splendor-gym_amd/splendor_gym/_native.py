@@ -10,12 +10,13 @@ import os
 import numpy as np
 
 LIB_NAME = "libsplendor_amd.so"
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # per-table flag bits (include/splendor_amd.h)
 POLICY_UNIFORM, POLICY_GREEDY_V1, POLICY_BASIC_PRIORITY = 0, 1, 2  # SPL_POLICY_* (device next_actions)
 F_ILLEGAL, F_DRAW, F_TURN_LIMIT = 0x01, 0x02, 0x04
 F_AFTER_TERMINAL, F_OOB, F_RESET, F_RNG_LIMIT = 0x08, 0x10, 0x20, 0x40
+F_FAULT = 0x80  # SPL_F_FAULT: the launch faulted (spl_ctx_faults), this step was not written
 
 OBS_DIM = 297
 OBS_U8 = 300  # spl_step_args_t.obs_u8 row: the 297 observation bytes, move_count >> 8, two zero bytes
@@ -97,6 +98,10 @@ SIGNATURES = {
     "spl_ctx_set_rollout_pipeline": ([c_void_p, c_int32], c_int32),
     "spl_ctx_set_rollout_delegation": ([c_void_p, c_int32], c_int32),
     "spl_ctx_token_lut": ([c_void_p, c_void_p, c_int64], c_int64),
+    "spl_ctx_faults": ([c_void_p, ctypes.POINTER(c_uint64), c_int32], c_int32),
+    "spl_ctx_fault_word": ([c_void_p], c_void_p),
+    "spl_ctx_launches": ([c_void_p], c_uint64),
+    "spl_debug_set_spin_limit": ([c_int64], c_int32),
     "spl_rollout_kernel_name": ([c_void_p, c_int32, c_int32, c_int32], ctypes.c_char_p),
     "spl_arena_bytes": ([c_int32, c_int32], c_int64),
     "spl_arena_init": ([c_void_p, ctypes.POINTER(ArenaDesc), c_void_p], c_int32),
@@ -173,6 +178,11 @@ def check(lib, code):
     if code < 0:
         raise NativeError(f"splendor engine error {code}: {lib.spl_last_error().decode()}")
     return code
+
+
+class LaunchFault(RuntimeError):
+    """A launch lost an internal hand-off (include/splendor_amd.h spl_ctx_faults): its outputs from
+    the faulted step on are not written (SPL_F_FAULT) and the tables must be reset."""
 
 
 def require_gpu():

@@ -9,7 +9,7 @@ import ctypes
 import numpy as np
 
 from . import _native
-from ._native import NUM_ACTIONS, OBS_DIM, OBS_U8, TABLE_DTYPE, ArenaDesc, StepArgs, check, ptr
+from ._native import NUM_ACTIONS, OBS_DIM, OBS_U8, TABLE_DTYPE, ArenaDesc, LaunchFault, StepArgs, check, ptr
 from .engine.state import load_tables
 from .seeding import pcg64_states
 
@@ -46,6 +46,7 @@ class Engine:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self._settings = (refill_period, refill_fused, pipeline, delegation)
         self.ctx = None
+        self._fault_carry = 0  # a fault seen on a context replaced by set_card_table
         self._create_ctx(cards)
         nbytes = int(self.lib.spl_arena_bytes(self.n, self.P))
         dev = self.device
@@ -85,6 +86,8 @@ class Engine:
             check(self.lib, self.lib.spl_ctx_create(self.device.index, tbl.ctypes.data, nobles.ctypes.data,
                                                     ctypes.byref(ctx)))
         self.ctx = ctx
+        # the context's fault word (host-mapped; the kernels write a faulting launch's serial there)
+        self._fault_word = ctypes.c_uint64.from_address(self.lib.spl_ctx_fault_word(ctx))
         self.custom_cards = None if cards is None else tbl.copy()
         refill_period, refill_fused, pipeline, delegation = self._settings
         num_players = self.P
@@ -110,10 +113,32 @@ class Engine:
             return
         self.torch.cuda.synchronize(self.device)
         old = self.ctx
+        self._fault_carry = self.faults()
         self._create_ctx(cards)
         self.lib.spl_ctx_destroy(old)
 
     # ------------------------------------------------------------------------------------
+    def faults(self):
+        """Serial of a launch that faulted since the last clear_faults() (0 = none): a lost internal
+        hand-off in a dealer-variant rollout (include/splendor_amd.h spl_ctx_faults).  Reads the
+        host-mapped fault word: no synchronisation, covers every launch that has finished."""
+        return self._fault_carry or int(self._fault_word.value)
+
+    def check_faults(self):
+        """Raise LaunchFault if a launch of this engine faulted (no synchronisation)."""
+        f = self.faults()
+        if f:
+            raise LaunchFault(f"splendor engine: launch {f} lost an internal hand-off; its outputs from the faulted "
+                              "step on are not written (flags carry SPL_F_FAULT) and the tables' state is undefined: "
+                              "reset the tables, then clear_faults()")
+
+    def clear_faults(self):
+        """Wait for this engine's work, then zero its fault word."""
+        self.torch.cuda.synchronize(self.device)
+        self._fault_carry = 0
+        f = ctypes.c_uint64()
+        check(self.lib, self.lib.spl_ctx_faults(self.ctx, ctypes.byref(f), 1))
+
     def stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -236,7 +261,9 @@ class Engine:
         (spl_rollout): the same trajectory as `steps` calls of step() with next_actions fed back
         and ply, ply+1, ...  out=None overwrites self.obs/mask/... each step; otherwise `out` is a
         dict of [steps, n, ...] tensors (obs, mask, reward, terminated, flags, winner, final_obs)
-        that receives every step's outputs (rollout storage)."""
+        that receives every step's outputs (rollout storage).  Raises LaunchFault when an earlier
+        launch faulted (check_faults; a rollout's own fault shows at the next call or check)."""
+        self.check_faults()
         torch = self.torch
         actions = self.actions if actions is None else actions
         if not (isinstance(actions, torch.Tensor) and actions.device == self.device and actions.dtype == torch.int32
@@ -299,12 +326,13 @@ class Engine:
 
     # ------------------------------------------------------------------------------------
     def download(self, first=0, count=None):
-        """numpy TABLE_DTYPE[count] host views (synchronous)."""
+        """numpy TABLE_DTYPE[count] host views (synchronous; raises LaunchFault after a faulted launch)."""
         count = self.n - first if count is None else count
         out = np.zeros(count, TABLE_DTYPE)
         with self.torch.cuda.device(self.device):
             check(self.lib, self.lib.spl_table_download(self.ctx, ctypes.byref(self.desc), first, count,
                                                         out.ctypes.data, self.stream()))
+        self.check_faults()
         return out
 
     def upload(self, records, first=0):

@@ -65,14 +65,16 @@ class SplendorEnv(Env):
     def reset(self, *, seed: Optional[int] = None, options: Optional[Dict[str, Any]] = None):
         super().reset(seed=seed)
         eng = self._engine()
+        # a new game deals fresh, canonical cards (state.py:183-184): drop the previous episode's
+        # edited card table BEFORE the reset kernel encodes the first obs and mask from it
+        self._cards = {}
+        eng.set_card_table(None)
         if seed is not None or not self._seeded:  # gymnasium: reseed, or first reset from entropy
             eng.reset(seeds=[seed])
             self._seeded = True
         else:                                     # continue this env's np_random stream
             eng.reset(seeds=None)
         self._view = None
-        self._cards = {}  # this episode's Card objects (a new game deals fresh, canonical cards)
-        eng.set_card_table(None)
         obs, mask = self._fetch()
         self._terminal = False
         self.current_player = int(obs[294])

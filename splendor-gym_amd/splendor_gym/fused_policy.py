@@ -22,6 +22,7 @@ accumulation, logits to bf16 accuracy.  Call ``refresh()`` after the module's we
 after each PPO update).
 """
 import ctypes
+import weakref
 
 from . import _native
 from ._native import (ACT_GREEDY, ACT_SAMPLE, ACT_VALUE, IMG_CRITIC, NUM_ACTIONS, OBS_DIM, OBS_U8, PREC_BF16, PREC_FP32, ActArgs, MlpDesc,
@@ -174,9 +175,14 @@ class OpponentPool:
     envs using the pool are tracked: DualStepVectorEnv registers its own), so episodes already
     playing it finish against it, as the reference's per-episode frozen copies do; add_snapshot
     writes the next ring slot that no pool member and no running episode uses, growing the ring
-    (up to 64 images) when every slot is busy.  (The reference appends agent.state_dict(), whose
+    (up to MAX_IMAGES) when every slot is busy.  The image ring and the grouping scratch are allocated
+    at their maximum size up front, so growing never moves them: memory a hipGraph captured stays valid
+    across add_snapshot (a graph holding act() bakes in the group count: re-capture it after the ring
+    grows).  (The reference appends agent.state_dict(), whose
     tensors alias the live parameters, so its "frozen" pool entries are the current weights at the
     episode's start; add_snapshot here copies the weights at the time it is called.)"""
+
+    MAX_IMAGES = 64
 
     def __init__(self, agent, pool_size: int = 12, p_current: float = 0.25, seed: int = 0, device=None):
         torch = _native.require_gpu()
@@ -187,37 +193,46 @@ class OpponentPool:
         self.device = torch.device(device) if device is not None else next(agent.parameters()).device
         self.image_bytes = int(self.lib.spl_policy_bytes(0, PREC_FP32))
         self.n_images = 1 + self.pool_size + 2
-        if self.n_images > 64:
-            raise ValueError("pool_size at most 61")
-        self.images = torch.zeros(self.n_images * self.image_bytes, dtype=torch.uint8, device=self.device)
+        if self.n_images > self.MAX_IMAGES:
+            raise ValueError(f"pool_size at most {self.MAX_IMAGES - 3}")
+        # every image slot the ring can ever grow to (~1 MB each): never reallocated (see the class doc)
+        self.images = torch.zeros(self.MAX_IMAGES * self.image_bytes, dtype=torch.uint8, device=self.device)
         self.pool = []                      # image slots in pool order (oldest first)
         self._next = 0                      # ring position of the next snapshot slot
         self.slots = torch.zeros(max(1, self.pool_size), dtype=torch.int32, device=self.device)
         self._scratch = None
         self._keep = []
-        self._users = []  # per-table image-slot tensors of the envs playing this pool (track())
+        self._users = []  # weak references to the per-table image-slot tensors of the envs playing this pool
         self.refresh()
 
     def track(self, group_of):
         """Register a per-table opponent tensor (image slot per table): add_snapshot never overwrites
-        a slot that one of its tables still plays."""
-        self._users.append(group_of)
+        a slot that one of its tables still plays.  Held weakly: an env that is dropped (or closed,
+        untrack) stops reserving its slots."""
+        self._users.append(weakref.ref(group_of))
+
+    def untrack(self, group_of):
+        """Stop reserving the slots of a tensor registered with track() (DualStepVectorEnv.close)."""
+        self._users = [r for r in self._users if r() is not None and r() is not group_of]
 
     def _in_use(self):
         used = set()
-        for g in self._users:
+        alive = []
+        for r in self._users:
+            g = r()
+            if g is None:
+                continue
+            alive.append(r)
             used.update(int(x) for x in self.torch.unique(g).tolist())
+        self._users = alive
         return used
 
     def _grow(self):
-        """One more image slot (the ring is full of snapshots still in play)."""
-        if self.n_images >= 64:
-            raise RuntimeError("OpponentPool: every one of the 64 image slots is in play; add snapshots less often "
-                               "than episodes end")
-        t = self.torch
-        bigger = t.zeros((self.n_images + 1) * self.image_bytes, dtype=t.uint8, device=self.device)
-        bigger[:self.images.numel()].copy_(self.images)
-        self.images = bigger
+        """One more image slot (the ring is full of snapshots still in play); the buffer is already
+        allocated at MAX_IMAGES, so nothing moves."""
+        if self.n_images >= self.MAX_IMAGES:
+            raise RuntimeError(f"OpponentPool: every one of the {self.MAX_IMAGES} image slots is in play; add "
+                               "snapshots less often than episodes end")
         self.n_images += 1
         return self.n_images - 1
 
@@ -280,9 +295,15 @@ class OpponentPool:
         if (obs.dtype not in (t.int32, t.uint8) or obs.shape[1] != (OBS_U8 if u8 else OBS_DIM) or not obs.is_contiguous()
                 or mask.dtype != t.int8 or not mask.is_contiguous()):
             raise ValueError("obs int32 [n, 297] (or uint8 [n, 300] compact rows) and mask int8 [n, 45], contiguous")
-        nbytes = int(self.lib.spl_policy_group_scratch_bytes(n, self.n_images))
+        # sized for every image the ring can hold, so growing the ring never reallocates it; its layout
+        # follows the group count, so a grown ring re-zeroes it once (the counters must start at zero)
+        nbytes = int(self.lib.spl_policy_group_scratch_bytes(n, self.MAX_IMAGES))
         if self._scratch is None or self._scratch.numel() < nbytes:  # zero-filled once (spl_policy_act_grouped)
             self._scratch = t.zeros(nbytes, dtype=t.uint8, device=self.device)
+            self._scratch_groups = self.n_images
+        elif self._scratch_groups != self.n_images:
+            self._scratch.zero_()
+            self._scratch_groups = self.n_images
         action = out if out is not None else t.empty(n, dtype=t.int32, device=self.device)
         a = ActArgs(obs=None if u8 else obs.data_ptr(), obs_u8=obs.data_ptr() if u8 else None, mask=mask.data_ptr(),
                     action=action.data_ptr(), logprob=None, entropy=None, value=None, logits=None, seed=0, ply=0,

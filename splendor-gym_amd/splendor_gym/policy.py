@@ -2,7 +2,9 @@
 
 ActorCritic / masked_categorical restate ppo_splendor.py:27-59 (same layers and masking rule);
 greedy_actions restates eval_suite.py:131-141 model_greedy_policy_from for a whole batch.
-Weights here are whatever the caller loads; the benchmark uses random initialisation.
+Weights here are whatever the caller loads; bench.py's config-5 line and tools/bench_selfplay.py load
+the reference checkpoint (runs/ppo_splendor/ppo_splendor_latest.pt, committed as
+tests/golden/ppo_splendor_latest.safetensors).
 """
 import torch
 import torch.nn as nn

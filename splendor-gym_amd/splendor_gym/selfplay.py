@@ -171,4 +171,6 @@ class DualStepVectorEnv:
         return e.obs, self.agent_reward, self.opp_obs, self.opp_reward, self.done, info
 
     def close(self):
+        if self.pool is not None:
+            self.pool.untrack(self.opp_group)
         self.eng.close()

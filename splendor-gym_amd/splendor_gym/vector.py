@@ -131,6 +131,7 @@ class SplendorVectorEnv:
         self._pin = torch.zeros(self.DEFER_RING, dtype=torch.int64).pin_memory() if check_actions == "deferred" else None
         self._events = [torch.cuda.Event() for _ in range(self.DEFER_RING)] if check_actions == "deferred" else None
         self._steps = 0
+        self._qslot = 0  # deferred check: the pinned slot / event the next copy uses (rotating)
         e = self.engine
         self._lib, self._ctx, self._desc = e.lib, e.ctx, ctypes.byref(e.desc)
         self._stream_obj = torch.cuda.current_stream(self.device)
@@ -176,6 +177,7 @@ class SplendorVectorEnv:
         return self._stream
 
     def reset(self, *, seed=None, options=None):
+        self.engine.check_faults()
         if self._unchecked and self.check_actions == "deferred":
             self._queue_check()
         self._raise_pending(block_all=True)
@@ -202,9 +204,11 @@ class SplendorVectorEnv:
     def _queue_check(self):
         """Copy the running error count back asynchronously (deferred mode)."""
         self._unchecked = 0
-        slot = self._steps % self.DEFER_RING
         if len(self._pending) >= self.DEFER_RING - 1:
             self._raise_pending(block_all=True)
+        # a rotating slot: a pending copy's slot is never reused before it is checked (ADVICE r03)
+        slot = self._qslot
+        self._qslot = (slot + 1) % self.DEFER_RING
         self._pin[slot:slot + 1].copy_(self._errors, non_blocking=True)
         self._events[slot].record(self._stream_obj)
         self._pending.append((slot, self._steps))
@@ -249,7 +253,9 @@ class SplendorVectorEnv:
 
     def step(self, actions):
         """One spl_step launch over every table.  copy=True: the returned tensors stay valid until the
-        caller drops them; copy=False: they are the env's buffers, overwritten by the next step."""
+        caller drops them; copy=False: they are the env's buffers, overwritten by the next step.
+        Raises LaunchFault when a launch of the engine faulted (host-mapped fault word, no sync)."""
+        self.engine.check_faults()
         self._raise_pending()
         a, host_checked = self._device_actions(actions)
         b = self._next_block()

@@ -534,8 +534,14 @@ def test_edited_card_cost_through_the_env_and_the_oracle():
     assert after.bank == [4, 5, 4, 5, 4, 6]
     # the edited object stays the episode's card: a later view shows the edited cost wherever it is
     assert all(c.cost == {"red": 2, "blue": 2} for c in after.cards().values() if c.id == card.id)
-    env.reset(seed=31)  # a new game deals canonical cards again
+    obs_r, info_r = env.reset(seed=31)  # a new game deals canonical cards again
     assert env.state.card_table() is None
+    # ... and the reset's own obs/mask come from the canonical table: the edited card
+    # is dealt to the same slot again, so an obs built from the old context would show its edit
+    fresh = SplendorEnv()
+    obs_f, info_f = fresh.reset(seed=31)
+    assert np.array_equal(obs_r, obs_f) and np.array_equal(info_r["action_mask"], info_f["action_mask"])
+    assert np.array_equal(obs_r, obs)
 
 
 STD = ["white", "blue", "green", "red", "black"]

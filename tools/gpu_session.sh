@@ -2,7 +2,7 @@
 # One GPU session (round 3).  Steps by name, run in order; each GPU step has its own time limit and
 # the chain stops at the first failure.
 #   tools/gpu_session.sh TAG step [step ...]
-# steps: tests steptests smoke driver prof deleg profc4 pmcc4 multi pmc2p pmcmulti pmcstep stamps selfplay spprof
+# steps: tests faults steptests smoke driver prof deleg profc4 pmcc4 multi pmc2p pmcmulti pmcstep stamps selfplay spprof
 #        poolsize vec policy stepmode rank2 bench poltests abl32
 set -o pipefail
 TAG=${1:?tag}
@@ -22,6 +22,8 @@ run() {  # run NAME SECONDS CMD... ; output to $O/NAME_$TAG.{out,err}
 for step in "$@"; do
   case $step in
     tests) run pytest_gpu 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread --durations=12 ;;
+    faults) run pytest_faults 400 python -u -m pytest tests/test_gpu_faults.py tests/test_gpu_env_api.py \
+                tests/test_gpu_parity.py -k "fault or dealer or edited or rollout_equals" -x -v --timeout 200 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     driver) run bench_driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof)
