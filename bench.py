@@ -60,6 +60,12 @@ STEP_ALGO_BYTES = {p: 2 * s + 297 * 4 + 45 + 4 + 4 + 1 for p, s in STATE_BYTES.i
 # pool refill period per player count: three pool deals per table must cover the resets between
 # refills (random games last ~77 plies at 2p, ~29 at 4p)
 REFILL_EVERY = {2: 64, 3: 32, 4: 16}
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table; no sparsity)
+# bf16 MFMA work of the fused fp32 ActorCritic (csrc/spl_policy32.hip) per table: every fp32 operand is
+# three bf16 planes; layer 1 (297 -> 256, observation exact in bf16) takes 3 plane products, layers
+# 2 (256 -> 256) and 3 (256 -> 45) take 6; the critic's 256 -> 1 output runs on VALU, not counted
+ACTOR_MFMA_FLOP = 2 * (297 * 256 * 3 + 256 * 256 * 6 + 256 * 45 * 6)   # 1 380 864
+CRITIC_MFMA_FLOP = 2 * (297 * 256 * 3 + 256 * 256 * 6)                 # 1 242 624
 ROLLOUT_K = 128    # env steps per spl_rollout launch = ppo_splendor.py's --num-steps default (:71)
 MIN_TIMED_LAUNCHES = 8  # rollout mode times at least this many launches (>= 16 ms), whatever --steps says
 
@@ -185,6 +191,17 @@ def cpu_baseline(players, procs, steps_per_proc):
                        "SURVEY.md §6")}
 
 
+def region_mark(name, edge, kernel=None, launches=None):
+    """A timed region's edge on stderr as one JSON line with CLOCK_BOOTTIME / CLOCK_MONOTONIC stamps:
+    tools/trace_timed.py picks the region's launches of `kernel` out of a rocprofv3 kernel trace of the
+    same run by these (so a committed profile can be averaged over the timed launches only)."""
+    rec = {"timed_region": name, "edge": edge, "boottime_ns": time.clock_gettime_ns(time.CLOCK_BOOTTIME),
+           "monotonic_ns": time.monotonic_ns()}
+    if kernel is not None:
+        rec.update(kernel=kernel, launches=launches)
+    print(json.dumps(rec), file=sys.stderr, flush=True)
+
+
 def launch_spread(times):
     """min / median / max / mean of per-launch times (seconds) -> microseconds, and the median in s."""
     xs = sorted(times)
@@ -260,24 +277,59 @@ def selfplay_line(dev, rank, world, N, iters, warmup):
     graph.replay()
     torch.cuda.synchronize(dev)
     barrier(dev)
+    region_mark("config5_selfplay", "start")
     t0 = time.perf_counter()
     for _ in range(iters):
         graph.replay()
     torch.cuda.synchronize(dev)
+    region_mark("config5_selfplay", "end")
     barrier(dev)
     el = max_over_ranks(time.perf_counter() - t0, device=dev)
+    # the agent's actor + critic + masked sample (k_act32<true, true>) on its own, eager, HIP events
+    # around each launch on the launch stream: its MFMA roofline
+    strm = torch.cuda.current_stream(dev)
+    n_act = 16
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_act)]
+    for a, b in ev:
+        a.record(strm)
+        b.record(strm)
+    act_out = {"action": torch.empty(N, dtype=torch.int32, device=dev),
+               "logprob": torch.empty(N, dtype=torch.float32, device=dev),
+               "entropy": torch.empty(N, dtype=torch.float32, device=dev),
+               "value": torch.empty(N, 1, dtype=torch.float32, device=dev)}
+    with torch.no_grad():
+        agent_k.act(obs, mask, seed=77, table0=rank * N, out=act_out)
+        torch.cuda.synchronize(dev)
+        region_mark("config5_actor", "start", "k_act32<true, true>", n_act)
+        for i, (a, b) in enumerate(ev):
+            a.record(strm)
+            agent_k.act(obs, mask, seed=77, ply=i, table0=rank * N, out=act_out)
+            b.record(strm)
+        torch.cuda.synchronize(dev)
+        region_mark("config5_actor", "end")
+    spread = launch_spread([a.elapsed_time(b) / 1e3 for a, b in ev])
+    flop = (ACTOR_MFMA_FLOP + CRITIC_MFMA_FLOP) * N
+    tflops = flop / spread["median_s"] / 1e12
     env.close()
     return {"metric": f"env-steps/sec (whole node), 2p self-play, on-device fp32 ActorCritic, {N} tables/GPU",
             "value": round(2 * N * world * iters / el, 1), "unit": "env-steps/s",
             "ms_per_dual_step": round(el / iters * 1e3, 4), "iters": iters,
             "dtype": "fp32 (fp32 operands as three bf16 planes, six plane products accumulated in fp32; torch fp32 tolerance 1e-5)",
+            "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tflops / BF16_MFMA_PEAK_TFLOPS, 4), "kernel": "k_act32<true, true>",
+                         "kernel_us": spread["us"], "flop_per_launch": flop,
+                         "flop_note": "bf16 MFMA work per table: actor 2*(297*256*3 + 256*256*6 + 256*45*6) + critic "
+                                      "2*(297*256*3 + 256*256*6) = 2 623 488 (three bf16 planes per fp32 operand: 3 plane "
+                                      "products in layer 1, 6 in layers 2-3; the critic's 256->1 output on VALU); "
+                                      "frac from the median of 16 eager launches (HIP events on the launch stream)",
+                         "traffic": None},
             "config": {"workload": "BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused, fp32-accurate split-bf16 MFMA) + "
                                    "DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of 12 frozen "
                                    "snapshots per episode, greedy), reset after done; hipGraph replays",
                        "tables_per_gpu": N, "weights": "reference checkpoint runs/ppo_splendor/ppo_splendor_latest.pt"}}
 
 
-def c4_share_line(dev, rank, world, T, launches, warmup):
+def c4_share_line(dev, rank, world, T, launches, warmup, pipeline=True):
     """BASELINE config 4's per-GPU share (262 144 4-player tables over 8 GPUs = 32 768 per GPU) on
     this rank: the same per-step rollout store as the headline (spl_rollout, 128 steps per launch,
     every step's obs/mask/reward/terminated/flags/winner into [128, T, ...]), `launches` launches
@@ -289,7 +341,7 @@ def c4_share_line(dev, rank, world, T, launches, warmup):
     from splendor_gym.parallel import barrier, max_over_ranks
     P, K = 4, ROLLOUT_K
     table0 = rank * T
-    eng = Engine(T, P, device=dev, refill_period=REFILL_EVERY[P], table0=table0)
+    eng = Engine(T, P, device=dev, refill_period=REFILL_EVERY[P], table0=table0, pipeline=pipeline)
     eng.reset(seeds=range(table0, table0 + T))
     out = dict(obs=torch.zeros((K, T, 297), dtype=torch.int32, device=dev),
                mask=torch.zeros((K, T, 45), dtype=torch.int8, device=dev),
@@ -319,12 +371,14 @@ def c4_share_line(dev, rank, world, T, launches, warmup):
     torch.cuda.synchronize(dev)
     eps0 = int(ep_cnt.sum().item())
     barrier(dev)
+    region_mark("config4_share", "start", eng.rollout_kernel_name(per_step=True), launches)
     t0 = time.perf_counter()
     for i in range(launches):
         ev0[i].record(strm)
         launch(warmup + i)
         ev1[i].record(strm)
     torch.cuda.synchronize(dev)
+    region_mark("config4_share", "end")
     barrier(dev)
     el = max_over_ranks(time.perf_counter() - t0, device=dev)
     times = [ev0[i].elapsed_time(ev1[i]) / 1e3 for i in range(launches)]
@@ -382,7 +436,7 @@ def main():
     ap.add_argument("--refill", choices=("fused", "separate"), default="fused",
                     help="rollout mode: due pool refills run inside the spl_rollout launch (fused) or as a "
                          "spl_refill launch after it (step mode always launches spl_refill)")
-    ap.add_argument("--pipeline", choices=("auto", "always", "half", "off"), default="auto",
+    ap.add_argument("--pipeline", choices=("auto", "always", "half", "off", "dealer", "dealer2"), default="auto",
                     help="rollout mode: two-wave pipelined kernel (auto: 32 or 64 tables per workgroup by grid "
                          "size; always: 64; half: 32) vs one wave per 64 tables (off)")
     ap.add_argument("--sp-tables", type=int, default=65536,
@@ -390,6 +444,8 @@ def main():
     ap.add_argument("--sp-iters", type=int, default=64, help="timed dual steps of the config-5 line")
     ap.add_argument("--c4-tables", type=int, default=32768,
                     help="tables per GPU of the config-4 share line (4 players; 0 = skip)")
+    ap.add_argument("--c4-pipeline", default=True, type=lambda v: {"auto": True}.get(v, v),
+                    help="rollout kernel of the config-4 share line: auto (default), dealer, dealer2, always, half")
     ap.add_argument("--delegation", type=int, default=0,
                     help="rollout store: every n-th step the odd-XCC workgroups' rows are stored by their "
                          "even-XCC partners (0 = off, the library default: a 1.5 %% gain, "
@@ -417,7 +473,8 @@ def main():
     R = args.refill_every or REFILL_EVERY[P]
     RK = args.rollout_k
     table0 = rank * T
-    pipe = {"auto": True, "always": "always", "half": "half", "off": False}[args.pipeline]
+    pipe = {"auto": True, "always": "always", "half": "half", "off": False, "dealer": "dealer",
+            "dealer2": "dealer2"}[args.pipeline]
     eng = Engine(T, P, device=dev, refill_period=R, table0=table0, refill_fused=args.refill == "fused",
                  pipeline=pipe, delegation=args.delegation)
     eng.reset(seeds=range(table0, table0 + T))
@@ -482,6 +539,12 @@ def main():
             if ev is not None:
                 ev[1][i].record()
 
+    def kernel_name(variant):
+        """The kernel the variant launches, as rocprofv3 names it (one name per instantiation)."""
+        if variant == "step":
+            return f"k_step_ws_{P}p"
+        return eng.rollout_kernel_name(per_step=variant == "rollout_store")
+
     def events(n):
         return ([torch.cuda.Event(enable_timing=True) for _ in range(n)],
                 [torch.cuda.Event(enable_timing=True) for _ in range(n)])
@@ -519,6 +582,7 @@ def main():
         for e in ev[0] + ev[1]:  # the HIP events are created on first record: outside the timed region
             e.record()
         torch.cuda.synchronize(dev)
+        region_mark(variant, "start", kernel_name(variant), K // per)
         t0 = time.perf_counter()
         if graph is not None:
             # recorded on the replay stream around each replay, not as graph nodes
@@ -531,6 +595,7 @@ def main():
         t_enq = time.perf_counter()
         torch.cuda.synchronize(dev)
         t_sync = time.perf_counter()
+        region_mark(variant, "end")
         barrier(dev)
         elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
         span = ev[0][0].elapsed_time(ev[1][-1]) / 1e3
@@ -575,7 +640,7 @@ def main():
         sp = selfplay_line(dev, rank, world, args.sp_tables, args.sp_iters, warmup=8)
     c4 = None
     if args.c4_tables > 0 and not args.only and args.players == 2:
-        c4 = c4_share_line(dev, rank, world, args.c4_tables, launches=8, warmup=2)
+        c4 = c4_share_line(dev, rank, world, args.c4_tables, launches=8, warmup=2, pipeline=args.c4_pipeline)
     # correctness canaries on the measured run: no error flags, episodes completed
     errs = _native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT | _native.F_FAULT
     bad = int(((eng.flags & errs) != 0).sum().item())
@@ -584,12 +649,6 @@ def main():
     faults = eng.faults()
     rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
     episodes = int(cnts.sum().item())
-
-    def kernel_name(variant):
-        """The kernel the variant launches, as rocprofv3 names it (one name per instantiation)."""
-        if variant == "step":
-            return f"k_step_ws_{P}p"
-        return eng.rollout_kernel_name(per_step=variant == "rollout_store")
 
     def summary(rec):
         v, plan = rec["variant"], rec["plan"]

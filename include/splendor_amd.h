@@ -142,8 +142,9 @@ int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused);
  * and stores the step's outputs) vs one wave per 64 tables (0).  1 (default) = auto: the three-wave
  * dealer variant (a third wave deals the pool refills beside the other two) when every workgroup of
  * it is resident at once (at most two per CU, e.g. 32 768 tables), else two-wave at 64 tables per
- * workgroup; 2 = two-wave at 64; 3 = two-wave at 32; 4 = the dealer variant.  Results are identical
- * in every mode. */
+ * workgroup; 2 = two-wave at 64; 3 = two-wave at 32; 4 = the dealer variant; 5 = the six-wave dealer
+ * variant (two dealer teams per 128-table workgroup, roles given to waves by the SIMD they run on).
+ * Results are identical in every mode. */
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
 /* spl_rollout with per_step_outputs at 64 tables per workgroup only: rollout-store delegation.  On
  * every `every`-th step (every >= 4; 0 = off) each workgroup on an odd XCC skips that step's encode

@@ -1593,6 +1593,113 @@ __device__ __forceinline__ void store_final_rows(const uint8_t *rows_lds, uint64
     }
 }
 
+// ---- column-parallel rows (round 4) --------------------------------------------------------
+// A terminal table's info["final_observation"] row encoded by the whole wave: lane l owns bytes
+// e = l + 64 i (i < 5) of the ONE row and stores them as int32, coalesced (five 256-byte dword
+// stores).  encode_row's lane-per-row form costs every lane a whole row even when one or two of the
+// wave's 64 tables ended (random 4-player games end every ~30 steps: most steps), which made the
+// 4-player output wave's encode 4.4 us against 2.6 us at 2 players.  Here a byte is one or two LDS
+// reads plus a few VALU ops, driven by a per-lane recipe built once per launch (col_recipe): which
+// state word holds it (absolute, or a word of the player to move / the next player), which byte of
+// that word, and whether it names a card / noble whose record byte is the value
+// (engine/encode.py:124-187; the same fields as build_row).
+enum : uint32_t {
+    CK_BYTE = 0,      // the byte itself
+    CK_NRES = 1,      // & 3 (n_reserved of PW3)
+    CK_BOARD = 2,     // board card id -> record byte f (0 when the slot is empty)
+    CK_OWN_RES = 3,   // own reserved card slot s (PW3 byte s + 1) -> record byte f, f == 13: present
+    CK_OPP_RES = 4,   // opponent's reserved slot s: as own, hidden (not revealed) -> zeros
+    CK_NOBLE = 5,     // visible noble slot s (SW_NOB0 byte s) -> noble record byte f
+    CK_MOVES = 6,     // move_count, the full value (no byte patch needed)
+    CK_TERMINAL = 7,  // game_over and to_play == 0
+    CK_NONE = 8       // past the row
+};
+// recipe: word (5 bits) | rel << 5 (0 absolute, 1 to_play's PW, 2 next player's PW) | byte << 7 |
+//         kind << 9 | f << 13 | s << 17
+__device__ __forceinline__ uint32_t col_recipe(int e) {
+    auto R = [](int w, int rel, int b, uint32_t kind, int f = 0, int s = 0) {
+        return (uint32_t)w | ((uint32_t)rel << 5) | ((uint32_t)b << 7) | (kind << 9) | ((uint32_t)f << 13) |
+               ((uint32_t)s << 17);
+    };
+    if (e >= kObsDim) return R(0, 0, 0, CK_NONE);
+    if (e < 4) return R(SW_BANK0, 0, e, CK_BYTE);                                   // bank :128
+    if (e < 6) return R(SW_BANK1, 0, e - 4, CK_BYTE);
+    if (e < 32) {                                                                    // players :131-142
+        const int rel = e < 19 ? 1 : 2, q = e - (e < 19 ? 6 : 19);
+        return q < 12 ? R(q >> 2, rel, q & 3, CK_BYTE) : R(3, rel, 0, CK_NRES);
+    }
+    if (e < 188) {                                                                   // board :144-147
+        const int k = (e - 32) / 13;
+        return R(SW_BOARD + k / 4, 0, k % 4, CK_BOARD, (e - 32) % 13);
+    }
+    if (e < 272) {                                                                   // reserved :151-168
+        const bool own = e < 230;
+        const int q = e - (own ? 188 : 230), s = q / 14;
+        return R(3, own ? 1 : 2, s + 1, own ? CK_OWN_RES : CK_OPP_RES, q % 14, s);
+    }
+    if (e < 290) {                                                                   // nobles[:3] :171-178
+        const int s = (e - 272) / 6;
+        return R(SW_NOB0, 0, s, CK_NOBLE, (e - 272) % 6, s);
+    }
+    if (e < 293) return R(SW_DECK, 0, e - 290, CK_BYTE);                            // deck sizes :180-181
+    if (e == 293) return R(SW_BANK1, 0, 3, CK_BYTE);                                // turn_count :183
+    if (e == 294) return R(SW_BANK1, 0, 2, CK_BYTE);                                // to_play :184
+    if (e == 295) return R(SW_MISC, 0, 0, CK_MOVES);                                // move_count :185
+    return R(SW_MISC, 0, 0, CK_TERMINAL);                                           // terminal :186
+}
+struct ColRecipes {
+    uint32_t r[5];
+};
+__device__ __forceinline__ ColRecipes col_recipes() {
+    ColRecipes c;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) c.r[i] = col_recipe(lane_id() + 64 * i);
+    return c;
+}
+
+// One table's observation row, column-parallel (wave-uniform call): word w of the table's state is
+// st[w * stride] in LDS (st and stride uniform); dst = the row's 297 int32 in global memory.
+template <int P>
+__device__ __forceinline__ void store_row_columns(const uint32_t *st, int stride, const Consts &L, const ColRecipes &C,
+                                                  int32_t *dst) {
+    const uint32_t bank1 = st[SW_BANK1 * stride], misc = st[SW_MISC * stride];
+    const int tp = (int)bget(bank1, 2), np = (tp + 1) % P;
+    const uint32_t deck = st[SW_DECK * stride], owners = (st[SW_NOB1 * stride] >> 8) & 0x7FFFu;
+    const uint8_t *cb = reinterpret_cast<const uint8_t *>(L.cards);
+    const uint8_t *nb = reinterpret_cast<const uint8_t *>(L.nobles);
+    uint32_t v[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t r = C.r[i];
+        const int w0 = (int)(r & 31u), rel = (int)((r >> 5) & 3u), b = (int)((r >> 7) & 3u);
+        const uint32_t kind = (r >> 9) & 15u;
+        const int f = (int)((r >> 13) & 15u), s = (int)((r >> 17) & 3u);
+        const int widx = rel == 0 ? w0 : pw_index(rel == 1 ? tp : np, w0);
+        const uint32_t w = st[widx * stride];
+        const uint32_t byte = bget(w, b);
+        // the record byte a card / noble kind reads (address clamped: read unconditionally)
+        const bool is_noble = kind == CK_NOBLE;
+        const uint32_t id = byte < (is_noble ? 10u : 90u) ? byte : 0u;
+        const uint32_t rec = is_noble ? (uint32_t)nb[id * 8 + (f < 6 ? f : 0)] : (uint32_t)cb[id * 16 + (f < 13 ? f : 0)];
+        const int nres = (int)(w & 3u), rev = (int)((w >> 2) & 7u);
+        const bool res_pr = s < nres && (kind == CK_OWN_RES || ((rev >> s) & 1));
+        const bool nob_pr = s < (int)bget(deck, 3) && ((owners >> (3 * s)) & 7u) == 0u && byte < 10u;
+        uint32_t out = byte;
+        out = kind == CK_NRES ? (w & 3u) : out;
+        out = kind == CK_BOARD ? (byte != 0xFFu ? rec : 0u) : out;
+        out = (kind == CK_OWN_RES || kind == CK_OPP_RES) ? (res_pr ? (f == 13 ? 1u : rec) : 0u) : out;
+        out = is_noble ? (nob_pr ? rec : 0u) : out;
+        out = kind == CK_MOVES ? (misc & 0xFFFFu) : out;
+        out = kind == CK_TERMINAL ? (((misc & ST_GAME_OVER) && tp == 0) ? 1u : 0u) : out;
+        v[i] = out;
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const int e = lane_id() + 64 * i;
+        if (e < kObsDim) dst[e] = (int32_t)v[i];
+    }
+}
+
 // spl_step_args_t.gate_*: the dual step's opponent moves only where the agent's move was applied
 // and left the game running (wrappers/dual_step_native.py:120-140, spl_dual_gate); elsewhere its
 // action becomes -1 (out of range: no move), written back so the caller sees the gated action.
@@ -1980,13 +2087,10 @@ __device__ __forceinline__ void ws_sync() {
 template <int P>
 struct __align__(16) StepWsLDS : Consts {
     static constexpr int kW = SW_COUNT + 4 * P;  // state words per table
-    static constexpr int kTermRows = 16;  // terminal rows the rules wave encodes per step (the rest: output wave)
     uint32_t st[kW][64];   // state after the step (and autoreset)
     uint32_t fst[kW][64];  // pre-reset state of the tables that ended (final_observation)
     uint64_t mask[64];
-    uint64_t fin;          // terminal rows left to the output wave (beyond kTermRows)
     uint32_t mbits[96];
-    uint32_t trow[kTermRows][75];  // the rules wave's terminal rows, compacted (297 bytes in 75 dwords)
     // observation staging (rows of 297 bytes, or 300 for obs_u8); before hand-off 1 the rules wave's
     // deal scratch + LaneMT
     alignas(16) uint8_t rows[64 * kObsU8];
@@ -2033,13 +2137,8 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
 #pragma unroll
             for (int w = 0; w < kW; ++w) L.fst[w][lane] = tab_word(T, w);
         }
-        // terminal rows: the first kTermRows of the wave are encoded and stored by this wave after
-        // hand-off 1 (it has no gathers left then), the rest by the output wave
+        // terminal rows: stored by this wave after hand-off 2, column-parallel (store_row_columns)
         const uint64_t fin_all = __ballot(fin_me);
-        const int fidx = __popcll(fin_all & ((1ull << lane) - 1ull));
-        const uint64_t fin_rules = __ballot(fin_me && fidx < StepWsLDS<P>::kTermRows);
-        const uint64_t fin = fin_all & ~fin_rules;
-        if (lane == 0) L.fin = fin;
         const float ep_add = (valid && o.term) ? final_reward_p0(T) : 0.0f;
         bool pool_dirty = false;
         if (ended && S.autoreset)
@@ -2048,37 +2147,17 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         for (int w = 0; w < kW; ++w) L.st[w][lane] = tab_word(T, w);
         STAMP(3);
         ws_sync();  // hand-off 1: state words (deal scratch in `rows` free again)
-        // Without terminal rows left to the output wave (the usual case) this wave encodes the first
-        // half of every row while the output wave encodes the second (encode 2.7 -> ~1.4 us before
-        // the obs stores start); otherwise the output wave encodes whole rows after its terminal ones.
-        if (fin == 0ull) {
-            if (compact) encode_row_u8<0>(T, L.rows, L);
-            else encode_row_half<0>(T, L.rows, L);
-        }
+        // this wave encodes the first half of every row while the output wave encodes the second
+        // (encode 2.7 -> ~1.4 us before the obs stores start)
+        if (compact) encode_row_u8<0>(T, L.rows, L);
+        else encode_row_half<0>(T, L.rows, L);
         ws_sync();  // hand-off 2: first row halves staged
         STAMP(4);
-        if (fin_rules) {  // info["final_observation"] rows, compacted in trow, stored row by row
-            Tab<P> F;
-#pragma unroll
-            for (int w = 0; w < kW; ++w) set_tab_word(F, w, L.fst[w][lane]);
-            const bool mine = (fin_rules >> lane) & 1ull;
-            if (mine) {
-                uint32_t R[76];
-                build_row(F, L, R);
-#pragma unroll
-                for (int j = 0; j < 75; ++j) L.trow[fidx][j] = R[j];
-            }
-            wave_lds_sync();
-            const uint8_t *tb = reinterpret_cast<const uint8_t *>(&L.trow[0][0]);
-            int k = 0;
-            for (uint64_t m = fin_rules; m; m &= m - 1, ++k) {
+        if (fin_all) {  // info["final_observation"] rows: each by the whole wave, from its listed words
+            const ColRecipes crc = col_recipes();
+            for (uint64_t m = fin_all; m; m &= m - 1) {
                 const int r = __ffsll((unsigned long long)m) - 1;
-                int32_t *dst = S.final_obs + (size_t)(t0 + r) * kObsDim;
-                for (int e = lane; e < kObsDim; e += 64) dst[e] = (int32_t)tb[k * 300 + e];
-            }
-            if (__any(mine && get_moves(F.sw) > 255)) {  // move_count > 255: crafted states only
-                __builtin_amdgcn_s_waitcnt(0);
-                if (mine && get_moves(F.sw) > 255) S.final_obs[(size_t)t * kObsDim + 295] = get_moves(F.sw);
+                store_row_columns<P>(&L.fst[0][r], 64, L, crc, S.final_obs + (size_t)(t0 + r) * kObsDim);
             }
         }
         if (o.mask & kMaskDeferred) o.mask = legal_of(T, L);
@@ -2115,32 +2194,10 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         Tab<P> T;
 #pragma unroll
         for (int w = 0; w < kW; ++w) set_tab_word(T, w, L.st[w][lane]);
-        const uint64_t fin = L.fin;
-        if (fin == 0ull) {
-            if (compact) encode_row_u8<1>(T, L.rows, L);
-            else encode_row_half<1>(T, L.rows, L);
-        }
+        if (compact) encode_row_u8<1>(T, L.rows, L);
+        else encode_row_half<1>(T, L.rows, L);
         ws_sync();  // hand-off 2
         STAMP(4);
-        if (fin) {  // terminal rows (info["final_observation"]) first, through the same staging rows
-            const bool mine = (fin >> lane) & 1ull;
-            Tab<P> F = T;
-            if (mine) {
-#pragma unroll
-                for (int w = 0; w < kW; ++w) set_tab_word(F, w, L.fst[w][lane]);
-            }
-            encode_row(F, L.rows, L);
-            wave_lds_sync();
-            store_final_rows(L.rows, fin, S.final_obs, t0);
-            if (__any(mine && get_moves(F.sw) > 255)) {  // move_count > 255: crafted states only
-                __builtin_amdgcn_s_waitcnt(0);
-                if (mine && get_moves(F.sw) > 255) S.final_obs[(size_t)t * kObsDim + 295] = get_moves(F.sw);
-            }
-            wave_lds_sync();  // the terminal rows' LDS reads are done
-            if (compact) encode_row_u8<2>(T, L.rows, L);
-            else encode_row(T, L.rows, L);
-            wave_lds_sync();
-        }
         STAMP(5);
         if (compact) {
             store_obs_u8_block(L.rows, rows, S.obs_u8 + (size_t)t0 * kObsU8);
@@ -2434,25 +2491,31 @@ __device__ __forceinline__ bool dealer_step(DealerLDS &D, Tab<P> &T, const KAren
 // kStore: per-step outputs (a [K][n][...] rollout store) or every step into the same [n][...] block;
 // a template argument so that the two variants are separate kernels in a profile.
 // kDealer: a third wave deals the pool refills (DealerLDS above; 64 tables per workgroup).
+// A wave's role in rollout_ws (0 rules, 1 output, 2 dealer) and the block of TPW tables it serves;
+// the default (role -1) takes both from the thread index and the workgroup (one block per workgroup).
+struct WaveRole {
+    int role, block;
+};
 template <int P, int TPW, bool kStore, bool kDealer = false, class LdsT = WsLDS<P>>
 __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep S, int K, int refill,
-                                           int deleg_every) {
+                                           int deleg_every, WaveRole wr = WaveRole{-1, -1}) {
     static_assert(TPW == 64 || TPW == 32, "64 or 32 tables per workgroup");
     static_assert(!kDealer || TPW == 64, "the dealer variant runs 64 tables per workgroup");
     constexpr bool per_step = kStore;
     constexpr int kW = WsLDS<P>::kW;
     const int lane = lane_id();
-    const bool rules_wave = threadIdx.x < 64;
+    const int role = wr.role >= 0 ? wr.role : (int)(threadIdx.x >> 6);
+    const bool rules_wave = role == 0;
     // delegation pairs neighbouring workgroups (blockIdx b and b + 1 on adjacent XCCs): identity map
     const bool deleg_shape = TPW == 64 && kStore && !kDealer && deleg_every >= 4;
-    const int t0 = (deleg_shape ? (int)blockIdx.x : wg_block()) * TPW;
+    const int t0 = (wr.block >= 0 ? wr.block : (deleg_shape ? (int)blockIdx.x : wg_block())) * TPW;
     const int t = t0 + lane;
     const bool valid = lane < TPW && t < A.n;
     const int rows = min(TPW, A.n - t0);
     const bool want_final = S.autoreset && S.final_obs != nullptr;
     load_tables_lds(L, Tb);
     if constexpr (kDealer) {  // the hand-off counters start at zero (LDS is not initialised)
-        if (threadIdx.x == 0) {
+        if (rules_wave && lane == 0) {
             L.dl.dreq = L.dl.ddone = L.dl.rdone = L.dl.odone = L.dl.stop = L.dl.abort = 0u;
         }
     }
@@ -2466,7 +2529,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
     const uint64_t clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     if constexpr (kDealer) {
-        if (threadIdx.x >= 128) {
+        if (role >= 2) {
             dealer_loop<P>(L.dl, A, t0);
             return;
         }
@@ -2590,7 +2653,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             if (pool_dirty) store_pool(A, t, pool);
         }
     } else {
-        const uint64_t below = (1ull << lane) - 1ull;
+        const ColRecipes crc = col_recipes();  // this lane's bytes of a column-parallel terminal row
 #ifdef SPL_STAMPS
         int rst_lo[kWsStamps] = {0}, rst_hi[kWsStamps] = {0};
 #endif
@@ -2627,24 +2690,16 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             Tab<P> T;
 #pragma unroll
             for (int w = 0; w < kW; ++w) set_tab_word(T, w, L.st[b][w][lane]);
-            const uint64_t fin = L.fin[b];
-            if (fin) {  // terminal rows (info["final_observation"]) first, through the same rows
+            // terminal rows (info["final_observation"]) first: each by the whole wave, column-parallel,
+            // straight from its listed state words (no staging, no LDS barrier)
+            uint64_t fin = __builtin_amdgcn_readfirstlane((uint32_t)L.fin[b]) |
+                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(L.fin[b] >> 32)) << 32);
+            if (fin) {
                 int32_t *fobs = S.final_obs + blk * kObsDim;
-                const bool mine = (fin >> lane) & 1ull;
-                const int idx = __popcll(fin & below);
-                Tab<P> F = T;
-                if (mine) {
-#pragma unroll
-                    for (int w = 0; w < kW; ++w) set_tab_word(F, w, L.tst[b][idx][w]);
+                for (int idx = 0; fin; fin &= fin - 1, ++idx) {
+                    const int r = __ffsll((unsigned long long)fin) - 1;
+                    store_row_columns<P>(&L.tst[b][idx][0], 1, L, crc, fobs + (size_t)(t0 + r) * kObsDim);
                 }
-                encode_row(F, L.rows, L);
-                wave_lds_sync();
-                store_final_rows(L.rows, fin, fobs, t0);
-                if (__any(mine && get_moves(F.sw) > 255)) {  // move_count > 255: crafted states only
-                    __builtin_amdgcn_s_waitcnt(0);
-                    if (mine && get_moves(F.sw) > 255) fobs[(size_t)t * kObsDim + 295] = get_moves(F.sw);
-                }
-                wave_lds_sync();  // the final rows' LDS reads are done
             }
             const bool big_moves = __any(valid && get_moves(T.sw) > 255);
             const bool deleg_now = dl.producer && deleg_step(k, K, dl.every);
@@ -2808,6 +2863,101 @@ SPL_DEALER_KERNEL(k_rollout_inplace_dealer_2p, 2, false)
 SPL_DEALER_KERNEL(k_rollout_inplace_dealer_3p, 3, false)
 SPL_DEALER_KERNEL(k_rollout_inplace_dealer_4p, 4, false)
 #undef SPL_DEALER_KERNEL
+
+// The six-wave dealer variant (round 4; k_rollout_*_dealer2_<P>p, 128 tables per workgroup, one
+// workgroup per CU): two dealer-rollout teams (rules, output, dealer wave, 64 tables each) in ONE
+// workgroup, so the roles can be given to waves by the SIMD each one landed on.  With two 3-wave
+// workgroups per CU the dispatcher's placement is blind to the roles: a rules wave — the latency-bound
+// critical path of the 4-player step — may share its SIMD with the other team's output or dealer
+// wave, and the 4-player C4 share's stamps showed the workgroups dispatched second on their CU
+// ending ~20 % after the first ones.  Here every wave reads its SIMD (HW_ID.SIMD_ID), the six are
+// exchanged through LDS, and all waves make the same choice: the two rules waves go to the least
+// occupied SIMDs (distinct ones), then the output waves, the dealers take the rest.  Each team is the
+// dealer rollout of rollout_ws on its own LDS half; only which wave plays which part changes, so
+// results are those of every other rollout shape.
+template <int P>
+struct __align__(16) WsDeal2LDS {
+    WsDealLDS<P> team[2];
+    uint32_t simd[6];
+};
+static_assert(sizeof(WsDeal2LDS<2>) <= 163840 && sizeof(WsDeal2LDS<3>) <= 163840 && sizeof(WsDeal2LDS<4>) <= 163840,
+              "the six-wave dealer rollout needs one workgroup per CU");
+
+// wave-uniform: (team * 3 + role) of wave w given the six waves' SIMDs.  Waves are taken in the
+// order (occupancy of their SIMD, wave index); each role takes two of them, preferring SIMDs that do
+// not hold a wave of that role yet: rules first, then output, then dealer.  Static indexing only.
+__device__ __forceinline__ int dealer2_assign(const uint32_t (&simd)[6], int w) {
+    int key[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        int occ = 0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) occ += simd[j] == simd[i] ? 1 : 0;
+        key[i] = occ * 8 + i;
+    }
+    int rank[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) r += key[j] < key[i] ? 1 : 0;
+        rank[i] = r;
+    }
+    int code[6] = {-1, -1, -1, -1, -1, -1};
+#pragma unroll
+    for (int role = 0; role < 3; ++role) {
+        uint32_t used = 0u;  // SIMDs that already hold a wave of this role
+        int got = 0;
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass)
+#pragma unroll
+            for (int r = 0; r < 6; ++r)
+#pragma unroll
+                for (int i = 0; i < 6; ++i) {
+                    const bool take = rank[i] == r && got < 2 && code[i] < 0 &&
+                                      (pass == 1 || ((used >> (simd[i] & 3u)) & 1u) == 0u);
+                    code[i] = take ? got * 3 + role : code[i];
+                    used |= take ? 1u << (simd[i] & 3u) : 0u;
+                    got += take ? 1 : 0;
+                }
+    }
+    int mine = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) mine = i == w ? code[i] : mine;
+    return mine;
+}
+
+template <int P, bool kStore>
+__device__ __forceinline__ void rollout_dealer2(WsDeal2LDS<P> &L, KArena A, KTables Tb, KStep S, int K, int refill) {
+    const int w = (int)(threadIdx.x >> 6);
+    if (lane_id() == 0) L.simd[w] = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;
+    __syncthreads();
+    uint32_t simd[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) simd[i] = __builtin_amdgcn_readfirstlane(L.simd[i]);
+    const int code = __builtin_amdgcn_readfirstlane(dealer2_assign(simd, w));
+    const int team = code / 3;
+    rollout_ws<P, 64, kStore, true>(L.team[team], A, Tb, S, K, refill, 0, WaveRole{code % 3, 2 * wg_block() + team});
+}
+template <int P, bool kStore>
+struct RolloutDealer2Kernel;
+#define SPL_DEALER2_KERNEL(NAME, P_, ST_)                                                                      \
+    __global__ __launch_bounds__(384) void NAME(KArena A, KTables Tb, KStep S, int K, int refill, int deleg) { \
+        __shared__ WsDeal2LDS<P_> L;                                                                           \
+        (void)deleg;                                                                                           \
+        rollout_dealer2<P_, ST_>(L, A, Tb, S, K, refill);                                                      \
+    }                                                                                                          \
+    template <>                                                                                                \
+    struct RolloutDealer2Kernel<P_, ST_> {                                                                     \
+        static constexpr void (*fn)(KArena, KTables, KStep, int, int, int) = NAME;                             \
+    };
+SPL_DEALER2_KERNEL(k_rollout_store_dealer2_2p, 2, true)
+SPL_DEALER2_KERNEL(k_rollout_store_dealer2_3p, 3, true)
+SPL_DEALER2_KERNEL(k_rollout_store_dealer2_4p, 4, true)
+SPL_DEALER2_KERNEL(k_rollout_inplace_dealer2_2p, 2, false)
+SPL_DEALER2_KERNEL(k_rollout_inplace_dealer2_3p, 3, false)
+SPL_DEALER2_KERNEL(k_rollout_inplace_dealer2_4p, 4, false)
+#undef SPL_DEALER2_KERNEL
 
 // Explicit reset (SplendorEnv.reset / VectorEnv.reset), then observation + mask of all tables.
 template <int P>
@@ -3106,6 +3256,7 @@ struct spl_ctx_s {
     int pipeline;      // spl_rollout: 0 one wave per 64 tables, 1 two-wave (auto tables per workgroup), 2 / 3 two-wave at 64 / 32
     int ws_resident[5];  // k_rollout_store_<P>p: workgroups resident per device (occupancy x CUs), index P
     int dealer_resident[5];  // k_rollout_store_dealer_<P>p: the same for the three-wave dealer variant
+    int dealer2_resident[5]; // k_rollout_store_dealer2_<P>p: the same for the six-wave dealer variant
     int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
     uint64_t *fault_host;  // host-mapped, fine-grained: the serial of a launch that faulted (0 = none), spl_ctx_faults
     uint64_t *fault_dev;   // its device address (KStep::fault)
@@ -3266,7 +3417,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         memcpy(&nrec[i], b, 8);
     }
     HIP_TRY(hipSetDevice(device));
-    int ws_resident[5], dealer_resident[5];
+    int ws_resident[5], dealer_resident[5], dealer2_resident[5];
     {
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -3280,6 +3431,11 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&docc[3], RolloutDealerKernel<3, true>::fn, 192, 0));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&docc[4], RolloutDealerKernel<4, true>::fn, 192, 0));
         for (int q = 0; q < 5; ++q) dealer_resident[q] = docc[q] * cus;
+        int d2occ[5] = {0, 0, 0, 0, 0};
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&d2occ[2], RolloutDealer2Kernel<2, true>::fn, 384, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&d2occ[3], RolloutDealer2Kernel<3, true>::fn, 384, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&d2occ[4], RolloutDealer2Kernel<4, true>::fn, 384, 0));
+        for (int q = 0; q < 5; ++q) dealer2_resident[q] = d2occ[q] * cus;
     }
     spl_ctx_t *c = new spl_ctx_t();
     c->device = device;
@@ -3289,6 +3445,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     c->pipeline = 1;
     memcpy(c->ws_resident, ws_resident, sizeof(ws_resident));
     memcpy(c->dealer_resident, dealer_resident, sizeof(dealer_resident));
+    memcpy(c->dealer2_resident, dealer2_resident, sizeof(dealer2_resident));
     if (hipMalloc(&c->cards, sizeof(uint4) * 90) != hipSuccess || hipMalloc(&c->nobles, sizeof(uint2) * 10) != hipSuccess ||
         hipMalloc(&c->lut, sizeof(uint4) * kLutEntries) != hipSuccess) {
         spl_ctx_destroy(c);
@@ -3352,7 +3509,7 @@ int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period) {
 
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on) {
     if (!ctx) return fail(SPL_E_ARG, "null ctx");
-    if (on < 0 || on > 4) return fail(SPL_E_ARG, "rollout pipeline must be 0..4");
+    if (on < 0 || on > 5) return fail(SPL_E_ARG, "rollout pipeline must be 0..5");
     ctx->pipeline = on;
     return SPL_OK;
 }
@@ -3507,11 +3664,12 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
 // k_rollout), or kDealerShape for the three-wave dealer variant.  Auto (pipeline 1): the dealer
 // variant when every workgroup is resident at once with its third wave (at most two per CU, e.g.
 // C4's 32 768 tables per GPU), else two waves at 64 tables per workgroup.
-constexpr int kDealerShape = -1;
+constexpr int kDealerShape = -1, kDealer2Shape = -2;
 static int rollout_tpw(const spl_ctx_t *ctx, int32_t n, int32_t players) {
     if (ctx->pipeline == 2) return 64;
     if (ctx->pipeline == 3) return 32;
     if (ctx->pipeline == 4) return kDealerShape;
+    if (ctx->pipeline == 5) return kDealer2Shape;
     if (ctx->pipeline == 1) return (int64_t)blocks_for(n) <= ctx->dealer_resident[players] ? kDealerShape : 64;
     return 0;
 }
@@ -3526,6 +3684,9 @@ const char *spl_rollout_kernel_name(spl_ctx_t *ctx, int32_t n, int32_t players, 
     static const char *const dealer[2][3] = {
         {"k_rollout_inplace_dealer_2p", "k_rollout_inplace_dealer_3p", "k_rollout_inplace_dealer_4p"},
         {"k_rollout_store_dealer_2p", "k_rollout_store_dealer_3p", "k_rollout_store_dealer_4p"}};
+    static const char *const dealer2[2][3] = {
+        {"k_rollout_inplace_dealer2_2p", "k_rollout_inplace_dealer2_3p", "k_rollout_inplace_dealer2_4p"},
+        {"k_rollout_store_dealer2_2p", "k_rollout_store_dealer2_3p", "k_rollout_store_dealer2_4p"}};
     if (!ctx || n <= 0 || players < 2 || players > 4) {
         fail(SPL_E_ARG, "spl_rollout_kernel_name: bad arguments");
         return nullptr;
@@ -3533,6 +3694,7 @@ const char *spl_rollout_kernel_name(spl_ctx_t *ctx, int32_t n, int32_t players, 
     const int tpw = rollout_tpw(ctx, n, players);
     if (tpw == 0) return one_wave[players - 2];
     if (tpw == kDealerShape) return dealer[per_step_outputs ? 1 : 0][players - 2];
+    if (tpw == kDealer2Shape) return dealer2[per_step_outputs ? 1 : 0][players - 2];
     return names[per_step_outputs ? 1 : 0][tpw == 32 ? 1 : 0][players - 2];
 }
 
@@ -3570,7 +3732,16 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
         hipLaunchKernelGGL((RolloutKernel<PP, TPW, false>::fn), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
                            (int)steps, fused, 0);                                                            \
     })
-    if (tpw == kDealerShape) {
+    if (tpw == kDealer2Shape) {
+        const unsigned blocks = (unsigned)((arena->n + 127) / 128);
+        DISPATCH_P(arena->players, if (p_out) {
+            hipLaunchKernelGGL((RolloutDealer2Kernel<PP, true>::fn), dim3(blocks), dim3(384), 0, s, A, ktables(ctx), S,
+                               (int)steps, fused, 0);
+        } else {
+            hipLaunchKernelGGL((RolloutDealer2Kernel<PP, false>::fn), dim3(blocks), dim3(384), 0, s, A, ktables(ctx), S,
+                               (int)steps, fused, 0);
+        })
+    } else if (tpw == kDealerShape) {
         DISPATCH_P(arena->players, if (p_out) {
             hipLaunchKernelGGL((RolloutDealerKernel<PP, true>::fn), dim3(blocks_for(arena->n)), dim3(192), 0, s, A,
                                ktables(ctx), S, (int)steps, fused, 0);

@@ -34,14 +34,14 @@ def _forced_fault_rollout(eng, K, a, na, out):
         _native.check(lib, lib.spl_debug_set_spin_limit(-1))
 
 
-@pytest.mark.parametrize("P", [2, 4])
-def test_dealer_handoff_timeout_is_reported_and_recoverable(P):
+@pytest.mark.parametrize("P,pipeline", [(2, "dealer"), (4, "dealer"), (4, "dealer2")])
+def test_dealer_handoff_timeout_is_reported_and_recoverable(P, pipeline):
     import torch
     from splendor_gym import _native
     from splendor_gym.device import Engine
     n, K = 1024, 16
-    eng = Engine(n, P, refill_period=16, pipeline="dealer")
-    assert eng.rollout_kernel_name(per_step=True) == f"k_rollout_store_dealer_{P}p"
+    eng = Engine(n, P, refill_period=16, pipeline=pipeline)
+    assert eng.rollout_kernel_name(per_step=True) == f"k_rollout_store_{pipeline}_{P}p"
     eng.reset(seeds=range(n))
     dev = eng.device
     a = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -67,7 +67,7 @@ def test_dealer_handoff_timeout_is_reported_and_recoverable(P):
     eng.reset(seeds=range(n))
     eng.clear_faults()
     assert eng.faults() == 0
-    ref = Engine(n, P, refill_period=16, pipeline="dealer")
+    ref = Engine(n, P, refill_period=16, pipeline="dealer")  # the three-wave variant as the reference
     ref.reset(seeds=range(n))
     a_r = torch.zeros_like(a)
     ref.sample_uniform(out=a_r, seed=1, ply=0)

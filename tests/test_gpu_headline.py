@@ -189,3 +189,98 @@ def test_selfplay_fused_fp32_actor_matches_torch(weights):
         done_total += int(dF[ok].sum())
     assert tainted.float().mean().item() <= 0.01, int(tainted.sum())
     assert done_total > 1000  # many games finished and were re-dealt inside the loop
+
+
+def test_config5_pool_selfplay_at_per_gpu_size_matches_torch():
+    """BASELINE config 5 at its per-GPU size (65 536 tables): the fused loop —
+    agent = fused fp32 ActorCritic, opponent = OpponentPool with 12 frozen snapshots + the current
+    policy drawn per episode (spl_policy_act_grouped) — against the same loop with the torch fp32
+    modules (each table's opponent = the network the pool drew for its episode), 40 dual steps.  Per
+    table: agent and opponent actions, rewards, done and the next observations equal, except tables
+    where either side met a near tie (top two legal logits within 1e-5; at most 1 % leave the
+    comparison).  The agent's sampling launch (k_act32<true, true>, the bench's config-5 kernel) is
+    run on the same observations every step and its critic value checked against torch (1e-5)."""
+    import os
+    import torch
+    from safetensors.torch import load_file
+    from splendor_gym.fused_policy import FusedActorCritic, OpponentPool
+    from splendor_gym.policy import ActorCritic
+    from splendor_gym.selfplay import DualStepVectorEnv
+    N, steps = 65536, 40
+    sd = load_file(os.path.join(os.path.dirname(__file__), "golden", "ppo_splendor_latest.safetensors"), device="cuda")
+    torch.manual_seed(5)
+
+    def net(noise):
+        m = ActorCritic().cuda().eval()
+        m.load_state_dict(sd)
+        if noise:
+            with torch.no_grad():
+                for p in m.parameters():
+                    p.add_(noise * torch.randn_like(p))
+        return m
+
+    agent = net(0.0)
+    snaps = [net(0.02) for _ in range(12)]
+    pool = OpponentPool(agent, pool_size=12, p_current=0.25, seed=99)
+    for m in snaps:
+        pool.add_snapshot(m)
+    nets = {0: agent}
+    nets.update({slot: m for slot, m in zip(pool.pool, snaps)})
+    fa = FusedActorCritic(agent, precision="fp32")
+    envF = DualStepVectorEnv(N, opponent=pool, opponent_obs=False)
+    cur = {}
+
+    def torch_pool(obs, mask):
+        groups = cur["groups"]
+        act = torch.zeros(obs.shape[0], dtype=torch.int32, device=obs.device)
+        lg_all = torch.empty(obs.shape[0], 45, device=obs.device)
+        with torch.no_grad():
+            for g in torch.unique(groups).tolist():
+                rows = groups == g
+                lg = nets[g].actor(obs[rows].float())
+                lg_all[rows] = lg
+                act[rows] = torch.argmax(lg.masked_fill(mask[rows] < 1, float("-inf")), dim=-1).to(torch.int32)
+        cur["opp_logits"], cur["opp_mask"] = lg_all, mask.clone()
+        return act
+
+    envT = DualStepVectorEnv(N, opponent=torch_pool, opponent_obs=False)
+    oF, iF = envF.reset(seed=7)
+    oT, iT = envT.reset(seed=7)
+    tainted = torch.zeros(N, dtype=torch.bool, device=oF.device)
+
+    def near_tie(logits, mask, rows):
+        m = logits[rows].masked_fill(mask[rows] < 1, float("-inf"))
+        top2 = torch.topk(m, 2, dim=-1).values
+        return ((top2[:, 0] - top2[:, 1]) <= 1e-5).all().item()
+
+    done_total = 0
+    for k in range(steps):
+        ok = ~tainted
+        assert torch.equal(oF[ok], oT[ok]) and torch.equal(iF["action_mask"][ok], iT["action_mask"][ok]), k
+        with torch.no_grad():
+            _, _, _, value = fa.act(oF, iF["action_mask"], seed=3, ply=k)
+            vT = agent.get_value(oF.float())
+            lgT = agent.actor(oT.float())
+        assert torch.allclose(value, vT, rtol=1e-5, atol=1e-5), k
+        aF = fa.greedy(oF, iF["action_mask"])
+        aT = torch.argmax(lgT.masked_fill(iT["action_mask"] < 1, float("-inf")), dim=-1).to(torch.int32)
+        diff = (aF != aT) & ok
+        if diff.any():
+            assert near_tie(lgT, iT["action_mask"], diff), k
+            tainted |= diff
+        oF, rF, _, orF, dF, iF = envF.dual_step(aF)
+        cur["groups"] = iF["episode_opponent_index"].clone()  # the network each table's opponent played
+        oT, rT, _, orT, dT, iT = envT.dual_step(aT)
+        ok = ~tainted
+        odiff = (iF["opponent_action"] != iT["opponent_action"]) & ok
+        if odiff.any():
+            assert near_tie(cur["opp_logits"], cur["opp_mask"], odiff), k
+            tainted |= odiff
+            ok = ~tainted
+        assert torch.equal(rF[ok], rT[ok]) and torch.equal(orF[ok], orT[ok]) and torch.equal(dF[ok], dT[ok]), k
+        done_total += int(dF[ok].sum())
+    assert tainted.float().mean().item() <= 0.01, int(tainted.sum())
+    assert len(torch.unique(cur["groups"])) == 13  # the current policy and all 12 snapshots played
+    assert done_total > 0  # episodes ended, re-dealt and drew their next opponents inside the loop
+    envF.close()
+    envT.close()

@@ -271,7 +271,9 @@ def test_unseeded_tables_deal_engine_seed_zero(orc):
                                                           (2, 16, True, "always", 16), (4, 64, True, "always", 16),
                                                           (4, 16, True, "always", 0), (2, 16, False, "half", 16),
                                                           (4, 128, True, "dealer", 16), (2, 16, True, "dealer", 0),
-                                                          (3, 64, False, "dealer", 32), (4, 64, True, "dealer", 1)])
+                                                          (3, 64, False, "dealer", 32), (4, 64, True, "dealer", 1),
+                                                          (4, 128, True, "dealer2", 16), (2, 16, True, "dealer2", 0),
+                                                          (3, 64, False, "dealer2", 32)])
 def test_rollout_equals_step_chain(P, K, refill_fused, pipeline, R):
     """spl_rollout(K) is K chained spl_step calls (next_actions fed back, plies ply..ply+K-1):
     every per-step output, the terminal rows of final_obs, episode statistics, the next action

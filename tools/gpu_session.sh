@@ -32,7 +32,11 @@ for step in "$@"; do
           python3 bench.py --gpus 1 --steps 20 --warmup 5
       cp $O/prof_driver_$TAG/run_kernel_stats.csv $O/kernel_stats_driver_$TAG.csv 2>/dev/null || \
           find $O/prof_driver_$TAG -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats_driver_$TAG.csv \;
-      head -8 $O/kernel_stats_driver_$TAG.csv ;;
+      head -8 $O/kernel_stats_driver_$TAG.csv
+      # the same trace averaged over the timed launches only (bench.py's region marks)
+      python3 tools/trace_timed.py $(find $O/prof_driver_$TAG -name '*kernel_trace.csv' | head -1) \
+          $O/prof_driver_${TAG}.err --source "rocprofv3 --kernel-trace --stats -- python3 bench.py --gpus 1 --steps 20 --warmup 5 ($TAG)" \
+          --out $O/kernel_trace_timed_$TAG.json | head -60 ;;
     deleg) run deleg_ab 600 python3 tools/deleg_ab.py --rounds 12 --arms 0,6 ;;
     profc4)
       run prof_c4 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4_$TAG -o run -- \
@@ -76,6 +80,12 @@ for step in "$@"; do
       run pytest_pol 500 python -u -m pytest tests/test_gpu_policy.py tests/test_gpu_opponent_pool.py \
           tests/test_gpu_compact_obs.py tests/test_gpu_headline.py tests/test_gpu_parity.py tests/test_wrappers.py \
           -x -v --timeout 200 --timeout-method thread ;;
+    pmcpol) bash tools/pmc_policy.sh $TAG || exit 1 ;;
+    bench4) run bench_4p_32768 600 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 --only ;;
+    c4ab)  # the C4 share's rollout kernels, alternating on one box: three-wave dealer vs six-wave dealer2
+      for i in 1 2; do for pl in dealer dealer2; do
+        run c4ab_${pl}_$i 300 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 --only --pipeline $pl
+      done; done ;;
     abl32) bash tools/ablate_policy32.sh || exit 1 ;;  # k_act32 timing ablations (BUILD=1 here first)
     *) echo "unknown step $step"; exit 2 ;;
   esac
