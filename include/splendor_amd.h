@@ -139,11 +139,12 @@ int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period);
  * Results are identical either way. */
 int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused);
 /* spl_rollout only: the two-wave pipelined kernel (one wave steps the tables, the other encodes
- * and stores the step's outputs) vs one wave per 64 tables (0).  1 (default) = auto: the three-wave
- * dealer variant (a third wave deals the pool refills beside the other two) when every workgroup of
- * it is resident at once (at most two per CU, e.g. 32 768 tables), else two-wave at 64 tables per
- * workgroup; 2 = two-wave at 64; 3 = two-wave at 32; 4 = the dealer variant; 5 = the six-wave dealer
- * variant (two dealer teams per 128-table workgroup, roles given to waves by the SIMD they run on).
+ * and stores the step's outputs) vs one wave per 64 tables (0).  1 (default) = auto: the six-wave
+ * dealer variant (5) when every 128-table workgroup of it is resident at once (one per CU, e.g.
+ * 32 768 tables), else the three-wave dealer variant (4: a third wave deals the pool refills beside the
+ * other two) when it fits, else two-wave at 64 tables per workgroup; 2 = two-wave at 64; 3 = two-wave
+ * at 32; 4 = the three-wave dealer variant; 5 = the six-wave dealer variant (two dealer teams per
+ * 128-table workgroup, roles given to waves by the SIMD they run on).
  * Results are identical in every mode. */
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
 /* spl_rollout with per_step_outputs at 64 tables per workgroup only: rollout-store delegation.  On

@@ -2692,8 +2692,9 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             for (int w = 0; w < kW; ++w) set_tab_word(T, w, L.st[b][w][lane]);
             // terminal rows (info["final_observation"]) first: each by the whole wave, column-parallel,
             // straight from its listed state words (no staging, no LDS barrier)
-            uint64_t fin = __builtin_amdgcn_readfirstlane((uint32_t)L.fin[b]) |
-                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(L.fin[b] >> 32)) << 32);
+            // (readfirstlane returns int: widen through uint32_t, or bit 31 sign-extends into lanes 32-63)
+            uint64_t fin = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)L.fin[b]) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(L.fin[b] >> 32)) << 32);
             if (fin) {
                 int32_t *fobs = S.final_obs + blk * kObsDim;
                 for (int idx = 0; fin; fin &= fin - 1, ++idx) {
@@ -3661,16 +3662,21 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
 }
 
 // The rollout kernel shape: tables per workgroup of the two-wave rollout (0 = the one-wave
-// k_rollout), or kDealerShape for the three-wave dealer variant.  Auto (pipeline 1): the dealer
-// variant when every workgroup is resident at once with its third wave (at most two per CU, e.g.
-// C4's 32 768 tables per GPU), else two waves at 64 tables per workgroup.
+// k_rollout), or kDealerShape / kDealer2Shape for the three- / six-wave dealer variants.  Auto
+// (pipeline 1): the six-wave dealer variant when every 128-table workgroup is resident at once (one
+// per CU, e.g. C4's 32 768 tables per GPU: 1 120-1 137 against 1 166-1 172 us per 128-step launch
+// for the three-wave one, alternating on one box, profiles/r04/c4ab_r04b.txt), else the three-wave
+// one when it fits, else two waves at 64 tables per workgroup.
 constexpr int kDealerShape = -1, kDealer2Shape = -2;
 static int rollout_tpw(const spl_ctx_t *ctx, int32_t n, int32_t players) {
     if (ctx->pipeline == 2) return 64;
     if (ctx->pipeline == 3) return 32;
     if (ctx->pipeline == 4) return kDealerShape;
     if (ctx->pipeline == 5) return kDealer2Shape;
-    if (ctx->pipeline == 1) return (int64_t)blocks_for(n) <= ctx->dealer_resident[players] ? kDealerShape : 64;
+    if (ctx->pipeline == 1) {  // auto: the six-wave dealer (SIMD-aware roles, -3.5 % on C4's share), else three-wave
+        if ((int64_t)((n + 127) / 128) <= ctx->dealer2_resident[players]) return kDealer2Shape;
+        return (int64_t)blocks_for(n) <= ctx->dealer_resident[players] ? kDealerShape : 64;
+    }
     return 0;
 }
 

@@ -49,7 +49,7 @@ def test_headline_rollout_65536_equals_step_chain_and_oracle(P, n, R):
     K, seed, launches = 128, 0, 2
     chain = engine(n, P, refill_period=R)
     roll = engine(n, P, refill_period=R, refill_fused=True, pipeline=True)  # bench.py defaults
-    assert roll.rollout_kernel_name() == ("k_rollout_store_2p" if P == 2 else "k_rollout_store_dealer_4p")
+    assert roll.rollout_kernel_name() == ("k_rollout_store_2p" if P == 2 else "k_rollout_store_dealer2_4p")
     chain.reset(seeds=range(n))
     roll.reset(seeds=range(n))
     dev = chain.device
