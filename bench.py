@@ -60,12 +60,14 @@ STEP_ALGO_BYTES = {p: 2 * s + 297 * 4 + 45 + 4 + 4 + 1 for p, s in STATE_BYTES.i
 # pool refill period per player count: three pool deals per table must cover the resets between
 # refills (random games last ~77 plies at 2p, ~29 at 4p)
 REFILL_EVERY = {2: 64, 3: 32, 4: 16}
-BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table; no sparsity)
-# bf16 MFMA work of the fused fp32 ActorCritic (csrc/spl_policy32.hip) per table: every fp32 operand is
-# three bf16 planes; layer 1 (297 -> 256, observation exact in bf16) takes 3 plane products, layers
-# 2 (256 -> 256) and 3 (256 -> 45) take 6; the critic's 256 -> 1 output runs on VALU, not counted
-ACTOR_MFMA_FLOP = 2 * (297 * 256 * 3 + 256 * 256 * 6 + 256 * 45 * 6)   # 1 380 864
-CRITIC_MFMA_FLOP = 2 * (297 * 256 * 3 + 256 * 256 * 6)                 # 1 242 624
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md chip table; no sparsity)
+# fp16 MFMA work of the fused fp32 ActorCritic (csrc/spl_policy32.hip, round 4) per table: every fp32
+# operand is two fp16 planes; layer 1 (297 -> 256, observation exact in fp16) takes 2 plane products,
+# layers 2 (256 -> 256) and 3 (256 -> 45) take 3; the critic's 256 -> 1 output runs on VALU, not counted
+ACTOR_MFMA_FLOP = 2 * (297 * 256 * 2 + 256 * 256 * 3 + 256 * 45 * 3)   # 766 464
+CRITIC_MFMA_FLOP = 2 * (297 * 256 * 2 + 256 * 256 * 3)                 # 697 344
+# the network's own fp32 work per table (2 x MACs of actor + critic), for the fp32-equivalent rate
+NET_FP32_FLOP = 2 * (297 * 256 + 256 * 256 + 256 * 45 + 297 * 256 + 256 * 256 + 256)
 ROLLOUT_K = 128    # env steps per spl_rollout launch = ppo_splendor.py's --num-steps default (:71)
 MIN_TIMED_LAUNCHES = 8  # rollout mode times at least this many launches (>= 16 ms), whatever --steps says
 
@@ -314,16 +316,19 @@ def selfplay_line(dev, rank, world, N, iters, warmup):
     return {"metric": f"env-steps/sec (whole node), 2p self-play, on-device fp32 ActorCritic, {N} tables/GPU",
             "value": round(2 * N * world * iters / el, 1), "unit": "env-steps/s",
             "ms_per_dual_step": round(el / iters * 1e3, 4), "iters": iters,
-            "dtype": "fp32 (fp32 operands as three bf16 planes, six plane products accumulated in fp32; torch fp32 tolerance 1e-5)",
-            "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tflops / BF16_MFMA_PEAK_TFLOPS, 4), "kernel": "k_act32<true, true>",
+            "dtype": "fp32 (fp32 operands as two fp16 planes of 22 significant bits, three plane products accumulated "
+                     "in fp32; torch fp32 tolerance 1e-5)",
+            "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tflops / F16_MFMA_PEAK_TFLOPS, 4), "kernel": "k_act32<true, true>",
                          "kernel_us": spread["us"], "flop_per_launch": flop,
-                         "flop_note": "bf16 MFMA work per table: actor 2*(297*256*3 + 256*256*6 + 256*45*6) + critic "
-                                      "2*(297*256*3 + 256*256*6) = 2 623 488 (three bf16 planes per fp32 operand: 3 plane "
-                                      "products in layer 1, 6 in layers 2-3; the critic's 256->1 output on VALU); "
-                                      "frac from the median of 16 eager launches (HIP events on the launch stream)",
+                         "fp32_equivalent_tflops": round(NET_FP32_FLOP * N / spread["median_s"] / 1e12, 1),
+                         "flop_note": "fp16 MFMA work per table: actor 2*(297*256*2 + 256*256*3 + 256*45*3) + critic "
+                                      "2*(297*256*2 + 256*256*3) = 1 463 808 (two fp16 planes per fp32 operand: 2 plane "
+                                      "products in layer 1, 3 in layers 2-3; the critic's 256->1 output on VALU); "
+                                      "frac from the median of 16 eager launches (HIP events on the launch stream); "
+                                      "fp32_equivalent_tflops = the network's 2 x MACs per table at that time",
                          "traffic": None},
-            "config": {"workload": "BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused, fp32-accurate split-bf16 MFMA) + "
+            "config": {"workload": "BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused, fp32-accurate two-plane fp16 MFMA) + "
                                    "DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of 12 frozen "
                                    "snapshots per episode, greedy), reset after done; hipGraph replays",
                        "tables_per_gpu": N, "weights": "reference checkpoint runs/ppo_splendor/ppo_splendor_latest.pt"}}

@@ -9,9 +9,10 @@
  * for opponents.  These entry points evaluate that network for a whole batch of tables in one
  * launch: observations (int32 [n][297]) and masks (int8 [n][45]) straight from the engine, tanh /
  * softmax / sampling fused.  Two precisions:
- *   SPL_PREC_FP32 (default)  the reference's fp32: fp32-accurate products (three bf16 planes per
- *                            operand, six plane products accumulated in fp32 on
- *                            v_mfma_f32_16x16x32_bf16; spl_policy32.hip), fp32 tanh
+ *   SPL_PREC_FP32 (default)  the reference's fp32: fp32-accurate products (two fp16 planes per
+ *                            operand, 22 significant bits, weights scaled per row by a power of two;
+ *                            three plane products accumulated in fp32 on v_mfma_f32_16x16x32_f16;
+ *                            spl_policy32.hip), fp32 tanh
  *   SPL_PREC_BF16 (opt-in)   bf16 MFMA (v_mfma_f32_32x32x16_bf16) with fp32 accumulation (spl_policy.hip)
  *
  *   spl_policy_bytes   size of a packed weight image (actor only, or actor + critic; per precision)
@@ -31,7 +32,8 @@
 extern "C" {
 #endif
 
-#define SPL_POLICY_ABI 3  /* 2: precision argument, args->image describes the image; 3: obs_u8 */
+#define SPL_POLICY_ABI 4  /* 2: precision argument, args->image describes the image; 3: obs_u8;
+                             4: fp32 images as two fp16 planes (spl_policy_bytes changed) */
 
 #define SPL_PREC_FP32 0
 #define SPL_PREC_BF16 1

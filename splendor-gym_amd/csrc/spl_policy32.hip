@@ -3,29 +3,32 @@
 // Same network and epilogue as spl_policy.hip's bf16 kernel (ppo_splendor.py:27-59: actor and
 // critic Linear(297,256)-Tanh-Linear(256,256)-Tanh-Linear(256,{45|1}); masked_categorical sample,
 // log_prob, entropy, critic value; or the greedy masked argmax of training_utils.py:263-276), with
-// fp32-accurate products on the bf16 matrix cores (gfx950 has no xf32 MFMA, and its fp32 MFMA runs
-// at 1/16 of the bf16 rate):
-//   * every fp32 operand x is split into three bf16 planes x = x0 + x1 + x2 (x0 = bf16(x),
-//     x1 = bf16(x - x0), x2 = bf16(x - x0 - x1): 3 x 8 significand bits, so x is represented to
-//     ~2^-25 relative; each residual is exact in fp32).  A weight-times-activation product is the
-//     six plane products of order <= 2, a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0, accumulated in
-//     fp32 by v_mfma_f32_16x16x32_bf16 (bf16 x bf16 products are exact in fp32); the three dropped
-//     terms are <= 3 x 2^-24 of |ab|, the size of an fp32 rounding.  Layer 1's operand is the
-//     observation, small integers exact in bf16: three products (a0 b + a1 b + a2 b).
-//     Smallest terms first into the accumulator.  6 (3) bf16 MFMAs per 32 inputs against 8 fp32
-//     v_mfma_f32_16x16x4_f32 of twice the cycles each: ~2.7x (5.3x) fewer matrix cycles.
+// fp32-accurate products on the 16-bit matrix cores (gfx950 has no xf32 MFMA, and its fp32 MFMA runs
+// at 1/16 of the fp16/bf16 rate):
+//   * every fp32 operand x is split into two fp16 planes x = x0 + x1 (x0 = fp16(x), x1 = fp16(x - x0):
+//     22 significant bits, x represented to 2^-22 relative; the residual is exact in fp32).  fp16's
+//     exponent range is narrow, so the weights are scaled per output row by a power of two (the row's
+//     largest |w| into [512, 1024)) and hidden activations (|tanh| < 1) by 2^10: every plane is a
+//     normal fp16.  A weight-times-activation product is the three plane products of order <= 1,
+//     a1 w0 + a0 w1 + a0 w0, accumulated in fp32 by v_mfma_f32_16x16x32_f16 (fp16 x fp16 products
+//     are exact in fp32); the dropped a1 w1 is <= 2^-22 of |aw|.  Smallest terms first; the row's sum
+//     comes back through the exact factor 2^-(row exponent + activation exponent).  Layer 1's operand,
+//     the observation, is integers < 2048, exact in fp16: two products (a w1 + a w0).
+//     Round 3 used three bf16 planes and six products (SPL_P32_F16=0 builds it): 1.8x the MFMAs and
+//     1.5x the weight bytes streamed for the same network (k_act32<true, true> 184 -> 140 us at 65 536
+//     tables, profiles/r04).
 //   * a wave = 16 tables = the 16 columns of every 16x16x32 tile; a workgroup = 8 waves = 128 tables
 //     (two waves per SIMD).  Activations are TRANSPOSED (hidden unit on the accumulator row, table
 //     on the lane): accumulator register i of lane group g holds unit 16t + 4g + i of tile t, and
 //     tiles 2s, 2s+1 are lane group g's B elements of k-step s of the next layer (element e = unit
 //     16(2s + e/4) + 4g + e%4) — no LDS round trip between layers; the packed weights carry the
 //     matching input-unit order.  tanh runs in fp32 (tanh_f32) before the split.
-//   * the observation (int32 -> bf16, exact) loads into registers as the 10 layer-1 B fragments
-//     and stays there through both networks' layer 1; a hidden layer's output is 3 planes x 8
-//     k-steps x 8 bf16 per lane.
-//   * weights stream once per workgroup through a 4-slot LDS ring (31-KB chunks = one 16-row
-//     output tile of one layer, [k-step][plane][lane][8 bf16] + bias, global_load_lds, 3 chunks in
-//     flight), shared by the 8 waves.
+//   * the observation (int32 -> fp16, exact) loads into registers as the 10 layer-1 B fragments
+//     and stays there through both networks' layer 1; a hidden layer's output is 2 planes x 8
+//     k-steps x 8 fp16 per lane.
+//   * weights stream once per workgroup through a 5-slot LDS ring (21-KB chunks = one 16-row
+//     output tile of one layer, [k-step][plane][lane][8 fp16] + scaled biases + row factors,
+//     global_load_lds, 4 chunks in flight), shared by the 8 waves.
 //   * the critic's one-unit output layer is a per-lane fp32 FMA chain over its layer-2 tiles.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -54,17 +57,38 @@ namespace splp32 {
 
 using spl::philox4x32;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Operand planes (round 4).  SPL_P32_F16 = 1 (default): every fp32 operand is two fp16 planes
+// x = x0 + x1 (x0 = fp16(x), x1 = fp16(x - x0): 22 significant bits, |x - x0 - x1| <= 2^-22 |x|) —
+// weights scaled per output row by a power of two so the row's largest |w| lands in [512, 1024) and
+// every plane stays a normal fp16, hidden activations (|tanh| < 1) scaled by 2^10; a hidden-layer
+// product is the three plane products a1 w0 + a0 w1 + a0 w0 on v_mfma_f32_16x16x32_f16 (the dropped
+// a1 w1 is <= 2^-22 |aw|), the observation (integers < 2048, exact in fp16) takes two; the scaled sum
+// is brought back by the exact power-of-two row factor.  0: three bf16 planes, six products (round 3).
+#ifndef SPL_P32_F16
+#define SPL_P32_F16 1
+#endif
+#if SPL_P32_F16
+typedef _Float16 pel;
+constexpr int kPlanes = 2;       // fp16 planes of a split fp32 operand
+constexpr int kActScaleExp = 10; // hidden activations enter the next layer as tanh * 2^10
+constexpr int kRowMaxExp = 10;   // a weight row's largest |w| is scaled into [2^9, 2^10)
+#else
+typedef __bf16 pel;
+constexpr int kPlanes = 3;       // bf16 planes of a split fp32 operand
+constexpr int kActScaleExp = 0;
+constexpr int kRowMaxExp = 0;    // bf16 has fp32's exponent range: no scaling
+#endif
+typedef pel pelx8 __attribute__((ext_vector_type(8)));
+typedef pel pelx2 __attribute__((ext_vector_type(2)));
 
 constexpr int kObs = 297, kAct = 45, kHid = 256;
 constexpr int kKs1 = 10;    // layer-1 k-steps of 32: 297 inputs padded to 320
 constexpr int kKs2 = 8;     // layers 2 and 3: 256 inputs
-constexpr int kPlanes = 3;  // bf16 planes of a split fp32 operand
-constexpr int kFrag = 1024;                       // one plane of one k-step: [lane][8 bf16]
-constexpr int kBiasOff = kKs1 * kPlanes * kFrag;  // 30 720: after the largest weight block
-constexpr int kChunk = 31 * 1024;                 // + the tile's 16 fp32 biases, in 1-KB blocks
+constexpr int kFrag = 1024;                       // one plane of one k-step: [lane][8 elements]
+constexpr int kBiasOff = kKs1 * kPlanes * kFrag;  // after the largest weight block
+constexpr int kChunk = kBiasOff + 1024;           // + the tile's 16 (scaled) fp32 biases and 16 row factors
 constexpr int kTiles = kHid / 16;                 // 16 output tiles of 16 rows per hidden layer
 constexpr int kActTiles = 3;                      // 48 rows >= 45 logits
 constexpr int kActorChunks = 2 * kTiles + kActTiles, kCriticChunks = 2 * kTiles;  // 35, 32
@@ -75,7 +99,7 @@ constexpr int kCriticTail = 272 * 4;  // fp32 critic output layer: w3 [256], b3,
 #define SPL_P32_WAVES 8  // waves per k_act32 workgroup (16 tables each)
 #endif
 #ifndef SPL_P32_RING
-#define SPL_P32_RING 4  // ring slots (SPL_P32_RING - 1 chunks in flight)
+#define SPL_P32_RING (SPL_P32_F16 ? 5 : 4)  // ring slots (SPL_P32_RING - 1 chunks in flight)
 #endif
 constexpr int kWaves = SPL_P32_WAVES, kRowsPerWave = 16, kRowsPerBlock = kWaves * kRowsPerWave;  // 128 tables
 constexpr int kSlots = SPL_P32_RING;
@@ -85,7 +109,7 @@ constexpr int kLdsMask = kSlots * kChunk;
 constexpr int kLds = kLdsMask + kWaves * kMaskWave;  // 132 736 B
 static_assert(kWaves * kRowsPerWave * kLogitRow * 4 <= kLdsMask, "logits reuse the weight ring");
 static_assert(kLds <= 160 * 1024, "LDS");
-static_assert(kBiasOff + 64 <= kChunk, "bias");
+static_assert(kBiasOff + 128 <= kChunk, "bias + row factors");
 
 // chunk order of an image (the order a forward pass consumes them): with a critic
 // [critic L1 x16][critic L2 x16], then [actor L1 x16][actor L2 x16][actor L3 x3]; the actor part of
@@ -102,16 +126,18 @@ __device__ __forceinline__ int unit_of(int layer, int s, int g, int e) {
     return layer == 1 ? 32 * s + 8 * g + e : 16 * (2 * s + (e >> 2)) + 4 * g + (e & 3);
 }
 
-// x = x0 + x1 + x2 in bf16 (round to nearest even; x - x0 and x - x0 - x1 are exact in fp32)
-__device__ __forceinline__ void split3(float x, __bf16 &x0, __bf16 &x1, __bf16 &x2) {
-    x0 = (__bf16)x;
-    const float r = x - (float)x0;
-    x1 = (__bf16)r;
-    x2 = (__bf16)(r - (float)x1);
+// x = x0 + x1 (+ x2) in the plane format (round to nearest even; the residuals are exact in fp32)
+__device__ __forceinline__ void split_planes(float x, pel (&q)[kPlanes]) {
+    q[0] = (pel)x;
+    const float r = x - (float)q[0];
+    q[1] = (pel)r;
+    if constexpr (kPlanes == 3) q[2] = (pel)(r - (float)q[1]);
 }
 
-// one block per physical chunk: [k-step s][plane p][lane][8 bf16], lane l = (g = l >> 4, r = l & 15)
-// holds W[row 16*tile + r][unit_of(layer, s, g, e)] split into planes 0..2; then 16 fp32 biases
+// one block per physical chunk: [k-step s][plane p][lane][8 elements], lane l = (g = l >> 4, r = l & 15)
+// holds W[row 16*tile + r][unit_of(layer, s, g, e)] * 2^e_row split into the planes; then the 16 rows'
+// biases scaled as the products are (2^(e_row + layer's activation exponent)) and the 16 exact
+// factors 2^-(e_row + activation exponent) that bring a row's sum back
 __global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, int with_critic, uint8_t *dst) {
     const int ch = blockIdx.x;
     const int net = with_critic && ch < kCriticChunks ? 1 : 0;  // 0 actor, 1 critic
@@ -124,26 +150,46 @@ __global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, i
     const int in = layer == 1 ? kObs : kHid, rows = layer == 3 ? P.out : kHid;
     const int ks = layer == 1 ? kKs1 : kKs2;
     uint8_t *out = dst + (size_t)ch * kChunk;
-    __bf16 *o = reinterpret_cast<__bf16 *>(out);
+    pel *o = reinterpret_cast<pel *>(out);
+    // each row's scale exponent: its largest |w| into [2^(kRowMaxExp-1), 2^kRowMaxExp) (fp16 planes)
+    __shared__ float part[16][17];
+    __shared__ int rexp[16];
+    {
+        const int r = threadIdx.x >> 4, c = threadIdx.x & 15, row = 16 * tile + r;
+        float m = 0.f;
+        if (row < rows)
+            for (int k = c; k < in; k += 16) m = fmaxf(m, fabsf(W[(size_t)row * in + k]));
+        part[r][c] = m;
+        __syncthreads();
+        if (threadIdx.x < 16) {
+            float mx = 0.f;
+            for (int j = 0; j < 16; ++j) mx = fmaxf(mx, part[threadIdx.x][j]);
+            int x = 0;
+            (void)frexpf(mx, &x);  // mx = f * 2^x, f in [0.5, 1)
+            rexp[threadIdx.x] = (kRowMaxExp == 0 || mx == 0.f) ? 0 : max(-40, min(60, kRowMaxExp - x));
+        }
+        __syncthreads();
+    }
     for (int v = threadIdx.x; v < ks * 64 * 8; v += blockDim.x) {
         const int e = v & 7, lane = (v >> 3) & 63, s = v >> 9;
         const int r = lane & 15, g = lane >> 4, row = 16 * tile + r, k = unit_of(layer, s, g, e);
-        const float w = (row < rows && k < in) ? W[(size_t)row * in + k] : 0.f;
-        __bf16 w0, w1, w2;
-        split3(w, w0, w1, w2);
+        const float w = (row < rows && k < in) ? ldexpf(W[(size_t)row * in + k], rexp[r]) : 0.f;
+        pel q[kPlanes];
+        split_planes(w, q);
         const size_t base = ((size_t)(s * kPlanes) * 64 + lane) * 8 + e;
-        o[base] = w0;
-        o[base + 64 * 8] = w1;
-        o[base + 2 * 64 * 8] = w2;
+#pragma unroll
+        for (int p = 0; p < kPlanes; ++p) o[base + (size_t)p * 64 * 8] = q[p];
     }
     for (int v = ks * kPlanes * kFrag + 4 * threadIdx.x; v < kBiasOff; v += 4 * blockDim.x)
         *reinterpret_cast<uint32_t *>(out + v) = 0u;
     float *bias = reinterpret_cast<float *>(out + kBiasOff);
-    if (threadIdx.x < 16) {  // bias in row order, then zero padding to the end of the chunk
-        const int row = 16 * tile + threadIdx.x;
-        bias[threadIdx.x] = row < rows ? B[row] : 0.f;
+    const int act_exp = layer == 1 ? 0 : kActScaleExp;  // layer 1 reads the observation unscaled
+    if (threadIdx.x < 16) {  // scaled biases in row order, then the row factors, zero padding to the end
+        const int row = 16 * tile + threadIdx.x, ex = rexp[threadIdx.x] + act_exp;
+        bias[threadIdx.x] = row < rows ? ldexpf(B[row], ex) : 0.f;
+        bias[16 + threadIdx.x] = ldexpf(1.f, -ex);
     }
-    for (int v = kBiasOff + 64 + 4 * threadIdx.x; v < kChunk; v += 4 * blockDim.x)
+    for (int v = kBiasOff + 128 + 4 * threadIdx.x; v < kChunk; v += 4 * blockDim.x)
         *reinterpret_cast<uint32_t *>(out + v) = 0u;
     if (net == 1 && layer == 2 && tile == 0) {  // the critic's output layer as fp32 (evaluated on VALU)
         float *tail = reinterpret_cast<float *>(dst + (size_t)kAllChunks * kChunk);
@@ -221,26 +267,30 @@ constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
 // a wave's loads of the chunks after chunk c that may stay in flight when it enters chunk c
 constexpr int kWaitMost = (kSlots - 2) * kBlocksPerWave, kWaitLast = (kSlots - 2) * (kBlocksPerWave - 1);
 
-__device__ __forceinline__ f32x4 mma(const bf16x8 &a, const bf16x8 &b, const f32x4 &c) {
+__device__ __forceinline__ f32x4 mma(const pelx8 &a, const pelx8 &b, const f32x4 &c) {
 #if SPL_POL_ABL & 8
     return c + (float)a[0] * (float)b[1];
+#elif SPL_P32_F16
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 #else
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 #endif
 }
 
-// one 16-row output tile: bias + sum over KS k-steps of 32 inputs.  B: NB planes of the layer's
-// input (1: the observation, exact in bf16; 3: a split hidden layer), in registers.  A: the tile's
-// three weight planes per k-step from `src` (the LDS ring slot, or the image in global memory for
-// the narrow kernel), D k-steps ahead of the MFMAs that use them.
+// one 16-row output tile: bias + sum over KS k-steps of 32 inputs, returned at the true scale (the
+// row factors undo the planes' scaling).  B: NB planes of the layer's input (1: the observation,
+// exact in one plane; kPlanes: a split hidden layer), in registers.  A: the tile's weight planes per
+// k-step from `src` (the LDS ring slot, or the image in global memory for the narrow kernel), D
+// k-steps ahead of the MFMAs that use them.
 template <int KS, int NB, int D>
-__device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const bf16x8 (&B)[NB][KS], int lane) {
-    static_assert(NB == 1 || NB == 3, "planes");
+__device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const pelx8 (&B)[NB][KS], int lane) {
+    static_assert(NB == 1 || NB == kPlanes, "planes");
     const float *bias = reinterpret_cast<const float *>(src + kBiasOff) + 4 * (lane >> 4);
     f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
-    const bf16x8 *A = reinterpret_cast<const bf16x8 *>(src) + lane;  // k-step s, plane p at A[(3s + p) * 64]
+    const f32x4 unscale = {bias[16], bias[17], bias[18], bias[19]};
+    const pelx8 *A = reinterpret_cast<const pelx8 *>(src) + lane;  // k-step s, plane p at A[(kPlanes s + p) * 64]
     constexpr int NR = D + 1;
-    bf16x8 af[NR][kPlanes];
+    pelx8 af[NR][kPlanes];
 #pragma unroll
     for (int q = 0; q < D && q < KS; ++q)
 #pragma unroll
@@ -251,10 +301,13 @@ __device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const bf16x8 (&B)[
 #pragma unroll
             for (int p = 0; p < kPlanes; ++p) af[(s + D) % NR][p] = A[(kPlanes * (s + D) + p) * 64];
         }
-        const bf16x8 *a = af[(SPL_POL_ABL & 4) ? s % D : s % NR];
-        if constexpr (NB == 1) {  // exact B: a2 b + a1 b + a0 b
-            acc = mma(a[2], B[0][s], acc);
+        const pelx8 *a = af[(SPL_POL_ABL & 4) ? s % D : s % NR];
+        if constexpr (NB == 1) {  // exact B: (a2 b +) a1 b + a0 b
+#pragma unroll
+            for (int p = kPlanes - 1; p >= 0; --p) acc = mma(a[p], B[0][s], acc);
+        } else if constexpr (kPlanes == 2) {  // the three products of order <= 1, smallest first
             acc = mma(a[1], B[0][s], acc);
+            acc = mma(a[0], B[1][s], acc);
             acc = mma(a[0], B[0][s], acc);
         } else {  // the six products of order <= 2, smallest first
             acc = mma(a[2], B[0][s], acc);
@@ -264,35 +317,36 @@ __device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const bf16x8 (&B)[
             acc = mma(a[0], B[1][s], acc);
             acc = mma(a[0], B[0][s], acc);
         }
-        if (NB == 3 || (s & 1) == 1) __builtin_amdgcn_sched_barrier(0);
+        if (NB > 1 || (s & 1) == 1) __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (kRowMaxExp != 0) acc *= unscale;  // exact: powers of two
     return acc;
 }
 
-// planes of a bf16x8 as dwords: element e in dword e / 2 (even e in the low half)
-__device__ __forceinline__ uint32_t pk2(__bf16 lo, __bf16 hi) {
-    const bf16x2 v = {lo, hi};
+// planes of a pelx8 as dwords: element e in dword e / 2 (even e in the low half)
+__device__ __forceinline__ uint32_t pk2(pel lo, pel hi) {
+    const pelx2 v = {lo, hi};
     return __builtin_bit_cast(uint32_t, v);
 }
 
-// the four fp32 outputs h[0..3] of tile t (units 16t + 4g + i) -> elements 4(t & 1) .. +3 of
-// k-step t / 2 of the next layer's three B planes
-__device__ __forceinline__ void put_split(bf16x8 (&H)[kPlanes][kKs2], int t, const float (&h)[4]) {
-    __bf16 x[4][kPlanes];
+// the four fp32 outputs h[0..3] of tile t (units 16t + 4g + i), scaled by 2^kActScaleExp (exact) ->
+// elements 4(t & 1) .. +3 of k-step t / 2 of the next layer's B planes
+__device__ __forceinline__ void put_split(pelx8 (&H)[kPlanes][kKs2], int t, const float (&h)[4]) {
+    pel x[4][kPlanes];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) split3(h[i], x[i][0], x[i][1], x[i][2]);
+    for (int i = 0; i < 4; ++i) split_planes(kActScaleExp ? h[i] * (float)(1 << kActScaleExp) : h[i], x[i]);
 #pragma unroll
     for (int p = 0; p < kPlanes; ++p) {
         u32x4 w = __builtin_bit_cast(u32x4, H[p][t >> 1]);
         w[2 * (t & 1)] = pk2(x[0][p], x[1][p]);
         w[2 * (t & 1) + 1] = pk2(x[2][p], x[3][p]);
-        H[p][t >> 1] = __builtin_bit_cast(bf16x8, w);
+        H[p][t >> 1] = __builtin_bit_cast(pelx8, w);
     }
 }
 
 // a hidden layer: 16 tiles, each tile's tanh split into the next layer's B planes
 template <int KS, int NB, int D, typename Enter>
-__device__ __forceinline__ void layer_tanh(Enter &enter, const bf16x8 (&B)[NB][KS], bf16x8 (&H)[kPlanes][kKs2],
+__device__ __forceinline__ void layer_tanh(Enter &enter, const pelx8 (&B)[NB][KS], pelx8 (&H)[kPlanes][kKs2],
                                            int lane) {
 #pragma unroll
     for (int t = 0; t < kTiles; ++t) {
@@ -306,7 +360,7 @@ __device__ __forceinline__ void layer_tanh(Enter &enter, const bf16x8 (&B)[NB][K
 
 // the same B fragments from a compact row (spl_step_args_t.obs_u8: 300 bytes, move_count >> 8 at
 // byte 297): 8 bytes per k-step as two dword loads, k = 296 alone, k >= 297 zero
-__device__ __forceinline__ void load_obs_u8(const uint8_t *xrow, int g, bf16x8 (&X)[1][kKs1]) {
+__device__ __forceinline__ void load_obs_u8(const uint8_t *xrow, int g, pelx8 (&X)[1][kKs1]) {
     const uint32_t *w = reinterpret_cast<const uint32_t *>(xrow);
 #pragma unroll
     for (int s = 0; s < kKs1; ++s) {
@@ -325,15 +379,15 @@ __device__ __forceinline__ void load_obs_u8(const uint8_t *xrow, int g, bf16x8 (
             v[4 + e] = (int)((hi >> (8 * e)) & 0xFFu);
         }
         if (k0 == 288) v[7] += 256 * (int)((w[74] >> 8) & 0xFFu);  // k = 295: move_count
-        const u32x4 q = {pk2((__bf16)(float)v[0], (__bf16)(float)v[1]), pk2((__bf16)(float)v[2], (__bf16)(float)v[3]),
-                         pk2((__bf16)(float)v[4], (__bf16)(float)v[5]), pk2((__bf16)(float)v[6], (__bf16)(float)v[7])};
-        X[0][s] = __builtin_bit_cast(bf16x8, q);
+        const u32x4 q = {pk2((pel)(float)v[0], (pel)(float)v[1]), pk2((pel)(float)v[2], (pel)(float)v[3]),
+                         pk2((pel)(float)v[4], (pel)(float)v[5]), pk2((pel)(float)v[6], (pel)(float)v[7])};
+        X[0][s] = __builtin_bit_cast(pelx8, q);
     }
 }
 
 // the observation's B fragments: lane (r, g), k-step s, element e = obs[table r][32s + 8g + e]
-// (integers < 256: exact in bf16)
-__device__ __forceinline__ void load_obs(const int32_t *xrow, int g, bf16x8 (&X)[1][kKs1]) {
+// (integers < 2048: exact in fp16; < 256 in the bf16 build)
+__device__ __forceinline__ void load_obs(const int32_t *xrow, int g, pelx8 (&X)[1][kKs1]) {
 #pragma unroll
     for (int s = 0; s < kKs1; ++s) {
         int v[8];
@@ -342,9 +396,9 @@ __device__ __forceinline__ void load_obs(const int32_t *xrow, int g, bf16x8 (&X)
             const int k = 32 * s + 8 * g + e;
             v[e] = k < kObs ? xrow[k < kObs ? k : 0] : 0;
         }
-        const u32x4 w = {pk2((__bf16)(float)v[0], (__bf16)(float)v[1]), pk2((__bf16)(float)v[2], (__bf16)(float)v[3]),
-                         pk2((__bf16)(float)v[4], (__bf16)(float)v[5]), pk2((__bf16)(float)v[6], (__bf16)(float)v[7])};
-        X[0][s] = __builtin_bit_cast(bf16x8, w);
+        const u32x4 w = {pk2((pel)(float)v[0], (pel)(float)v[1]), pk2((pel)(float)v[2], (pel)(float)v[3]),
+                         pk2((pel)(float)v[4], (pel)(float)v[5]), pk2((pel)(float)v[6], (pel)(float)v[7])};
+        X[0][s] = __builtin_bit_cast(pelx8, w);
     }
 }
 
@@ -454,7 +508,7 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
     const int32_t tid_own = (a.order && lane < valid) ? a.order[tbase + lane] : 0;
     // observation B fragments (load_obs)
     const int64_t xt = valid > 0 ? (a.order ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : tbase + (r < valid ? r : 0)) : 0;
-    bf16x8 X[1][kKs1];
+    pelx8 X[1][kKs1];
     if (a.obs_u8) load_obs_u8(a.obs_u8 + (size_t)xt * 300, g, X);
     else load_obs(a.obs + (size_t)xt * kObs, g, X);
     if constexpr (!kActor) {
@@ -506,7 +560,7 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
     };
     static_assert(kWaitMost <= 63, "vmcnt range");
 
-    bf16x8 H1[kPlanes][kKs2];
+    pelx8 H1[kPlanes][kKs2];
     float value = 0.f;
     if constexpr (kCritic) {
         layer_tanh<kKs1, 1, kAheadL1>(enter, X, H1, lane);
@@ -530,7 +584,7 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
         return;
     }
     layer_tanh<kKs1, 1, kAheadL1>(enter, X, H1, lane);
-    bf16x8 H2[kPlanes][kKs2];
+    pelx8 H2[kPlanes][kKs2];
     layer_tanh<kKs2, kPlanes, kAheadHid>(enter, H1, H2, lane);
     f32x4 L[kActTiles];
 #pragma unroll
@@ -572,8 +626,8 @@ constexpr int kNarrowWaves = 8;  // two hidden-layer tiles per wave (2 waves per
 // one hidden layer split over the waves (wave w: tiles w and w + 8), then every wave gathers all
 // 16 tiles' tanh outputs (its next layer's B fragments) from LDS
 template <int KS, int NB>
-__device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const bf16x8 (&B)[NB][KS],
-                                             bf16x8 (&H)[kPlanes][kKs2], float *xbuf, int wave, int lane) {
+__device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const pelx8 (&B)[NB][KS],
+                                             pelx8 (&H)[kPlanes][kKs2], float *xbuf, int wave, int lane) {
 #pragma unroll
     for (int h = 0; h < kTiles / kNarrowWaves; ++h) {
         const int t = wave + kNarrowWaves * h;
@@ -609,7 +663,7 @@ __global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_
     const int valid = (int)max<int64_t>(0, min<int64_t>(kRowsPerWave, gend - tbase));
     const int32_t tid_own = lane < valid ? a.order[tbase + lane] : 0;
     const int64_t xt = valid > 0 ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : 0;
-    bf16x8 X[1][kKs1];
+    pelx8 X[1][kKs1];
     if (a.obs_u8) load_obs_u8(a.obs_u8 + (size_t)xt * 300, g, X);
     else load_obs(a.obs + (size_t)xt * kObs, g, X);
     if (wave == 0) {  // the wave-tile's mask bytes (gathered rows), for the epilogue
@@ -627,7 +681,7 @@ __global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_
             if (e < valid * kAct) ms[e] = (uint8_t)mv[i];
         }
     }
-    bf16x8 H1[kPlanes][kKs2], H2[kPlanes][kKs2];
+    pelx8 H1[kPlanes][kKs2], H2[kPlanes][kKs2];
     narrow_layer(W, 0, X, H1, xbuf, wave, lane);
     narrow_layer(W, kTiles, H1, H2, xbuf, wave, lane);
     if (wave < kActTiles) {  // logits: waves 0..2 take one 16-row tile each

@@ -15,9 +15,9 @@ tables in one HIP launch straight from the engine's int32 observations and int8 
     of ppo_splendor.py:302): the critic alone, fp32.
 
 precision="fp32" (default, the reference's precision): fp32-accurate products — every operand split
-into three bf16 planes, the six plane products of order <= 2 accumulated in fp32 on
-v_mfma_f32_16x16x32_bf16 (csrc/spl_policy32.hip) — so logits and values equal the fp32 module's to
-summation-order rounding (tests/test_gpu_policy.py: 1e-5 relative).  precision="bf16" (opt-in): bf16 MFMA with fp32
+into two fp16 planes (22 significant bits; weights scaled per row by a power of two), the three plane
+products of order <= 1 accumulated in fp32 on v_mfma_f32_16x16x32_f16 (csrc/spl_policy32.hip) — so
+logits and values equal the fp32 module's to within 1e-5 relative (tests/test_gpu_policy.py).  precision="bf16" (opt-in): bf16 MFMA with fp32
 accumulation, logits to bf16 accuracy.  Call ``refresh()`` after the module's weights change (e.g.
 after each PPO update).
 """

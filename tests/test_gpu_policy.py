@@ -1,10 +1,12 @@
 """Fused ActorCritic forward (include/splendor_policy.h) against the torch fp32 module it replaces
 (ppo_splendor.py:27-59 ActorCritic / masked_categorical; training_utils.py:263-276 greedy).
 
-fp32 kernel (the default, the reference's precision; fp32-accurate products: three bf16 planes per
-operand, six plane products accumulated in fp32 on v_mfma_f32_16x16x32_bf16):
+fp32 kernel (the default, the reference's precision; fp32-accurate products: two fp16 planes per
+operand (22 significant bits, weights scaled per row by a power of two), three plane products
+accumulated in fp32 on v_mfma_f32_16x16x32_f16):
   * |logit - ref| <= 1e-5 * (|ref| + 1) and |value - ref| <= 1e-5 * (|ref| + 1) against the plain
-    fp32 module (what is left is summation order and the kernel's few-ulp tanh vs torch's, ~1e-7);
+    fp32 module (what is left is summation order, the planes' 2^-22 representation and the kernel's
+    few-ulp tanh vs torch's, ~1e-6);
   * greedy actions EQUAL torch's argmax on every row whose top two legal logits are more than
     1e-5 apart (closer pairs are ties at fp32 rounding: each side's sums round differently).
 

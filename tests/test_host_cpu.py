@@ -50,8 +50,9 @@ def test_policy_abi_host_side_errors():
     lib = _native.load_library()
     # bf16: actor 18 chunks, full image 35 chunks + the fp32 critic output layer; fp32: 35 / 67 chunks + tail
     assert lib.spl_policy_bytes(0, 1) == 18 * 20480 and lib.spl_policy_bytes(1, 1) == 35 * 20480 + 272 * 4
-    # fp32 images: 31-KB chunks (3 bf16 planes of a 16-row tile + its biases, spl_policy32.hip)
-    assert lib.spl_policy_bytes(0, 0) == 35 * 31744 and lib.spl_policy_bytes(1, 0) == 67 * 31744 + 272 * 4
+    # fp32 images: 21-KB chunks (2 fp16 planes of a 16-row tile + its scaled biases and row factors,
+    # spl_policy32.hip)
+    assert lib.spl_policy_bytes(0, 0) == 35 * 21504 and lib.spl_policy_bytes(1, 0) == 67 * 21504 + 272 * 4
     assert lib.spl_policy_bytes(0, 9) == -1
     assert lib.spl_policy_pack(None, None, 0, None, None) == -1
     assert b"actor" in lib.spl_last_error()
