@@ -134,17 +134,17 @@ __device__ uint64_t *g_wsstamps;
 __device__ uint32_t *g_wshwid;  // [workgroup][wave][2]: HW_ID (SIMD, CU, SE) and XCC_ID of each wave
 __device__ uint64_t *g_wsclk;   // [workgroup][4]: s_memtime / s_memrealtime at the rules wave's start and end
 __device__ uint64_t *g_wsend;   // [workgroup][2]: s_memrealtime at the output wave's last step and at its end
-#define WSHWID(wave)                                                                             \
+#define WSHWID(sid, wave)                                                                        \
     do {                                                                                         \
         if (g_wshwid && lane_id() == 0) {                                                        \
-            g_wshwid[((size_t)blockIdx.x * 2 + (wave)) * 2 + 0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  \
-            g_wshwid[((size_t)blockIdx.x * 2 + (wave)) * 2 + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20); \
+            g_wshwid[((size_t)(sid) * 2 + (wave)) * 2 + 0] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  \
+            g_wshwid[((size_t)(sid) * 2 + (wave)) * 2 + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 20); \
         }                                                                                        \
     } while (0)
 #define WSSTAMP(i, k) RSTAMP(i, k)
 #else
-#define WSHWID(wave) \
-    do {             \
+#define WSHWID(sid, wave) \
+    do {                  \
     } while (0)
 #define WSSTAMP(i, k) \
     do {              \
@@ -1316,6 +1316,21 @@ __device__ __forceinline__ void load_tables_lds(Consts &L, const KTables &Tb) {
     for (int i = lane_id(); i < 90; i += 64) L.cards[i] = Tb.cards[i];
     if (lane_id() < 10) L.nobles[lane_id()] = Tb.nobles[lane_id()];
 }
+// The same tables by LDS-DMA from ONE wave (global_load_lds, 16 B per lane: 90 card records, then the
+// 80-B noble array as five 16-B pieces): no registers and no LDS write instructions, and the issuing
+// wave's own vmcnt covers their landing — a later s_waitcnt vmcnt(0) of that wave makes them readable
+// to it, and a barrier after that to the workgroup.
+typedef __attribute__((address_space(3))) void lds_void_t;
+__device__ __forceinline__ void dma_tables_lds(Consts &L, const KTables &Tb) {
+    const int lane = lane_id();
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(Tb.cards + lane), (lds_void_t *)&L.cards[0], 16, 0, 0);
+    if (lane < 26)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(Tb.cards + 64 + lane), (lds_void_t *)&L.cards[64],
+                                         16, 0, 0);
+    if (lane < 5)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint8_t *>(Tb.nobles) + 16 * lane,
+                                         (lds_void_t *)&L.nobles[0], 16, 0, 0);
+}
 
 template <int P>
 __device__ __forceinline__ uint64_t legal_of(const Tab<P> &T, const Consts &L) {
@@ -1327,13 +1342,17 @@ __device__ __forceinline__ uint64_t legal_of(const Tab<P> &T, const Consts &L) {
     return legal_mask(T.sw, p, bank, L);
 }
 
-// uniform-random legal action: Philox(seed; table, ply) scaled to the legal count
-__device__ __forceinline__ int sample_uniform(uint64_t m, uint64_t seed, uint64_t table, uint64_t ply) {
+// the uniform policy's Philox(seed; table, ply) word: independent of the state, so a wave with spare
+// time can draw it ahead (the dealer rollout's output wave, two steps ahead of the rules wave)
+__device__ __forceinline__ uint32_t uniform_draw(uint64_t seed, uint64_t table, uint64_t ply) {
+    return philox4x32(make_uint4((uint32_t)table, (uint32_t)(table >> 32), (uint32_t)ply, (uint32_t)(ply >> 32)),
+                      make_uint2((uint32_t)seed, (uint32_t)(seed >> 32))).x;
+}
+// uniform-random legal action from a drawn word: scaled to the legal count, the k-th legal action
+__device__ __forceinline__ int sample_uniform_word(uint64_t m, uint32_t rx) {
     const int n = __popcll(m);
     if (n == 0) return 0;
-    const uint4 r = philox4x32(make_uint4((uint32_t)table, (uint32_t)(table >> 32), (uint32_t)ply, (uint32_t)(ply >> 32)),
-                               make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
-    int k = (int)(((uint64_t)r.x * (uint64_t)n) >> 32);
+    int k = (int)(((uint64_t)rx * (uint64_t)n) >> 32);
     // position of the k-th set bit
     uint64_t mm = m;
     int pos = 0;
@@ -1347,6 +1366,10 @@ __device__ __forceinline__ int sample_uniform(uint64_t m, uint64_t seed, uint64_
         mm = up ? (mm >> width) : low;
     }
     return pos;
+}
+// uniform-random legal action: Philox(seed; table, ply) scaled to the legal count
+__device__ __forceinline__ int sample_uniform(uint64_t m, uint64_t seed, uint64_t table, uint64_t ply) {
+    return sample_uniform_word(m, uniform_draw(seed, table, ply));
 }
 
 // scripts/eval_suite.py opponents over a 45-bit legal mask; their random choices are Philox
@@ -2114,6 +2137,10 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         Tab<P> T;
         int action = 0;
         Deal pool = empty_deal();
+        // the constant tables by LDS-DMA first: they land while the state loads are in flight, and the
+        // vmcnt(0) below (which the state needs anyway) covers them — no staging wave, no hand-off 0
+        // (a barrier that the stamps put at 2.8 us, ~0.7 us after the state had landed)
+        dma_tables_lds(L, Tb);
         if (valid) {
             load_tab(T, A, t);
             action = gated_action(S, t);
@@ -2121,8 +2148,8 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         } else {
             fresh_state(T, 0u, empty_deal());
         }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): state, action, pool and the tables' DMA have landed
         const StepPre pre = step_prefetch(T, action, valid, A, t, Tb);
-        ws_sync();  // hand-off 0: the output wave staged the constant tables
         STAMP(1);
         uint32_t *const mtx = reinterpret_cast<uint32_t *>(&L.rows[64 * kScratchStride]);
         StepOut o = step_rules(T, action, pre, valid, L, Tb, mtx, false, 0ull, true);
@@ -2185,11 +2212,9 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         }
         STAMP(6);
     } else {
-        load_tables_lds(L, Tb);
         STAMP(1);
-        ws_sync();  // hand-off 0
         STAMP(2);
-        ws_sync();  // hand-off 1
+        ws_sync();  // hand-off 1 (the rules wave's table DMA landed before it)
         STAMP(3);
         Tab<P> T;
 #pragma unroll
@@ -2314,6 +2339,7 @@ struct DealerLDS {
     uint32_t dreq, ddone;     // batches posted (rules wave) / dealt (dealer)
     uint32_t rdone, odone;    // steps handed off by the rules wave / finished by the output wave
     uint32_t stop;            // rules wave: no more batches
+    uint32_t rnd[2][64];      // the uniform policy's words of step k in slot k & 1, drawn by the output wave at step k - 2
     uint32_t abort;           // a wait ran out (lds_wait_ge): every later wait returns at once
 };
 template <int P>
@@ -2521,7 +2547,10 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
     }
     ws_sync();
 
-    WSHWID(rules_wave ? 0 : 1);
+    // stamp slot of this team (diagnostic builds): its 64-table block for the six-wave dealer, else the workgroup
+    const int sid = wr.block >= 0 ? wr.block : (int)blockIdx.x;
+    (void)sid;
+    WSHWID(sid, rules_wave ? 0 : 1);
     // the rules wave is the critical path: it wins issue arbitration against the CU's output
     // waves (rollout store 1134 -> 1103 us per launch on one box; 1 and 3 measure the same)
     if (rules_wave) __builtin_amdgcn_s_setprio(SPL_WS_PRIO);
@@ -2604,7 +2633,13 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             }
             WSSTAMP(7, k);
             L.small[b][lane] = pack_small(valid, o, wnr, valid && o.term, ep_add);  // stored by the output wave
-            action = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
+            if (kDealer && S.policy == SPL_POLICY_UNIFORM && k >= 2) {
+                // the Philox word was drawn by the output wave at step k - 2 (it published odone >= k - 1
+                // after writing it, which this step waited for): only the scaling stays on this chain
+                if constexpr (kDealer) action = sample_uniform_word(o.mask, L.dl.rnd[b][lane]);
+            } else {
+                action = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)k);
+            }
             cur_mask = o.mask;
             if (k + 1 < K) pre = step_prefetch(T, action, valid, A, t, Tb);
 #pragma unroll
@@ -2636,15 +2671,15 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         {
             const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
             if (g_wsclk && lane == 0) {
-                g_wsclk[blockIdx.x * 4 + 0] = clk0;
-                g_wsclk[blockIdx.x * 4 + 1] = rt0;
-                g_wsclk[blockIdx.x * 4 + 2] = clk1;
-                g_wsclk[blockIdx.x * 4 + 3] = rt1;
+                g_wsclk[sid * 4 + 0] = clk0;
+                g_wsclk[sid * 4 + 1] = rt0;
+                g_wsclk[sid * 4 + 2] = clk1;
+                g_wsclk[sid * 4 + 3] = rt1;
             }
         }
         if (g_wsstamps && lane < K)
             for (int i = 0; i < kWsStamps; ++i)
-                g_wsstamps[(((size_t)blockIdx.x * 2 + 0) * 64 + lane) * kWsStamps + i] =
+                g_wsstamps[(((size_t)sid * 2 + 0) * 64 + lane) * kWsStamps + i] =
                     ((uint64_t)(uint32_t)rst_hi[i] << 32) | (uint32_t)rst_lo[i];
 #endif
         if (valid) {
@@ -2654,6 +2689,8 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         }
     } else {
         const ColRecipes crc = col_recipes();  // this lane's bytes of a column-parallel terminal row
+        const uint64_t ply0 = S.ply + (S.ply_base ? *S.ply_base : 0ull);  // the policy words drawn ahead (dealer)
+        (void)ply0;
 #ifdef SPL_STAMPS
         int rst_lo[kWsStamps] = {0}, rst_hi[kWsStamps] = {0};
 #endif
@@ -2757,11 +2794,15 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 flag_store(ready_flag(pend), dl.epoch << 1);
                 pend = -1;
             }
-            if constexpr (kDealer) lds_publish(&L.dl.odone, (uint32_t)(k + 1));  // slot b is free again
+            if constexpr (kDealer) {
+                if (S.policy == SPL_POLICY_UNIFORM && k + 2 < K)  // step k + 2's policy word, slot b again
+                    L.dl.rnd[b][lane] = uniform_draw(S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)(k + 2));
+                lds_publish(&L.dl.odone, (uint32_t)(k + 1));  // slot b is free again
+            }
             WSSTAMP(3, k);
         }
 #ifdef SPL_STAMPS
-        if (g_wsend && lane == 0) g_wsend[blockIdx.x * 2 + 0] = __builtin_amdgcn_s_memrealtime();
+        if (g_wsend && lane == 0) g_wsend[sid * 2 + 0] = __builtin_amdgcn_s_memrealtime();
 #endif
         if (dl.on && !dl.producer) {
             // consumer: the partner's staged blocks, each as soon as its ready flag shows
@@ -2806,13 +2847,13 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
 #ifdef SPL_STAMPS
         if (g_wsend) {
             __builtin_amdgcn_s_waitcnt(0);  // this wave's stores have completed
-            if (lane == 0) g_wsend[blockIdx.x * 2 + 1] = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) g_wsend[sid * 2 + 1] = __builtin_amdgcn_s_memrealtime();
         }
 #endif
 #ifdef SPL_STAMPS
         if (g_wsstamps && lane < K)
             for (int i = 0; i < kWsStamps; ++i)
-                g_wsstamps[(((size_t)blockIdx.x * 2 + 1) * 64 + lane) * kWsStamps + i] =
+                g_wsstamps[(((size_t)sid * 2 + 1) * 64 + lane) * kWsStamps + i] =
                     ((uint64_t)(uint32_t)rst_hi[i] << 32) | (uint32_t)rst_lo[i];
 #endif
     }

@@ -257,3 +257,36 @@ def test_refresh_tracks_weight_updates(precision):
     f.refresh()
     v2 = f.act(obs, mask)[3]
     assert torch.allclose(v2 - v1, torch.ones_like(v1), atol=1e-3)
+
+
+def test_large_crafted_observation_values_are_exact():
+    """observation values above 255 (crafted move_count / token counts; the device keeps
+    move_count <= 508 and counts <= 255, SPL_E_RANGE beyond) must enter layer 1 exactly.  Round 4's
+    fp16 planes hold integers < 2048 exactly, on the int32 rows and on the compact obs_u8 rows (byte
+    297 carries move_count >> 8): logits and values stay within the fp32 tolerance of torch."""
+    import torch
+    from splendor_gym import _native
+    from splendor_gym.fused_policy import FusedActorCritic
+    n = 64
+    e, _, _ = states(n)
+    recs = e.download()
+    recs["move_count"] = np.arange(n) * 7 + 60          # 60 .. 501: many above 255
+    recs["turn_count"] = np.minimum(recs["move_count"] // 2 + 1, 99)
+    e.upload(recs)
+    obs = e.encode().clone()
+    mask = e.legal().clone()
+    assert int(obs[:, 295].max()) > 255 and torch.equal(obs[:, 295].cpu(), torch.from_numpy(recs["move_count"]).int())
+    # the compact rows of the same observations: bytes, move_count high byte at 297
+    u8 = torch.zeros(n, _native.OBS_U8, dtype=torch.uint8, device=obs.device)
+    u8[:, :297] = (obs & 0xFF).to(torch.uint8)
+    u8[:, 297] = (obs[:, 295] >> 8).to(torch.uint8)
+    m = model("trained")
+    f = FusedActorCritic(m, with_critic=True)
+    a32, lp32, _, v32, lg32 = f.act(obs, mask, seed=3, ply=1, want_logits=True)
+    a8, lp8, _, v8, lg8 = f.act(u8, mask, seed=3, ply=1, want_logits=True)
+    with torch.no_grad():
+        ref = m.actor(obs.float())
+        vref = m.get_value(obs.float())
+    assert fp32_close(lg32, ref), (lg32 - ref).abs().max().item()
+    assert fp32_close(v32, vref), (v32 - vref).abs().max().item()
+    assert torch.equal(lg8, lg32) and torch.equal(v8, v32) and torch.equal(a8, a32) and torch.equal(lp8, lp32)

@@ -60,6 +60,10 @@ for step in "$@"; do
     poolsize) for ps in 0 1 3 6 12; do run sps_$ps 200 python3 tools/bench_selfplay.py --opponent pool --pool-size $ps; done ;;
     pmcstep) bash tools/pmc.sh ${TAG}_2p_step 2 65536 step all || exit 1 ;;
     stamps) run stamps 300 python3 tools/stamps.py --run ;;
+    wsstamps4) WS_P=4 WS_T=32768 run wsstamps4 300 python3 tools/wsstamps.py --run ;;
+    wsstamps2) run wsstamps2 300 python3 tools/wsstamps.py --run ;;
+    stepab) run bench_step 300 python3 bench.py --mode step --only --no-cpu-baseline --sp-tables 0 ;;
+    poltest1) run pytest_pol1 300 python -u -m pytest tests/test_gpu_policy.py -x -q --timeout 200 --timeout-method thread ;;
     selfplay) run sp_pool 300 python tools/bench_selfplay.py
               run sp_frozen 300 python tools/bench_selfplay.py --opponent frozen ;;
     bench) run bench_default 600 python3 bench.py ;;
