@@ -41,6 +41,9 @@
 #ifndef SPL_TANH_LIBM
 #define SPL_TANH_LIBM 0
 #endif
+#ifndef SPL_TANH_EXP
+#define SPL_TANH_EXP 1
+#endif
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
 // streaming, no per-tile barrier), 4 A fragments loaded once per tile (no per-group LDS reads)
 #ifndef SPL_POL_ABL
@@ -216,7 +219,11 @@ struct ActArgs {
     int64_t image_stride;
 };
 
-// tanh in fp32 without branches (SPL_TANH_LIBM=1 restores libm tanhf).  |x| < 0.625:
+// tanh in fp32 without branches.  Default (round 4, SPL_TANH_EXP=1): 1 - 2 / (exp(2|x|) + 1) alone,
+// six VALU ops (two transcendental): its error is ABSOLUTE, ~1e-7 over the whole range (a few ulp of
+// 1 from v_exp_f32 / v_rcp_f32), relative only near 0, where the next layer multiplies the unit by
+// weights of ~1e-1 anyway; tanh was ~17 % of the kernel (SPL_POL_ABL=1 ablation, profiles/r04).
+// SPL_TANH_EXP=0 is round 3's accurate form (SPL_TANH_LIBM=1 restores libm tanhf).  |x| < 0.625:
 // x + x^3 P(x^2), a degree-4 fit in x^2 (<= 0.9 ulp in fp32 Horner, checked over [0, 0.625]);
 // otherwise 1 - 2 / (exp(2|x|) + 1) on v_exp_f32 / v_rcp_f32 (~1.5 ulp with correctly rounded
 // exp2 and rcp, a few ulp on the hardware's).  Both halves are evaluated and selected, so a
@@ -227,6 +234,9 @@ __device__ __forceinline__ float tanh_f32(float x) {
     return x;
 #elif SPL_TANH_LIBM
     return tanhf(x);
+#elif SPL_TANH_EXP
+    const float e = __builtin_amdgcn_exp2f(__builtin_fabsf(x) * 2.8853900817779268f);  // exp(2|x|)
+    return __builtin_copysignf(__builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f), x);
 #else
     const float ax = __builtin_fabsf(x);
     const float z = ax * ax;

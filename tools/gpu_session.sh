@@ -63,6 +63,16 @@ for step in "$@"; do
     wsstamps4) WS_P=4 WS_T=32768 run wsstamps4 300 python3 tools/wsstamps.py --run ;;
     wsstamps2) run wsstamps2 300 python3 tools/wsstamps.py --run ;;
     stepab) run bench_step 300 python3 bench.py --mode step --only --no-cpu-baseline --sp-tables 0 ;;
+    abl2)  # actor timing ablation: no ring streaming (one weight chunk; wrong results by design)
+      run pol_full 200 python tools/bench_policy.py --fused-only --iters 30
+      SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_abl2.so run pol_abl2 200 python tools/bench_policy.py --fused-only --iters 30
+      SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_abl1.so run pol_abl1 200 python tools/bench_policy.py --fused-only --iters 30
+      SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_abl8.so run pol_abl8 200 python tools/bench_policy.py --fused-only --iters 30 ;;
+    tanhab)  # the actor's tanh: exp form (product) vs round 3's polynomial, alternating on one box
+      for i in 1 2; do
+        run pol_tanhexp_$i 200 python tools/bench_policy.py --fused-only --iters 30
+        SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_tanhpoly.so run pol_tanhpoly_$i 200 python tools/bench_policy.py --fused-only --iters 30
+      done ;;
     poltest1) run pytest_pol1 300 python -u -m pytest tests/test_gpu_policy.py -x -q --timeout 200 --timeout-method thread ;;
     selfplay) run sp_pool 300 python tools/bench_selfplay.py
               run sp_frozen 300 python tools/bench_selfplay.py --opponent frozen ;;
