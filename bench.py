@@ -334,7 +334,16 @@ def selfplay_line(dev, rank, world, N, iters, warmup):
                        "tables_per_gpu": N, "weights": "reference checkpoint runs/ppo_splendor/ppo_splendor_latest.pt"}}
 
 
-def c4_share_line(dev, rank, world, T, launches, warmup, pipeline=True):
+def partner_stats(lib, clear=False):
+    """The six-wave dealer's partner hand-off counters (spl_debug_partner_stats; synchronises)."""
+    import ctypes
+    st = (ctypes.c_uint64 * 2)()
+    if lib.spl_debug_partner_stats(st, 1 if clear else 0) != 0:
+        return None
+    return {"stored_by_partner": int(st[0]), "claimed_back": int(st[1])}
+
+
+def c4_share_line(dev, rank, world, T, launches, warmup, pipeline=True, partner_lead=None):
     """BASELINE config 4's per-GPU share (262 144 4-player tables over 8 GPUs = 32 768 per GPU) on
     this rank: the same per-step rollout store as the headline (spl_rollout, 128 steps per launch,
     every step's obs/mask/reward/terminated/flags/winner into [128, T, ...]), `launches` launches
@@ -346,7 +355,8 @@ def c4_share_line(dev, rank, world, T, launches, warmup, pipeline=True):
     from splendor_gym.parallel import barrier, max_over_ranks
     P, K = 4, ROLLOUT_K
     table0 = rank * T
-    eng = Engine(T, P, device=dev, refill_period=REFILL_EVERY[P], table0=table0, pipeline=pipeline)
+    eng = Engine(T, P, device=dev, refill_period=REFILL_EVERY[P], table0=table0, pipeline=pipeline,
+                 partner_lead=partner_lead)
     eng.reset(seeds=range(table0, table0 + T))
     out = dict(obs=torch.zeros((K, T, 297), dtype=torch.int32, device=dev),
                mask=torch.zeros((K, T, 45), dtype=torch.int8, device=dev),
@@ -375,6 +385,7 @@ def c4_share_line(dev, rank, world, T, launches, warmup, pipeline=True):
         e.record(strm)
     torch.cuda.synchronize(dev)
     eps0 = int(ep_cnt.sum().item())
+    partner_stats(eng.lib, clear=True)
     barrier(dev)
     region_mark("config4_share", "start", eng.rollout_kernel_name(per_step=True), launches)
     t0 = time.perf_counter()
@@ -395,6 +406,7 @@ def c4_share_line(dev, rank, world, T, launches, warmup, pipeline=True):
     traffic, src = load_pmc_traffic(name, T, K)
     # the dealer kernel's hand-off faults (spl_ctx_faults) and error flags of the last launch's steps
     faults = eng.faults()
+    handoffs = partner_stats(eng.lib)
     bad = int(((out["flags"] & (_native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_FAULT)) != 0).sum().item())
     eng.close()
     achieved = algo / spread["median_s"] / 1e9
@@ -411,6 +423,8 @@ def c4_share_line(dev, rank, world, T, launches, warmup, pipeline=True):
                          "traffic": traffic, "traffic_source": src,
                          "traffic_over_algo": None if traffic is None else round(traffic / algo, 4)},
             "error_flags": bad, "launch_faults": faults,
+            "partner_handoffs": None if handoffs is None else dict(handoffs, launches=launches,
+                                                                   row_blocks_per_launch=K * T // 64),
             "config": {"workload": "4-player SplendorEnv.step, device uniform-random policy, same-step autoreset, "
                                    "per-step rollout store [128, T, ...]", "tables_per_gpu": T, "players": P}}
 
@@ -455,6 +469,9 @@ def main():
                     help="rollout store: every n-th step the odd-XCC workgroups' rows are stored by their "
                          "even-XCC partners (0 = off, the library default: a 1.5 %% gain, "
                          "profiles/r03/deleg_ab_r03a.txt)")
+    ap.add_argument("--partner-lead", type=int, default=None,
+                    help="six-wave dealer rollout store: a team this many steps behind its neighbouring-XCC "
+                         "partner hands it whole steps of rows (library default 2; 0 = off)")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -481,7 +498,7 @@ def main():
     pipe = {"auto": True, "always": "always", "half": "half", "off": False, "dealer": "dealer",
             "dealer2": "dealer2"}[args.pipeline]
     eng = Engine(T, P, device=dev, refill_period=R, table0=table0, refill_fused=args.refill == "fused",
-                 pipeline=pipe, delegation=args.delegation)
+                 pipeline=pipe, delegation=args.delegation, partner_lead=args.partner_lead)
     eng.reset(seeds=range(table0, table0 + T))
     lib = eng.lib
     buf = [torch.zeros(T, dtype=torch.int32, device=dev) for _ in range(2)]
@@ -645,13 +662,15 @@ def main():
         sp = selfplay_line(dev, rank, world, args.sp_tables, args.sp_iters, warmup=8)
     c4 = None
     if args.c4_tables > 0 and not args.only and args.players == 2:
-        c4 = c4_share_line(dev, rank, world, args.c4_tables, launches=8, warmup=2, pipeline=args.c4_pipeline)
+        c4 = c4_share_line(dev, rank, world, args.c4_tables, launches=8, warmup=2, pipeline=args.c4_pipeline,
+                           partner_lead=args.partner_lead)
     # correctness canaries on the measured run: no error flags, episodes completed
     errs = _native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT | _native.F_FAULT
     bad = int(((eng.flags & errs) != 0).sum().item())
     if store is not None:  # every step of the last rollout-store launch
         bad += int(((store["flags"] & errs) != 0).sum().item())
     faults = eng.faults()
+    handoffs = partner_stats(lib) if "dealer2" in kernel_name("rollout_store") else None
     rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
     episodes = int(cnts.sum().item())
 
@@ -736,6 +755,8 @@ def main():
             "error_flags": bad,
             "launch_faults": faults,
         }
+        if handoffs is not None:  # the six-wave dealer's partner hand-offs over this process (warm-up included)
+            out["partner_handoffs"] = handoffs
         for v in variants[1:]:
             s = with_traffic(summary(recs[v]))
             s.pop("plan")

@@ -44,7 +44,8 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 6  /* 6: SPL_F_FAULT + spl_ctx_faults (a lost hand-off in a rollout launch is reported);
+#define SPL_ABI_VERSION 7  /* 7: spl_ctx_set_partner_lead, spl_debug_partner_stats (six-wave dealer partner hand-off);
+                              6: SPL_F_FAULT + spl_ctx_faults (a lost hand-off in a rollout launch is reported);
                               5: spl_step_args_t.obs_u8 (compact observation), gate_terminated / gate_flags */
 
 /* ---- per-table flag bits (uint8) --------------------------------------------------- */
@@ -156,6 +157,13 @@ int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
  * Turned off for grids larger than the resident workgroup capacity (pairs might not run together).
  * Default: SPL_DELEG_EVERY (DESIGN.md §2 gives the measured A/B).  Results are identical either way. */
 int spl_ctx_set_rollout_delegation(spl_ctx_t *ctx, int every);
+/* Partner hand-off of the six-wave dealer rollout with per-step outputs (pipeline 5 /
+ * k_rollout_store_dealer2_*): a 64-table team that falls `lead` or more steps behind the same team of
+ * the workgroup on the neighbouring XCC hands whole steps of observation rows (its state words, ~6 KB)
+ * to that team's dealer wave, which encodes and stores them (the XCCs drain the rollout store at
+ * different rates under load).  0 = off, -1 = hand off whenever a slot is free (tests).
+ * Default SPL_PARTNER_LEAD (2).  Results are identical either way. */
+int spl_ctx_set_partner_lead(spl_ctx_t *ctx, int lead);
 /* The name of the kernel spl_rollout launches for n tables of `players` players under the context's
  * settings (e.g. "k_rollout_store_2p", "k_rollout_inplace_half_4p"): every instantiation has a name
  * of its own, so a rocprofv3 summary row maps to one variant.  NULL (spl_last_error) on bad input. */
@@ -246,6 +254,10 @@ int spl_debug_set_stream_limit(int outputs);
  * spl_ctx_faults; default and maximum 2^22, a fraction of a second; negative = default).  Process-wide,
  * current device.  0 makes the first wait that has to wait fault: tests force the fault path with it. */
 int spl_debug_set_spin_limit(int64_t polls);
+/* DIAGNOSTIC: partner hand-off tasks since the last clear, process-wide on the current device:
+ * stats[0] stored by the partner's dealer wave, stats[1] claimed back by the team that posted them.
+ * Synchronises the device; `clear` zeroes them. */
+int spl_debug_partner_stats(uint64_t *stats, int clear);
 
 /* TEST HOOK of the bounds-check build (libsplendor_amd_checked.so, -DSPL_BOUNDS_CHECK): the OR of the
  * invariant violations the kernels recorded (table / slot / deck / token-table / deal-scratch index,

@@ -174,6 +174,11 @@ constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 // that would pay for a cross-XCC hand-off in the headline kernel
 #define SPL_DELEG_EVERY 0
 #endif
+#ifndef SPL_PARTNER_LEAD
+// partner hand-off of the six-wave dealer rollout (spl_ctx_set_partner_lead): a team hands a step's
+// rows to its neighbouring-XCC partner when that one is this many steps ahead
+#define SPL_PARTNER_LEAD 2
+#endif
 #ifndef SPL_XCD_MAP
 #define SPL_XCD_MAP 1
 #endif
@@ -183,11 +188,12 @@ constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 // of the block (store-only pattern: 880 -> 844-862 us per 64 steps on one box,
 // tools/microbench_hbm_store.hip rows_x).  Only which workgroup steps which tables changes: every
 // table's chain is its own, so results are identical (A/B build switch SPL_XCD_MAP=0).
-__device__ __forceinline__ int wg_block() {
-    const uint32_t nb = gridDim.x, b = blockIdx.x;
+__device__ __forceinline__ int wg_block_of(uint32_t b) {
+    const uint32_t nb = gridDim.x;
     if (!SPL_XCD_MAP || (nb & 7u)) return (int)b;
     return (int)((b & 7u) * (nb >> 3) + (b >> 3));
 }
+__device__ __forceinline__ int wg_block() { return wg_block_of(blockIdx.x); }
 #ifndef SPL_STEP_OBS_NT
 #define SPL_STEP_OBS_NT false  // k_step_ws observation stores non-temporal (A/B switch)
 #endif
@@ -2394,6 +2400,107 @@ __device__ __forceinline__ Deal deal_of_lds(const DealerLDS &D, int lane) {
     return Deal{{D.rdeal[0][lane], D.rdeal[1][lane], D.rdeal[2][lane]}, D.rdeal[3][lane], D.rdeal[4][lane]};
 }
 
+// ---- partner hand-off (six-wave dealer rollout, per-step outputs; ctx partner_lead) -------------
+// Under the rollout store's write stream the XCCs do not keep the same pace: the C4 share's stamps put
+// the teams of one or two XCCs 7-16 % behind the rest (their observation-row stores issue slower;
+// without the row stores every XCC runs the same period, profiles/r04/wsstamps4_r04k.txt), and the
+// launch ends with the slowest team.  So a team that falls behind hands whole steps of observation
+// rows to the same team of the workgroup on the neighbouring XCC (blockIdx b ^ 1), whose OUTPUT wave
+// encodes and stores them between its own steps:
+//   * each side's output wave publishes its progress (steps done) every step and reads the partner's
+//     (sc1 words, one step stale); when the partner is `lead` or more steps ahead and the next task
+//     slot is free, the step's state words go to the slot (sc1 stores, ~6 KB) instead of the encode
+//     and the 76 KB row block, and the slot's flag turns READY(launch, step) after a vmcnt(0) at the
+//     top of the next step (the guide's drained-sc1 hand-off: sc1 payload, vmcnt(0), sc1 flag);
+//   * at the top of each step the partner's output wave looks at the flag of the next slot (loaded a
+//     step ahead) and takes at most one READY task: an agent-scope compare-and-swap READY -> TAKEN,
+//     the words loaded sc1, encoded and stored, the slot freed; after its own steps it keeps serving
+//     until the partner's DONE word shows (bounded by time: a partner that never finishes keeps its
+//     tasks);
+//   * at the end the producer posts DONE and claims back, by the same compare-and-swap, every task
+//     still READY, and stores those rows itself: each task's rows are stored once, by its flag's winner.
+// (The dealer wave as the consumer took too few tasks: a deal keeps it busy ~90 us at a time.)
+// Masks, small outputs and terminal rows stay with the producer; rows are encoded by the same code
+// from the same words, so results do not depend on who stores them.  Launch counters (one per side,
+// in the arena, zeroed with it; both sides count the same launches) tag every flag, so nothing from
+// an earlier launch or graph replay matches.
+struct PartnerLink {
+    bool on;
+    int side, lead;    // lead < 0: hand off whenever a slot is free (tests)
+    uint32_t e;        // this launch's counter value
+    uint32_t *fl;      // the pair's flag lines
+    uint8_t *pay;      // the pair's payload slots
+    int t0p;           // the partner team's first table
+    __device__ __forceinline__ uint32_t *line(int l) const { return fl + l * kFlagLine; }
+    __device__ __forceinline__ uint8_t *slot(int j) const { return pay + (size_t)j * kDelegPayload; }
+};
+constexpr uint32_t kPtReady = 1u, kPtTaken = 2u;
+constexpr uint64_t kPartnerWait = 500000;  // 5 ms of s_memrealtime (100 MHz): the consumer's wait for DONE
+__device__ __forceinline__ uint32_t pt_flag(uint32_t e, int k, uint32_t st) { return e << 16 | (uint32_t)k << 2 | st; }
+__device__ unsigned long long g_partner_stats[2];  // tasks stored by the partner / claimed back (diagnostics)
+
+// lane 0 moves a task flag READY -> TAKEN (agent scope: performed past the XCC's L2); wave-uniform
+__device__ __forceinline__ bool pt_claim(uint32_t *f, uint32_t ready) {
+    uint32_t seen = 0u;
+    if (lane_id() == 0) {
+        seen = ready;
+        __hip_atomic_compare_exchange_strong(f, &seen, (ready & ~3u) | kPtTaken, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return (uint32_t)__builtin_amdgcn_readfirstlane(seen) == ready;
+}
+// one task's rows: the staged words -> rows in LDS -> the row block (whole wave, 64 full rows)
+template <int P>
+__device__ __forceinline__ void pt_store_task(const uint8_t *slot, uint8_t *rows_lds, const Consts &C, int32_t *dst) {
+    Tab<P> T;
+    unstage_state(slot, T);
+    encode_row(T, rows_lds, C);
+    wave_lds_sync();
+    store_obs_block<64, true>(rows_lds, 64, dst);
+    wave_lds_sync();  // the block's LDS reads are done before the next task's rows land
+}
+// consumer (the partner team's output wave): `v` = the flag of the partner's slot cseq; if it is READY,
+// claim it and store the task's rows (staged through `rows`); true if the slot held a task
+template <int P>
+__device__ __forceinline__ bool pt_serve_v(const PartnerLink &pl, uint32_t &cseq, uint32_t v, uint8_t *rows,
+                                           const Consts &C, int32_t *obs, int n) {
+    if ((v & 3u) != kPtReady || (v >> 16) != pl.e) return false;
+    const int j = (pl.side ^ 1) * kPartnerSlots + (int)(cseq % kPartnerSlots);
+    ++cseq;  // tasks fill the ring in order: the next one is in the next slot, whoever stores this one
+    uint32_t *f = pl.line(pt_ready_line(j));
+    if (!pt_claim(f, v)) return true;
+    const int k = (int)((v >> 2) & 0x3FFFu);
+    pt_store_task<P>(pl.slot(j), rows, C, obs + ((size_t)k * (size_t)n + (size_t)pl.t0p) * kObsDim);
+    // the slot's words were read (the encode used them) before it is free again; no vmcnt wait: the
+    // rows' stores need not have completed
+    __asm__ volatile("" ::: "memory");
+    flag_store(f, 0u);
+    if (lane_id() == 0) atomicAdd(&g_partner_stats[0], 1ull);
+    return true;
+}
+__device__ __forceinline__ uint32_t pt_next_flag(const PartnerLink &pl, uint32_t cseq) {
+    return flag_load(pl.line(pt_ready_line((pl.side ^ 1) * kPartnerSlots + (int)(cseq % kPartnerSlots))));
+}
+// consumer, after its own steps: serve until the partner's DONE word shows (or kPartnerWait passes)
+template <int P>
+__device__ __forceinline__ void pt_drain(const PartnerLink &pl, uint32_t &cseq, uint8_t *rows, const Consts &C,
+                                         int32_t *obs, int n) {
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (pt_serve_v<P>(pl, cseq, (uint32_t)__builtin_amdgcn_readfirstlane(pt_next_flag(pl, cseq)), rows, C, obs, n))
+            continue;
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_readfirstlane(flag_load(pl.line(pt_done_line(pl.side ^ 1))));
+        if (dn == pl.e) {  // its READY flags were stored before DONE: what is left of them, then out
+            while (pt_serve_v<P>(pl, cseq, (uint32_t)__builtin_amdgcn_readfirstlane(pt_next_flag(pl, cseq)), rows, C,
+                                 obs, n)) {
+            }
+            return;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t_start > kPartnerWait) return;
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
 // The dealer wave: batches until the rules wave stops and none is left.  An idle wait that runs out
 // ends the dealer quietly: a batch posted after that is never dealt, so the rules wave's wait for it
 // runs out and faults the launch (lds_wait_ge).  A faulted workgroup's dealer ends after its batch.
@@ -2543,6 +2650,31 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
     if constexpr (kDealer) {  // the hand-off counters start at zero (LDS is not initialised)
         if (rules_wave && lane == 0) {
             L.dl.dreq = L.dl.ddone = L.dl.rdone = L.dl.odone = L.dl.stop = L.dl.abort = 0u;
+        }
+    }
+    // partner hand-off (six-wave dealer, per-step outputs; deleg_every = the lead in steps, 0 = off):
+    // team j of workgroups b and b ^ 1, both full, K < 2^14 (the step fits a flag)
+    PartnerLink pl{false, 0, deleg_every, 0u, nullptr, nullptr, 0};
+    if constexpr (kDealer && kStore) {
+        if (wr.block >= 0 && deleg_every != 0 && K < (1 << 14)) {
+            const uint32_t b = blockIdx.x, pb = b ^ 1u;
+            const int team = wr.block - 2 * wg_block();
+            const int t0p = (2 * wg_block_of(pb) + team) * 64;
+            const int pair = (int)(b >> 1) * 2 + team;
+            if (pb < gridDim.x && t0 + 64 <= A.n && t0p + 64 <= A.n && pair < A.n / 128) {
+                pl.on = true;
+                pl.side = (int)(b & 1u);
+                pl.t0p = t0p;
+                pl.fl = A.dflags + (size_t)pair * kDelegFlagWords;
+                pl.pay = A.deleg + (size_t)pair * kDelegTasks * kDelegPayload;
+            }
+        }
+        if (pl.on && role == 1) {  // this side's launch counter (the output wave is both sides' party)
+            uint32_t *el = pl.line(pt_epoch_line(pl.side));
+            uint32_t e = ((uint32_t)__builtin_amdgcn_readfirstlane(flag_load(el)) + 1u) & 0xFFFFu;
+            e = e == 0u ? 1u : e;
+            flag_store(el, e);
+            pl.e = e;
         }
     }
     ws_sync();
@@ -2709,7 +2841,26 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         auto slot_of = [&](int j) { return A.deleg + ((size_t)dl.pair * kDelegTasks + j) * kDelegPayload; };
         int pend = -1, pend_k = -1;  // producer: task staged at step pend_k, ready flag not yet set
         uint32_t staged = 0u;        // producer: tasks staged (not stored here)
+        // partner hand-off, producer side: tasks posted, the one staged but not yet READY, and the
+        // partner's progress and this side's next slot flag (loaded one step ahead)
+        // consumer side: the partner's tasks seen and the flag of its next slot (loaded a step ahead)
+        uint32_t pseq = 0u, pprog = 0u, pslot = 0u, cseq = 0u, pnext = 0u;
+        int ppend = -1, ppend_k = 0;
+        if (pl.on) {
+            pprog = flag_load(pl.line(pt_progress_line(pl.side ^ 1)));
+            pslot = flag_load(pl.line(pt_ready_line(pl.side * kPartnerSlots)));
+            pnext = pt_next_flag(pl, 0u);
+        }
         for (int k = 0; k < K; ++k) {
+            if (pl.on) {
+                if (ppend >= 0) {  // the task staged last step: its words have completed, then READY
+                    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                    flag_store(pl.line(pt_ready_line(ppend)), pt_flag(pl.e, ppend_k, kPtReady));
+                    ppend = -1;
+                }
+                // at most one of the partner's tasks per step, between this team's steps
+                pt_serve_v<P>(pl, cseq, (uint32_t)__builtin_amdgcn_readfirstlane(pnext), L.rows, L, S.obs, A.n);
+            }
             if constexpr (kDealer) {
                 if (!lds_wait_ge(L.dl, &L.dl.rdone, (uint32_t)(k + 1))) {  // hand-off of step k
                     // steps k.. are not stored: their flags say so (the blocks keep stale rows)
@@ -2741,13 +2892,27 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             }
             const bool big_moves = __any(valid && get_moves(T.sw) > 255);
             const bool deleg_now = dl.producer && deleg_step(k, K, dl.every);
-            if (!deleg_now || big_moves) {  // a delegated step's rows are encoded by the partner
+            bool handed = false;  // partner hand-off of this step's rows
+            if (pl.on && !big_moves) {
+                const uint32_t pp = (uint32_t)__builtin_amdgcn_readfirstlane(pprog);
+                const uint32_t sf = (uint32_t)__builtin_amdgcn_readfirstlane(pslot);
+                const bool ahead = pl.lead < 0 || ((pp >> 16) == pl.e && (int)(pp & 0xFFFFu) >= k + pl.lead);
+                handed = ahead && ((sf & 3u) == 0u || (sf >> 16) != pl.e);  // the slot is free (or stale)
+            }
+            if (handed) {
+                const int j = pl.side * kPartnerSlots + (int)(pseq % kPartnerSlots);
+                stage_state(T, pl.slot(j));
+                ppend = j;
+                ppend_k = k;
+                ++pseq;
+            } else if (!deleg_now || big_moves) {  // a delegated step's rows are encoded by the partner
                 encode_row(T, L.rows, L);
                 wave_lds_sync();
             }
             WSSTAMP(1, k);
             int32_t *obs = S.obs + blk * kObsDim;
-            if (deleg_now) {
+            if (handed) {
+            } else if (deleg_now) {
                 const int j = k / dl.every;
                 if (big_moves) {  // a patched row: stored here, the partner skips the task
                     store_obs_block<TPW, true>(L.rows, rows, obs + (size_t)t0 * kObsDim);
@@ -2799,7 +2964,39 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                     L.dl.rnd[b][lane] = uniform_draw(S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)(k + 2));
                 lds_publish(&L.dl.odone, (uint32_t)(k + 1));  // slot b is free again
             }
+            if (pl.on) {  // progress out; the partner's and the next slot's flag in, for the next decision
+                flag_store(pl.line(pt_progress_line(pl.side)), pl.e << 16 | (uint32_t)(k + 1));
+                pprog = flag_load(pl.line(pt_progress_line(pl.side ^ 1)));
+                pslot = flag_load(pl.line(pt_ready_line(pl.side * kPartnerSlots + (int)(pseq % kPartnerSlots))));
+                pnext = pt_next_flag(pl, cseq);
+            }
             WSSTAMP(3, k);
+        }
+        if (pl.on) {
+            if (ppend >= 0) {
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+                flag_store(pl.line(pt_ready_line(ppend)), pt_flag(pl.e, ppend_k, kPtReady));
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // every READY flag has completed before DONE
+            flag_store(pl.line(pt_done_line(pl.side)), pl.e);
+            if (pseq > 0u) {  // claim back the tasks the partner has not taken, and store them here
+                uint32_t mine = 0u;  // lane j: slot j's flag (relaxed agent load: global_load sc1)
+                if (lane < kPartnerSlots)
+                    mine = __hip_atomic_load(pl.line(pt_ready_line(pl.side * kPartnerSlots + lane)), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                uint64_t rm = __ballot(lane < kPartnerSlots && (mine & 3u) == kPtReady && (mine >> 16) == pl.e);
+                for (; rm; rm &= rm - 1) {
+                    const int j = __ffsll((unsigned long long)rm) - 1;
+                    const uint32_t vj = (uint32_t)__builtin_amdgcn_readlane((int)mine, j);
+                    uint32_t *f = pl.line(pt_ready_line(pl.side * kPartnerSlots + j));
+                    if (!pt_claim(f, vj)) continue;
+                    const int kk = (int)((vj >> 2) & 0x3FFFu);
+                    pt_store_task<P>(pl.slot(pl.side * kPartnerSlots + j), L.rows, L,
+                                     S.obs + ((size_t)kk * (size_t)A.n + (size_t)t0) * kObsDim);
+                    if (lane == 0) atomicAdd(&g_partner_stats[1], 1ull);
+                }
+            }
+            pt_drain<P>(pl, cseq, L.rows, L, S.obs, A.n);  // then the partner's, until it is done
         }
 #ifdef SPL_STAMPS
         if (g_wsend && lane == 0) g_wsend[sid * 2 + 0] = __builtin_amdgcn_s_memrealtime();
@@ -2970,7 +3167,8 @@ __device__ __forceinline__ int dealer2_assign(const uint32_t (&simd)[6], int w) 
 }
 
 template <int P, bool kStore>
-__device__ __forceinline__ void rollout_dealer2(WsDeal2LDS<P> &L, KArena A, KTables Tb, KStep S, int K, int refill) {
+__device__ __forceinline__ void rollout_dealer2(WsDeal2LDS<P> &L, KArena A, KTables Tb, KStep S, int K, int refill,
+                                                int lead) {
     const int w = (int)(threadIdx.x >> 6);
     if (lane_id() == 0) L.simd[w] = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;
     __syncthreads();
@@ -2979,15 +3177,14 @@ __device__ __forceinline__ void rollout_dealer2(WsDeal2LDS<P> &L, KArena A, KTab
     for (int i = 0; i < 6; ++i) simd[i] = __builtin_amdgcn_readfirstlane(L.simd[i]);
     const int code = __builtin_amdgcn_readfirstlane(dealer2_assign(simd, w));
     const int team = code / 3;
-    rollout_ws<P, 64, kStore, true>(L.team[team], A, Tb, S, K, refill, 0, WaveRole{code % 3, 2 * wg_block() + team});
+    rollout_ws<P, 64, kStore, true>(L.team[team], A, Tb, S, K, refill, lead, WaveRole{code % 3, 2 * wg_block() + team});
 }
 template <int P, bool kStore>
 struct RolloutDealer2Kernel;
 #define SPL_DEALER2_KERNEL(NAME, P_, ST_)                                                                      \
     __global__ __launch_bounds__(384) void NAME(KArena A, KTables Tb, KStep S, int K, int refill, int deleg) { \
         __shared__ WsDeal2LDS<P_> L;                                                                           \
-        (void)deleg;                                                                                           \
-        rollout_dealer2<P_, ST_>(L, A, Tb, S, K, refill);                                                      \
+        rollout_dealer2<P_, ST_>(L, A, Tb, S, K, refill, deleg);                                               \
     }                                                                                                          \
     template <>                                                                                                \
     struct RolloutDealer2Kernel<P_, ST_> {                                                                     \
@@ -3300,6 +3497,7 @@ struct spl_ctx_s {
     int dealer_resident[5];  // k_rollout_store_dealer_<P>p: the same for the three-wave dealer variant
     int dealer2_resident[5]; // k_rollout_store_dealer2_<P>p: the same for the six-wave dealer variant
     int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
+    int partner_lead;    // six-wave dealer per-step store: partner hand-off lead in steps (0 off, < 0 forced)
     uint64_t *fault_host;  // host-mapped, fine-grained: the serial of a launch that faulted (0 = none), spl_ctx_faults
     uint64_t *fault_dev;   // its device address (KStep::fault)
     uint64_t launches;     // launch serial (KStep::fault_tag)
@@ -3484,6 +3682,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     c->refill_period = 64;
     c->refill_fused = 1;
     c->deleg_every = SPL_DELEG_EVERY;
+    c->partner_lead = SPL_PARTNER_LEAD;
     c->pipeline = 1;
     memcpy(c->ws_resident, ws_resident, sizeof(ws_resident));
     memcpy(c->dealer_resident, dealer_resident, sizeof(dealer_resident));
@@ -3553,6 +3752,26 @@ int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on) {
     if (!ctx) return fail(SPL_E_ARG, "null ctx");
     if (on < 0 || on > 5) return fail(SPL_E_ARG, "rollout pipeline must be 0..5");
     ctx->pipeline = on;
+    return SPL_OK;
+}
+
+int spl_ctx_set_partner_lead(spl_ctx_t *ctx, int lead) {
+    if (!ctx || lead < -1 || lead > 64) return fail(SPL_E_ARG, "partner lead must be in [-1, 64]");
+    ctx->partner_lead = lead;
+    return SPL_OK;
+}
+
+int spl_debug_partner_stats(uint64_t *stats, int clear) {
+    if (!stats) return fail(SPL_E_ARG, "stats must be non-null");
+    unsigned long long v[2] = {0ull, 0ull};
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_partner_stats), sizeof(v)));
+    stats[0] = v[0];
+    stats[1] = v[1];
+    if (clear) {
+        const unsigned long long z[2] = {0ull, 0ull};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_partner_stats), z, sizeof(z)));
+    }
     return SPL_OK;
 }
 
@@ -3783,7 +4002,7 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
         const unsigned blocks = (unsigned)((arena->n + 127) / 128);
         DISPATCH_P(arena->players, if (p_out) {
             hipLaunchKernelGGL((RolloutDealer2Kernel<PP, true>::fn), dim3(blocks), dim3(384), 0, s, A, ktables(ctx), S,
-                               (int)steps, fused, 0);
+                               (int)steps, fused, ctx->partner_lead);
         } else {
             hipLaunchKernelGGL((RolloutDealer2Kernel<PP, false>::fn), dim3(blocks), dim3(384), 0, s, A, ktables(ctx), S,
                                (int)steps, fused, 0);

@@ -81,6 +81,17 @@ constexpr int kFlagLine = 32;            // u32 words per flag
 enum : int { DF_PROD_EPOCH = 0, DF_CONS_EPOCH = 1, DF_TASKS = 2 };  // + 2 * task + {0 ready, 1 taken}
 constexpr int kDelegFlagWords = (DF_TASKS + 2 * kDelegTasks) * kFlagLine;
 
+// Partner hand-off of the six-wave dealer rollout (k_rollout_store_dealer2_*; see the kernel): team j of
+// workgroups 2q and 2q+1 (XCCs x and x^1) share pair (q*2 + j) of the same arena lines and slots.  Side s
+// (0: workgroup 2q) posts into task slots [s*kPartnerSlots, (s+1)*kPartnerSlots); its launch counter is
+// line DF_PROD_EPOCH + s, its progress and done words the taken lines of its first two slots.
+constexpr int kPartnerSlots = 12;
+static_assert(2 * kPartnerSlots <= kDelegTasks, "both sides' partner slots fit the delegation slots");
+__host__ __device__ constexpr int pt_ready_line(int slot) { return DF_TASKS + 2 * slot; }
+__host__ __device__ constexpr int pt_progress_line(int side) { return DF_TASKS + 2 * (side * kPartnerSlots) + 1; }
+__host__ __device__ constexpr int pt_done_line(int side) { return DF_TASKS + 2 * (side * kPartnerSlots + 1) + 1; }
+__host__ __device__ constexpr int pt_epoch_line(int side) { return DF_PROD_EPOCH + side; }
+
 struct ArenaLayout {
     int64_t planes, pool, slots, pcg, deleg, dflags, total;
 };

@@ -33,7 +33,7 @@ class Engine:
     DEFAULT_REFILL = {2: 64, 3: 32, 4: 16}
 
     def __init__(self, num_tables, num_players=2, device=None, refill_period=None, table0=0, refill_fused=True,
-                 pipeline=True, delegation=None, cards=None):
+                 pipeline=True, delegation=None, cards=None, partner_lead=None):
         torch = _native.require_gpu()
         self.torch = torch
         self.lib = _native.load_library()
@@ -45,7 +45,7 @@ class Engine:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
-        self._settings = (refill_period, refill_fused, pipeline, delegation)
+        self._settings = (refill_period, refill_fused, pipeline, delegation, partner_lead)
         self.ctx = None
         self._fault_carry = 0  # a fault seen on a context replaced by set_card_table
         self._create_ctx(cards)
@@ -90,7 +90,7 @@ class Engine:
         # the context's fault word (host-mapped; the kernels write a faulting launch's serial there)
         self._fault_word = ctypes.c_uint64.from_address(self.lib.spl_ctx_fault_word(ctx))
         self.custom_cards = None if cards is None else tbl.copy()
-        refill_period, refill_fused, pipeline, delegation = self._settings
+        refill_period, refill_fused, pipeline, delegation, partner_lead = self._settings
         num_players = self.P
         if refill_period is None:
             refill_period = self.DEFAULT_REFILL.get(int(num_players), 16)
@@ -104,6 +104,11 @@ class Engine:
         # their even-XCC partners (None = the library default, 0 = off); same results
         if delegation is not None:
             check(self.lib, self.lib.spl_ctx_set_rollout_delegation(self.ctx, int(delegation)))
+        # rollout() of the six-wave dealer into a per-step store: a team this many steps behind its
+        # neighbouring-XCC partner hands it whole steps of rows (None = library default, 0 = off,
+        # -1 = whenever a slot is free); same results
+        if partner_lead is not None:
+            check(self.lib, self.lib.spl_ctx_set_partner_lead(self.ctx, int(partner_lead)))
 
     def set_card_table(self, cards=None):
         """Evaluate the tables from now on with card table `cards` (int32 [90, 8]; None = canonical):

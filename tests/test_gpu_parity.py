@@ -284,10 +284,15 @@ def test_rollout_equals_step_chain(P, K, refill_fused, pipeline, R):
     pipelined kernel (32 or 64 tables per workgroup), the three-wave dealer variant (the auto choice
     at this size: a third wave deals the refills, spent pools post a batch and wait) or one wave per
     64 tables."""
+    _check_rollout_vs_chain(P, K, refill_fused, pipeline, R)
+
+
+def _check_rollout_vs_chain(P, K, refill_fused, pipeline, R, partner_lead=None, launches=None):
     import torch
-    n, launches, seed = 1024, 5 if K <= 16 else 3, 11
+    n, seed = 1024, 11
+    launches = launches or (5 if K <= 16 else 3)
     chain = engine(n, P, refill_period=R)
-    fused = engine(n, P, refill_period=R, refill_fused=refill_fused, pipeline=pipeline)
+    fused = engine(n, P, refill_period=R, refill_fused=refill_fused, pipeline=pipeline, partner_lead=partner_lead)
     chain.reset(seeds=range(n))
     fused.reset(seeds=range(n))
     dev = chain.device
@@ -336,6 +341,28 @@ def test_rollout_equals_step_chain(P, K, refill_fused, pipeline, R):
     for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
         assert torch.equal(getattr(chain, name), getattr(fused, name)), name
     assert torch.equal(a_c, na_f)
+    return fused
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,lead", [(4, -1), (2, -1), (4, 2), (3, 1)])
+def test_dealer2_partner_handoff_equals_step_chain(P, lead):
+    """The six-wave dealer rollout's partner hand-off (spl_ctx_set_partner_lead): with lead -1 every
+    team hands its steps' rows to the same team of the neighbouring-XCC workgroup whenever a task slot
+    is free, so the partner's output wave encodes and stores many row blocks between its own steps (and
+    the poster claims back what is left at the end); every per-step output still equals the chained
+    spl_step bit for bit, and the diagnostic counters show the hand-offs happened.  Lead 1-2: hand-offs
+    only when a partner runs ahead (timing-dependent; same results either way)."""
+    import ctypes
+    from splendor_gym import _native
+    st = (ctypes.c_uint64 * 2)()
+    probe = engine(128, 2)
+    _native.check(probe.lib, probe.lib.spl_debug_partner_stats(st, 1))
+    fused = _check_rollout_vs_chain(P, 64, True, "dealer2", 16, partner_lead=lead, launches=3)
+    assert fused.rollout_kernel_name() == f"k_rollout_store_dealer2_{P}p"
+    _native.check(fused.lib, fused.lib.spl_debug_partner_stats(st, 1))
+    if lead < 0:
+        assert st[0] > 0, (st[0], st[1])  # the partners stored handed-off blocks
 
 
 @pytest.mark.parametrize("pipeline", [True, "always", False])

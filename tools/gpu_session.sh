@@ -1,9 +1,10 @@
 #!/bin/bash
-# One GPU session (round 3).  Steps by name, run in order; each GPU step has its own time limit and
+# One GPU session (rounds 3-4).  Steps by name, run in order; each GPU step has its own time limit and
 # the chain stops at the first failure.
 #   tools/gpu_session.sh TAG step [step ...]
-# steps: tests faults steptests smoke driver prof deleg profc4 pmcc4 multi pmc2p pmcmulti pmcstep stamps selfplay spprof
-#        poolsize vec policy stepmode rank2 bench poltests abl32
+# steps: tests faults steptests smoke driver prof deleg profc4 pmcc4 multi pmc2p pmcmulti pmcstep pmcfinal stamps
+#        wsstamps4 wsstamps4noobs wsstamps4gather selfplay spprof poolsize vec policy stepmode rank2 bench poltests
+#        pmcpol bench4 c4ab abl32 tanhab poltest1
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -58,9 +59,27 @@ for step in "$@"; do
                    tests/test_gpu_opponent_pool.py -x -v --timeout 200 --timeout-method thread ;;
     spprof) bash tools/gpu_sp_prof.sh || exit 1 ;;
     poolsize) for ps in 0 1 3 6 12; do run sps_$ps 200 python3 tools/bench_selfplay.py --opponent pool --pool-size $ps; done ;;
+    pmcfinal)  # HBM traffic (FETCH_SIZE, WRITE_SIZE passes) of every kernel bench.py's lines quote, final tree
+      bash tools/pmc.sh ${TAG}_2p 2 65536 store traffic || exit 1
+      bash tools/pmc.sh ${TAG}_4p_32768 4 32768 store traffic || exit 1
+      bash tools/pmc.sh ${TAG}_2p_step 2 65536 step traffic || exit 1 ;;
+    partnertests) run pytest_partner 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_faults.py \
+                      -k "partner or dealer2" -x -v --timeout 200 --timeout-method thread ;;
+    partnerab)  # the C4 share (4p x 32768, six-wave dealer) with the partner hand-off off / lead 2 / lead 4, alternating
+      for i in 1 2; do for ld in 0 2 4; do
+        run c4_lead${ld}_$i 300 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 --only --partner-lead $ld
+      done; done ;;
     pmcstep) bash tools/pmc.sh ${TAG}_2p_step 2 65536 step all || exit 1 ;;
     stamps) run stamps 300 python3 tools/stamps.py --run ;;
-    wsstamps4) WS_P=4 WS_T=32768 run wsstamps4 300 python3 tools/wsstamps.py --run ;;
+    wsstamps4) WS_P=4 WS_T=32768 WS_RAW=$O/wsstamps4_raw_$TAG.npz run wsstamps4 300 python3 tools/wsstamps.py --run ;;
+    wsstamps4lead)  # partner hand-off off / on (lead 2), the same stamps
+      WS_LEAD=0 WS_P=4 WS_T=32768 WS_RAW=$O/wsstamps4lead0_raw_$TAG.npz run wsstamps4lead0 300 python3 tools/wsstamps.py --run
+      WS_LEAD=2 WS_P=4 WS_T=32768 WS_RAW=$O/wsstamps4lead2_raw_$TAG.npz run wsstamps4lead2 300 python3 tools/wsstamps.py --run ;;
+    wsstamps4noobs)  # the same without the observation stores (-DSPL_ABL=1024): is the odd-XCC lag the store path?
+      WS_P=4 WS_T=32768 WS_RAW=$O/wsstamps4noobs_raw_$TAG.npz run wsstamps4noobs 300 python3 tools/wsstamps.py --run --lib splendor-gym_amd/ablate/lib_wsstamps_noobs.so ;;
+    wsstamps4gather)  # the same with the deck-top / LUT gathers replaced by constants (-DSPL_ABL=16384 / 32768)
+      WS_P=4 WS_T=32768 run wsstamps4nodeck 300 python3 tools/wsstamps.py --run --lib splendor-gym_amd/ablate/lib_wsstamps_nodeck.so
+      WS_P=4 WS_T=32768 run wsstamps4nolut 300 python3 tools/wsstamps.py --run --lib splendor-gym_amd/ablate/lib_wsstamps_nolut.so ;;
     wsstamps2) run wsstamps2 300 python3 tools/wsstamps.py --run ;;
     stepab) run bench_step 300 python3 bench.py --mode step --only --no-cpu-baseline --sp-tables 0 ;;
     abl2)  # actor timing ablation: no ring streaming (one weight chunk; wrong results by design)

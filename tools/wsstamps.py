@@ -23,7 +23,8 @@ from splendor_gym import _native
 from splendor_gym.device import Engine
 inplace = sys.argv[2] == "1"
 T, K, P = int(os.environ.get("WS_T", "65536")), 64, int(os.environ.get("WS_P", "2"))
-e = Engine(T, P, device="cuda:0", refill_period={2: 64, 3: 32, 4: 16}[P])
+lead = os.environ.get("WS_LEAD")  # partner hand-off lead of the six-wave dealer (None = library default)
+e = Engine(T, P, device="cuda:0", refill_period={2: 64, 3: 32, 4: 16}[P], partner_lead=None if lead is None else int(lead))
 e.lib.spl_debug_set_ws_stamps.argtypes = [ctypes.c_void_p]
 e.reset(seeds=range(T))
 buf = [torch.zeros(T, dtype=torch.int32, device=e.device) for _ in range(2)]
@@ -125,6 +126,7 @@ def main():
     e_last = end[-1]
     print("XCC of wg (blockIdx % 8 -> xcc):", [int(np.bincount(xcc[np.arange(nwg) % 8 == x, 0] & 15).argmax()) for x in range(8)])
     print("mean end by XCC: " + " ".join(f"{e_last[(xcc[:, 0] & 15) == x].mean():.0f}" for x in range(8)))
+    print("mean step-0 start by XCC: " + " ".join(f"{us(R[-1, (xcc[:, 0] & 15) == x, 0, 0]).mean():.1f}" for x in range(8)))
     print("s_memtime rate (GHz) by XCC: " + " ".join(f"{ghz[(xcc[:, 0] & 15) == x].mean():.3f}" for x in range(8)))
     pair = simd[:, 0] * 4 + simd[:, 1]
     print("(rules SIMD, output SIMD) counts / mean end: " + "; ".join(
@@ -147,12 +149,25 @@ def main():
            "refill/final/autoreset": (R[..., 4:63, 7] - R[..., 4:63, 1]), "policy+prefetch+LDS": (R[..., 4:63, 2] - R[..., 4:63, 7])}
     print("rules-wave sub-phases, steps 4..62, median/mean us: " + "; ".join(
         f"{k} {np.median(us(v[ok])):.2f}/{us(v[ok]).mean():.2f}" for k, v in sub.items()))
-    # per XCC (blockIdx % 8 is the XCC, checked above): where the rules wave's time goes
+    xs = xcc[:, 0] & 15
+    for par in (0, 1):  # even / odd XCCs: where the rules wave's extra time goes
+        sel = (xs % 2 == par)[None, :, None] & ok
+        print(f"  {'even' if par == 0 else 'odd '} XCCs sub-phase means: " + "; ".join(
+            f"{k.strip()} {us(v[sel]).mean():.2f}" for k, v in sub.items()))
+    raw = os.environ.get("WS_RAW")
+    if raw:  # the raw stamps for offline analysis
+        np.savez_compressed(raw, runs=runs, hws=hws, clks=clks, ends=ends)
+    # per XCC (from HW_ID/XCC_ID): where the rules wave's time goes
+    xcd = xcc[:, 0] & 15  # the XCC each stamp slot's rules wave ran on (last launch; the map is static)
     rs = us(R[..., 4:63, 1] - R[..., 4:63, 0])  # [run, wg, step]
     tl = us(R[..., 4:63, 2] - R[..., 4:63, 1])
     enc = us(O[..., 4:63, 1] - O[..., 4:63, 0])
     ost = us(O[..., 4:63, 2] - O[..., 4:63, 1])
-    for name, v in (("rules", rs), ("tail", tl), ("out encode", enc), ("out obs st", ost)):
+    rw = us(R[..., 4:63, 3] - R[..., 4:63, 2])
+    ow = us(O[..., 5:64, 0] - O[..., 4:63, 3])
+    per = us(R[..., 5:64, 0] - R[..., 4:63, 0])
+    for name, v in (("rules", rs), ("tail", tl), ("rules wait", rw), ("out encode", enc), ("out obs st", ost),
+                    ("out wait", ow), ("period", per)):
         print(f"per-step {name:10s} by XCC mean/p90/p99: " + " | ".join(
             f"{v[:, xcd == x].mean():.2f}/{np.percentile(v[:, xcd == x], 90):.1f}/{np.percentile(v[:, xcd == x], 99):.1f}"
             for x in range(8)))
