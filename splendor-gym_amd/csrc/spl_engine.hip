@@ -176,8 +176,11 @@ constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 #endif
 #ifndef SPL_PARTNER_LEAD
 // partner hand-off of the six-wave dealer rollout (spl_ctx_set_partner_lead): a team hands a step's
-// rows to its neighbouring-XCC partner when that one is this many steps ahead
-#define SPL_PARTNER_LEAD 2
+// rows to its neighbouring-XCC partner when that one is this many steps ahead.  Off by default: on
+// the C4 share it evened the XCCs' ends but made every team slower (the per-step flag loads wait
+// behind the output wave's own row stores in vmcnt): lead 0 / 2 / 4 medians 1 069-1 083 / 1 075-1 082 /
+// 1 080-1 087 us per launch, stamps max end 480-498 vs 499-517 us (profiles/r04/partner_ab_r04n.txt)
+#define SPL_PARTNER_LEAD 0
 #endif
 #ifndef SPL_XCD_MAP
 #define SPL_XCD_MAP 1
