@@ -471,7 +471,7 @@ def main():
                          "profiles/r03/deleg_ab_r03a.txt)")
     ap.add_argument("--partner-lead", type=int, default=None,
                     help="six-wave dealer rollout store: a team this many steps behind its neighbouring-XCC "
-                         "partner hands it whole steps of rows (library default 0 = off)")
+                         "partner hands it whole steps of rows (library default 2; 0 = off)")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))

@@ -162,7 +162,7 @@ int spl_ctx_set_rollout_delegation(spl_ctx_t *ctx, int every);
  * the workgroup on the neighbouring XCC hands whole steps of observation rows (its state words, ~6 KB)
  * to that team's dealer wave, which encodes and stores them (the XCCs drain the rollout store at
  * different rates under load).  0 = off, -1 = hand off whenever a slot is free (tests).
- * Default SPL_PARTNER_LEAD (0: off; DESIGN.md §2 gives the measured A/B).  Results are identical either way. */
+ * Default SPL_PARTNER_LEAD (2; DESIGN.md §2 gives the measured A/B).  Results are identical either way. */
 int spl_ctx_set_partner_lead(spl_ctx_t *ctx, int lead);
 /* The name of the kernel spl_rollout launches for n tables of `players` players under the context's
  * settings (e.g. "k_rollout_store_2p", "k_rollout_inplace_half_4p"): every instantiation has a name

@@ -176,11 +176,12 @@ constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 #endif
 #ifndef SPL_PARTNER_LEAD
 // partner hand-off of the six-wave dealer rollout (spl_ctx_set_partner_lead): a team hands a step's
-// rows to its neighbouring-XCC partner when that one is this many steps ahead.  Off by default: on
-// the C4 share it evened the XCCs' ends but made every team slower (the per-step flag loads wait
-// behind the output wave's own row stores in vmcnt): lead 0 / 2 / 4 medians 1 069-1 083 / 1 075-1 082 /
-// 1 080-1 087 us per launch, stamps max end 480-498 vs 499-517 us (profiles/r04/partner_ab_r04n.txt)
-#define SPL_PARTNER_LEAD 0
+// rows to its neighbouring-XCC partner when that one is this many steps ahead.  With the flag words
+// polled by the dealer wave (not the output wave, whose loads would wait behind its own row stores),
+// lead 2 against off, arms alternating on two boxes: median launch 1 075-1 082 vs 1 095-1 104 us, run
+// throughput +0.8 / +2.7 % (profiles/r04/partner_ab_r04u.txt); the first form, polling from the output
+// wave, was slower than off (partner_ab_r04n.txt)
+#define SPL_PARTNER_LEAD 2
 #endif
 #ifndef SPL_XCD_MAP
 #define SPL_XCD_MAP 1
@@ -2350,6 +2351,12 @@ struct DealerLDS {
     uint32_t stop;            // rules wave: no more batches
     uint32_t rnd[2][64];      // the uniform policy's words of step k in slot k & 1, drawn by the output wave at step k - 2
     uint32_t abort;           // a wait ran out (lds_wait_ge): every later wait returns at once
+    // partner hand-off (six-wave dealer): the dealer wave polls the pair's flag words between batches so
+    // the output wave never waits on a global load behind its own row stores (one in-order vmcnt)
+    uint32_t pepoch;          // output wave -> dealer: this launch's counter
+    uint32_t pt_seq[2];       // output wave -> dealer: tasks posted (pseq), partner tasks seen (cseq)
+    uint64_t pt_in[3];        // dealer -> output wave: partner progress; pseq << 32 | my next slot's flag;
+                              // cseq << 32 | the partner's next slot's flag
 };
 template <int P>
 struct __align__(16) WsDealLDS : WsLDS<P> {
@@ -2411,18 +2418,22 @@ __device__ __forceinline__ Deal deal_of_lds(const DealerLDS &D, int lane) {
 // rows to the same team of the workgroup on the neighbouring XCC (blockIdx b ^ 1), whose OUTPUT wave
 // encodes and stores them between its own steps:
 //   * each side's output wave publishes its progress (steps done) every step and reads the partner's
-//     (sc1 words, one step stale); when the partner is `lead` or more steps ahead and the next task
-//     slot is free, the step's state words go to the slot (sc1 stores, ~6 KB) instead of the encode
+//     from its dealer's snapshot; when the partner is `lead` or more steps ahead and the next task
+//     slot is free (by a snapshot of that slot's flag), the step's state words go to the slot (sc1 stores, ~6 KB) instead of the encode
 //     and the 76 KB row block, and the slot's flag turns READY(launch, step) after a vmcnt(0) at the
 //     top of the next step (the guide's drained-sc1 hand-off: sc1 payload, vmcnt(0), sc1 flag);
-//   * at the top of each step the partner's output wave looks at the flag of the next slot (loaded a
-//     step ahead) and takes at most one READY task: an agent-scope compare-and-swap READY -> TAKEN,
+//   * at the top of each step the partner's output wave looks at the snapshot of the next slot's flag
+//     and takes at most one READY task: an agent-scope compare-and-swap READY -> TAKEN,
 //     the words loaded sc1, encoded and stored, the slot freed; after its own steps it keeps serving
 //     until the partner's DONE word shows (bounded by time: a partner that never finishes keeps its
 //     tasks);
 //   * at the end the producer posts DONE and claims back, by the same compare-and-swap, every task
 //     still READY, and stores those rows itself: each task's rows are stored once, by its flag's winner.
-// (The dealer wave as the consumer took too few tasks: a deal keeps it busy ~90 us at a time.)
+// (The dealer wave as the consumer took too few tasks: a deal keeps it busy ~90 us at a time.  It does
+// poll the pair's flag words for its output wave between batches (pt_poll: LDS snapshots tagged with
+// the sequence numbers they are for), so that the output wave issues no global load it must wait for
+// behind its own row stores in the one in-order vmcnt; polled by the output wave itself, the hand-off
+// made every team slower than it won.)
 // Masks, small outputs and terminal rows stay with the producer; rows are encoded by the same code
 // from the same words, so results do not depend on who stores them.  Launch counters (one per side,
 // in the arena, zeroed with it; both sides count the same launches) tag every flag, so nothing from
@@ -2507,8 +2518,29 @@ __device__ __forceinline__ void pt_drain(const PartnerLink &pl, uint32_t &cseq, 
 // The dealer wave: batches until the rules wave stops and none is left.  An idle wait that runs out
 // ends the dealer quietly: a batch posted after that is never dealt, so the rules wave's wait for it
 // runs out and faults the launch (lds_wait_ge).  A faulted workgroup's dealer ends after its batch.
+// the dealer wave's poll of the pair's words for its output wave (a snapshot; tags say which slots)
+__device__ __forceinline__ void pt_poll(DealerLDS &D, const PartnerLink &pl) {
+    const uint32_t ps = lds_poll(&D.pt_seq[0]), cs = lds_poll(&D.pt_seq[1]);
+    const uint32_t a = flag_load(pl.line(pt_progress_line(pl.side ^ 1)));
+    const uint32_t b = flag_load(pl.line(pt_ready_line(pl.side * kPartnerSlots + (int)(ps % kPartnerSlots))));
+    const uint32_t c = flag_load(pl.line(pt_ready_line((pl.side ^ 1) * kPartnerSlots + (int)(cs % kPartnerSlots))));
+    const uint32_t ra = (uint32_t)__builtin_amdgcn_readfirstlane(a), rb = (uint32_t)__builtin_amdgcn_readfirstlane(b),
+                   rc = (uint32_t)__builtin_amdgcn_readfirstlane(c);
+    if (lane_id() == 0) {
+        __hip_atomic_store(&D.pt_in[0], (uint64_t)ra, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&D.pt_in[1], (uint64_t)ps << 32 | rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&D.pt_in[2], (uint64_t)cs << 32 | rc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+__device__ __forceinline__ uint64_t lds_poll64(const uint64_t *p) {
+    const uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32;
+}
+
 template <int P>
-__device__ __forceinline__ void dealer_loop(DealerLDS &D, const KArena &A, int t0) {
+__device__ __forceinline__ void dealer_loop(DealerLDS &D, const KArena &A, int t0, const PartnerLink &pl) {
     const int lane = lane_id();
     const uint32_t limit = g_spin_limit;
     uint32_t done = 0;
@@ -2518,6 +2550,7 @@ __device__ __forceinline__ void dealer_loop(DealerLDS &D, const KArena &A, int t
             if (lds_poll(&D.abort)) return;
             req = lds_poll(&D.dreq);
             if (req != done || lds_poll(&D.stop)) break;
+            if (pl.on) pt_poll(D, pl);
             if (spins >= limit) {
                 SPL_CHECK(false, BC_SPIN);
                 break;
@@ -2672,15 +2705,24 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 pl.pay = A.deleg + (size_t)pair * kDelegTasks * kDelegPayload;
             }
         }
-        if (pl.on && role == 1) {  // this side's launch counter (the output wave is both sides' party)
+        if (pl.on && role == 1) {  // this side's launch counter: the output wave counts, the dealer reads it
             uint32_t *el = pl.line(pt_epoch_line(pl.side));
             uint32_t e = ((uint32_t)__builtin_amdgcn_readfirstlane(flag_load(el)) + 1u) & 0xFFFFu;
             e = e == 0u ? 1u : e;
             flag_store(el, e);
             pl.e = e;
+            if (lane == 0) {
+                L.dl.pepoch = e;
+                L.dl.pt_seq[0] = L.dl.pt_seq[1] = 0u;
+                L.dl.pt_in[0] = 0ull;
+                L.dl.pt_in[1] = L.dl.pt_in[2] = ~0ull;  // no snapshot yet (tags match no sequence number)
+            }
         }
     }
     ws_sync();
+    if constexpr (kDealer && kStore) {
+        if (pl.on && role == 2) pl.e = (uint32_t)__builtin_amdgcn_readfirstlane(L.dl.pepoch);
+    }
 
     // stamp slot of this team (diagnostic builds): its 64-table block for the six-wave dealer, else the workgroup
     const int sid = wr.block >= 0 ? wr.block : (int)blockIdx.x;
@@ -2694,7 +2736,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
 #endif
     if constexpr (kDealer) {
         if (role >= 2) {
-            dealer_loop<P>(L.dl, A, t0);
+            dealer_loop<P>(L.dl, A, t0, pl);
             return;
         }
     }
@@ -2847,13 +2889,8 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         // partner hand-off, producer side: tasks posted, the one staged but not yet READY, and the
         // partner's progress and this side's next slot flag (loaded one step ahead)
         // consumer side: the partner's tasks seen and the flag of its next slot (loaded a step ahead)
-        uint32_t pseq = 0u, pprog = 0u, pslot = 0u, cseq = 0u, pnext = 0u;
+        uint32_t pseq = 0u, cseq = 0u;
         int ppend = -1, ppend_k = 0;
-        if (pl.on) {
-            pprog = flag_load(pl.line(pt_progress_line(pl.side ^ 1)));
-            pslot = flag_load(pl.line(pt_ready_line(pl.side * kPartnerSlots)));
-            pnext = pt_next_flag(pl, 0u);
-        }
         for (int k = 0; k < K; ++k) {
             if (pl.on) {
                 if (ppend >= 0) {  // the task staged last step: its words have completed, then READY
@@ -2861,8 +2898,14 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                     flag_store(pl.line(pt_ready_line(ppend)), pt_flag(pl.e, ppend_k, kPtReady));
                     ppend = -1;
                 }
-                // at most one of the partner's tasks per step, between this team's steps
-                pt_serve_v<P>(pl, cseq, (uint32_t)__builtin_amdgcn_readfirstlane(pnext), L.rows, L, S.obs, A.n);
+                // at most one of the partner's tasks per step, between this team's steps (the dealer's
+                // snapshot of its next slot, if it is for the task this wave expects)
+                if constexpr (kDealer) {
+                    const uint64_t nx = lds_poll64(&L.dl.pt_in[2]);
+                    if ((uint32_t)(nx >> 32) == cseq && pt_serve_v<P>(pl, cseq, (uint32_t)nx, L.rows, L, S.obs, A.n) &&
+                        lane == 0)
+                        __hip_atomic_store(&L.dl.pt_seq[1], cseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             }
             if constexpr (kDealer) {
                 if (!lds_wait_ge(L.dl, &L.dl.rdone, (uint32_t)(k + 1))) {  // hand-off of step k
@@ -2896,11 +2939,15 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             const bool big_moves = __any(valid && get_moves(T.sw) > 255);
             const bool deleg_now = dl.producer && deleg_step(k, K, dl.every);
             bool handed = false;  // partner hand-off of this step's rows
-            if (pl.on && !big_moves) {
-                const uint32_t pp = (uint32_t)__builtin_amdgcn_readfirstlane(pprog);
-                const uint32_t sf = (uint32_t)__builtin_amdgcn_readfirstlane(pslot);
-                const bool ahead = pl.lead < 0 || ((pp >> 16) == pl.e && (int)(pp & 0xFFFFu) >= k + pl.lead);
-                handed = ahead && ((sf & 3u) == 0u || (sf >> 16) != pl.e);  // the slot is free (or stale)
+            if constexpr (kDealer) {
+                if (pl.on && !big_moves) {
+                    const uint32_t pp = (uint32_t)lds_poll64(&L.dl.pt_in[0]);
+                    const uint64_t ms = lds_poll64(&L.dl.pt_in[1]);
+                    const uint32_t sf = (uint32_t)ms;
+                    const bool ahead = pl.lead < 0 || ((pp >> 16) == pl.e && (int)(pp & 0xFFFFu) >= k + pl.lead);
+                    // the slot is free (or stale), by a snapshot taken for this very slot
+                    handed = ahead && (uint32_t)(ms >> 32) == pseq && ((sf & 3u) == 0u || (sf >> 16) != pl.e);
+                }
             }
             if (handed) {
                 const int j = pl.side * kPartnerSlots + (int)(pseq % kPartnerSlots);
@@ -2908,6 +2955,9 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 ppend = j;
                 ppend_k = k;
                 ++pseq;
+                if constexpr (kDealer) {
+                    if (lane == 0) __hip_atomic_store(&L.dl.pt_seq[0], pseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             } else if (!deleg_now || big_moves) {  // a delegated step's rows are encoded by the partner
                 encode_row(T, L.rows, L);
                 wave_lds_sync();
@@ -2969,9 +3019,6 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             }
             if (pl.on) {  // progress out; the partner's and the next slot's flag in, for the next decision
                 flag_store(pl.line(pt_progress_line(pl.side)), pl.e << 16 | (uint32_t)(k + 1));
-                pprog = flag_load(pl.line(pt_progress_line(pl.side ^ 1)));
-                pslot = flag_load(pl.line(pt_ready_line(pl.side * kPartnerSlots + (int)(pseq % kPartnerSlots))));
-                pnext = pt_next_flag(pl, cseq);
             }
             WSSTAMP(3, k);
         }
