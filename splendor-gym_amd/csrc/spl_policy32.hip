@@ -83,6 +83,7 @@ constexpr int kPlanes = 3;       // bf16 planes of a split fp32 operand
 constexpr int kActScaleExp = 0;
 constexpr int kRowMaxExp = 0;    // bf16 has fp32's exponent range: no scaling
 #endif
+constexpr float kTwoLog2e = 2.8853900817779268f;  // 2 log2(e): exp(2|x|) = exp2(2 log2(e) |x|)
 typedef pel pelx8 __attribute__((ext_vector_type(8)));
 typedef pel pelx2 __attribute__((ext_vector_type(2)));
 
@@ -112,7 +113,7 @@ constexpr int kLdsMask = kSlots * kChunk;
 constexpr int kLds = kLdsMask + kWaves * kMaskWave;  // 132 736 B
 static_assert(kWaves * kRowsPerWave * kLogitRow * 4 <= kLdsMask, "logits reuse the weight ring");
 static_assert(kLds <= 160 * 1024, "LDS");
-static_assert(kBiasOff + 128 <= kChunk, "bias + row factors");
+static_assert(kBiasOff + 192 <= kChunk, "bias + row factors + tanh factors");
 
 // chunk order of an image (the order a forward pass consumes them): with a critic
 // [critic L1 x16][critic L2 x16], then [actor L1 x16][actor L2 x16][actor L3 x3]; the actor part of
@@ -187,12 +188,15 @@ __global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, i
         *reinterpret_cast<uint32_t *>(out + v) = 0u;
     float *bias = reinterpret_cast<float *>(out + kBiasOff);
     const int act_exp = layer == 1 ? 0 : kActScaleExp;  // layer 1 reads the observation unscaled
-    if (threadIdx.x < 16) {  // scaled biases in row order, then the row factors, zero padding to the end
+    if (threadIdx.x < 16) {  // scaled biases in row order, the row factors, the tanh factors, zero padding
         const int row = 16 * tile + threadIdx.x, ex = rexp[threadIdx.x] + act_exp;
         bias[threadIdx.x] = row < rows ? ldexpf(B[row], ex) : 0.f;
         bias[16 + threadIdx.x] = ldexpf(1.f, -ex);
+        // 2 log2(e) * the row factor (exact: a power of two): tanh's exp2 argument straight from the
+        // unscaled sum (tanh_fold)
+        bias[32 + threadIdx.x] = ldexpf(kTwoLog2e, -ex);
     }
-    for (int v = kBiasOff + 128 + 4 * threadIdx.x; v < kChunk; v += 4 * blockDim.x)
+    for (int v = kBiasOff + 192 + 4 * threadIdx.x; v < kChunk; v += 4 * blockDim.x)
         *reinterpret_cast<uint32_t *>(out + v) = 0u;
     if (net == 1 && layer == 2 && tile == 0) {  // the critic's output layer as fp32 (evaluated on VALU)
         float *tail = reinterpret_cast<float *>(dst + (size_t)kAllChunks * kChunk);
@@ -235,7 +239,7 @@ __device__ __forceinline__ float tanh_f32(float x) {
 #elif SPL_TANH_LIBM
     return tanhf(x);
 #elif SPL_TANH_EXP
-    const float e = __builtin_amdgcn_exp2f(__builtin_fabsf(x) * 2.8853900817779268f);  // exp(2|x|)
+    const float e = __builtin_amdgcn_exp2f(__builtin_fabsf(x) * kTwoLog2e);  // exp(2|x|)
     return __builtin_copysignf(__builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f), x);
 #else
     const float ax = __builtin_fabsf(x);
@@ -246,10 +250,21 @@ __device__ __forceinline__ float tanh_f32(float x) {
     p = __builtin_fmaf(p, z, 0.13331513106822968f);
     p = __builtin_fmaf(p, z, -0.3333328664302826f);
     const float small = __builtin_fmaf(ax * z, p, ax);
-    const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);  // exp(2|x|)
+    const float e = __builtin_amdgcn_exp2f(ax * kTwoLog2e);  // exp(2|x|)
     const float big = __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
     return __builtin_copysignf(ax < 0.625f ? small : big, x);
 #endif
+}
+
+// tanh with the tile's row factor and the next layer's activation scale folded in (SPL_TANH_EXP):
+// 2^S tanh(x u) for c = 2 log2(e) u, bitwise the same as tanh_f32(x * u) * 2^S (u and 2^S powers of
+// two; |x| c and |x u| 2 log2(e) are the same real product, rounded once) and two VALU ops fewer
+// per output (the unscale and the activation-scale multiplies)
+constexpr bool kFoldTanh = SPL_TANH_EXP && !(SPL_POL_ABL & 1) && !SPL_TANH_LIBM;
+template <int S>
+__device__ __forceinline__ float tanh_fold(float x, float c) {
+    const float e = __builtin_amdgcn_exp2f(__builtin_fabsf(x) * c);
+    return __builtin_copysignf(__builtin_fmaf(-(float)(2 << S), __builtin_amdgcn_rcpf(e + 1.0f), (float)(1 << S)), x);
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -292,12 +307,16 @@ __device__ __forceinline__ f32x4 mma(const pelx8 &a, const pelx8 &b, const f32x4
 // exact in one plane; kPlanes: a split hidden layer), in registers.  A: the tile's weight planes per
 // k-step from `src` (the LDS ring slot, or the image in global memory for the narrow kernel), D
 // k-steps ahead of the MFMAs that use them.
-template <int KS, int NB, int D>
-__device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const pelx8 (&B)[NB][KS], int lane) {
+// kFold: the sum is returned as the products left it (scaled by the row factor's inverse) and
+// `fold` gets the tile's tanh factors (tanh_fold) instead.
+template <int KS, int NB, int D, bool kFold = false>
+__device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const pelx8 (&B)[NB][KS], int lane,
+                                          f32x4 *fold = nullptr) {
     static_assert(NB == 1 || NB == kPlanes, "planes");
     const float *bias = reinterpret_cast<const float *>(src + kBiasOff) + 4 * (lane >> 4);
     f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
     const f32x4 unscale = {bias[16], bias[17], bias[18], bias[19]};
+    if constexpr (kFold) *fold = f32x4{bias[32], bias[33], bias[34], bias[35]};
     const pelx8 *A = reinterpret_cast<const pelx8 *>(src) + lane;  // k-step s, plane p at A[(kPlanes s + p) * 64]
     constexpr int NR = D + 1;
     pelx8 af[NR][kPlanes];
@@ -329,7 +348,7 @@ __device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const pelx8 (&B)[N
         }
         if (NB > 1 || (s & 1) == 1) __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (kRowMaxExp != 0) acc *= unscale;  // exact: powers of two
+    if constexpr (kRowMaxExp != 0 && !kFold) acc *= unscale;  // exact: powers of two
     return acc;
 }
 
@@ -341,10 +360,12 @@ __device__ __forceinline__ uint32_t pk2(pel lo, pel hi) {
 
 // the four fp32 outputs h[0..3] of tile t (units 16t + 4g + i), scaled by 2^kActScaleExp (exact) ->
 // elements 4(t & 1) .. +3 of k-step t / 2 of the next layer's B planes
+template <bool kScaled = false>  // kScaled: h already carries 2^kActScaleExp (tanh_fold)
 __device__ __forceinline__ void put_split(pelx8 (&H)[kPlanes][kKs2], int t, const float (&h)[4]) {
     pel x[4][kPlanes];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) split_planes(kActScaleExp ? h[i] * (float)(1 << kActScaleExp) : h[i], x[i]);
+    for (int i = 0; i < 4; ++i)
+        split_planes((kActScaleExp && !kScaled) ? h[i] * (float)(1 << kActScaleExp) : h[i], x[i]);
 #pragma unroll
     for (int p = 0; p < kPlanes; ++p) {
         u32x4 w = __builtin_bit_cast(u32x4, H[p][t >> 1]);
@@ -360,11 +381,19 @@ __device__ __forceinline__ void layer_tanh(Enter &enter, const pelx8 (&B)[NB][KS
                                            int lane) {
 #pragma unroll
     for (int t = 0; t < kTiles; ++t) {
-        const f32x4 acc = tile_mma<KS, NB, D>(enter(), B, lane);
         float h[4];
+        if constexpr (kFoldTanh) {
+            f32x4 c;
+            const f32x4 acc = tile_mma<KS, NB, D, true>(enter(), B, lane, &c);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) h[i] = tanh_f32(acc[i]);
-        put_split(H, t, h);
+            for (int i = 0; i < 4; ++i) h[i] = tanh_fold<kActScaleExp>(acc[i], c[i]);
+            put_split<true>(H, t, h);
+        } else {
+            const f32x4 acc = tile_mma<KS, NB, D>(enter(), B, lane);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) h[i] = tanh_f32(acc[i]);
+            put_split(H, t, h);
+        }
     }
 }
 
@@ -577,12 +606,22 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
         // layer 2 tile t -> tanh -> its units' share of the fp32 output unit, on the spot
 #pragma unroll 1
         for (int t = 0; t < kTiles; ++t) {
-            const f32x4 acc = tile_mma<kKs2, kPlanes, kAheadHid>(enter(), H1, lane);
             const float4 w = *reinterpret_cast<const float4 *>(a.critic_out + 16 * t + 4 * g);
-            value = __builtin_fmaf(w.x, tanh_f32(acc[0]), value);
-            value = __builtin_fmaf(w.y, tanh_f32(acc[1]), value);
-            value = __builtin_fmaf(w.z, tanh_f32(acc[2]), value);
-            value = __builtin_fmaf(w.w, tanh_f32(acc[3]), value);
+            float h[4];
+            if constexpr (kFoldTanh) {
+                f32x4 c;
+                const f32x4 acc = tile_mma<kKs2, kPlanes, kAheadHid, true>(enter(), H1, lane, &c);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) h[i] = tanh_fold<0>(acc[i], c[i]);
+            } else {
+                const f32x4 acc = tile_mma<kKs2, kPlanes, kAheadHid>(enter(), H1, lane);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) h[i] = tanh_f32(acc[i]);
+            }
+            value = __builtin_fmaf(w.x, h[0], value);
+            value = __builtin_fmaf(w.y, h[1], value);
+            value = __builtin_fmaf(w.z, h[2], value);
+            value = __builtin_fmaf(w.w, h[3], value);
         }
         value += __shfl_xor(value, 16);  // the other lane groups' units, then the bias
         value += __shfl_xor(value, 32);

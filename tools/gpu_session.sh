@@ -96,6 +96,11 @@ for step in "$@"; do
         run pol_tanhexp_$i 200 python tools/bench_policy.py --fused-only --iters 30
         SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_tanhpoly.so run pol_tanhpoly_$i 200 python tools/bench_policy.py --fused-only --iters 30
       done ;;
+    foldab)  # the actor's tanh with the row factor and activation scale folded in (product) vs not (ablate/lib_prefold.so)
+      for i in 1 2 3; do
+        run pol_fold_$i 200 python tools/bench_policy.py --fused-only --iters 30
+        SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_prefold.so run pol_prefold_$i 200 python tools/bench_policy.py --fused-only --iters 30
+      done ;;
     poltest1) run pytest_pol1 300 python -u -m pytest tests/test_gpu_policy.py -x -q --timeout 200 --timeout-method thread ;;
     selfplay) run sp_pool 300 python tools/bench_selfplay.py
               run sp_frozen 300 python tools/bench_selfplay.py --opponent frozen ;;
