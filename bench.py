@@ -471,7 +471,7 @@ def main():
                          "profiles/r03/deleg_ab_r03a.txt)")
     ap.add_argument("--partner-lead", type=int, default=None,
                     help="six-wave dealer rollout store: a team this many steps behind its neighbouring-XCC "
-                         "partner hands it whole steps of rows (library default 2; 0 = off)")
+                         "partner hands it whole steps of rows (library default 4; 0 = off)")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -670,7 +670,7 @@ def main():
     if store is not None:  # every step of the last rollout-store launch
         bad += int(((store["flags"] & errs) != 0).sum().item())
     faults = eng.faults()
-    handoffs = partner_stats(lib) if "dealer2" in kernel_name("rollout_store") else None
+    handoffs = partner_stats(lib) if headline == "rollout_store" else None
     rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
     episodes = int(cnts.sum().item())
 
@@ -755,7 +755,7 @@ def main():
             "error_flags": bad,
             "launch_faults": faults,
         }
-        if handoffs is not None:  # the six-wave dealer's partner hand-offs over this process (warm-up included)
+        if handoffs is not None:  # the rollout store's partner hand-offs over this process (warm-up included)
             out["partner_handoffs"] = handoffs
         for v in variants[1:]:
             s = with_traffic(summary(recs[v]))

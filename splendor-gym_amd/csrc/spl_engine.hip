@@ -175,13 +175,15 @@ constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 #define SPL_DELEG_EVERY 0
 #endif
 #ifndef SPL_PARTNER_LEAD
-// partner hand-off of the six-wave dealer rollout (spl_ctx_set_partner_lead): a team hands a step's
+// partner hand-off of the rollout-store kernels (spl_ctx_set_partner_lead): a team hands a step's
 // rows to its neighbouring-XCC partner when that one is this many steps ahead.  With the flag words
-// polled by the dealer wave (not the output wave, whose loads would wait behind its own row stores),
-// lead 2 against off, arms alternating on two boxes: median launch 1 075-1 082 vs 1 095-1 104 us, run
-// throughput +0.8 / +2.7 % (profiles/r04/partner_ab_r04u.txt); the first form, polling from the output
-// wave, was slower than off (partner_ab_r04n.txt)
-#define SPL_PARTNER_LEAD 2
+// polled by a wave that issues no row stores (the dealer, or the two-wave kernel's rules wave) and
+// arms alternating on one box: C4 (six-wave dealer) median launch 1 081-1 084 (lead 4) / 1 076-1 080
+// (lead 2) vs 1 098-1 104 us off (profiles/r04/partner_ab_r04u.txt); the headline (two-wave, 2p x
+// 65 536) 2 027-2 036 (lead 4) / 2 048-2 060 (lead 2) vs 2 055-2 061 us off, ~12 000 of 131 072
+// team-steps handed off per launch (partner_ab_head_r04zb.txt).  Polled by the output wave itself
+// the hand-off was slower than off (partner_ab_r04n.txt).
+#define SPL_PARTNER_LEAD 4
 #endif
 #ifndef SPL_XCD_MAP
 #define SPL_XCD_MAP 1
@@ -2043,10 +2045,21 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
 // rules wave's own state slot st[k & 1]: a deal (fused refill or inline autoreset deal) runs
 // before that slot is written for step k, and the output wave finished reading it (step k - 2)
 // before the hand-off barrier of step k - 1.
+// partner hand-off (rollout store kernels): another wave of the team (the dealer, or the rules wave of
+// the two-wave kernel) polls the pair's flag words so the output wave never waits on a global load
+// behind its own row stores (one in-order vmcnt)
+struct PtShared {
+    uint32_t pepoch;  // output wave -> poller: this launch's counter
+    uint32_t seq[2];  // output wave -> poller: tasks posted (pseq), partner tasks seen (cseq)
+    uint64_t in[3];   // poller -> output wave: partner progress; pseq << 32 | my next slot's flag;
+                      // cseq << 32 | the partner's next slot's flag
+};
+
 template <int P>
 struct __align__(16) WsLDS : Consts {
     static constexpr int kW = SW_COUNT + 4 * P;  // state words per table
-    static constexpr int kTerm = P == 3 ? 8 : (P == 4 ? 15 : 16);  // terminal states listed per step
+    PtShared pt;
+    static constexpr int kTerm = P == 3 ? 7 : (P == 4 ? 15 : 16);  // terminal states listed per step (3p: 7, room for PtShared)
     static constexpr int kScrStride = P == 2 ? kScratchStride : 100;
     static constexpr bool kScrInSlot = P == 4;
     static_assert(!kScrInSlot || kW * 64 * 4 >= 64 * kScrStride, "scratch must fit the state slot");
@@ -2351,12 +2364,6 @@ struct DealerLDS {
     uint32_t stop;            // rules wave: no more batches
     uint32_t rnd[2][64];      // the uniform policy's words of step k in slot k & 1, drawn by the output wave at step k - 2
     uint32_t abort;           // a wait ran out (lds_wait_ge): every later wait returns at once
-    // partner hand-off (six-wave dealer): the dealer wave polls the pair's flag words between batches so
-    // the output wave never waits on a global load behind its own row stores (one in-order vmcnt)
-    uint32_t pepoch;          // output wave -> dealer: this launch's counter
-    uint32_t pt_seq[2];       // output wave -> dealer: tasks posted (pseq), partner tasks seen (cseq)
-    uint64_t pt_in[3];        // dealer -> output wave: partner progress; pseq << 32 | my next slot's flag;
-                              // cseq << 32 | the partner's next slot's flag
 };
 template <int P>
 struct __align__(16) WsDealLDS : WsLDS<P> {
@@ -2449,6 +2456,7 @@ struct PartnerLink {
     __device__ __forceinline__ uint8_t *slot(int j) const { return pay + (size_t)j * kDelegPayload; }
 };
 constexpr uint32_t kPtReady = 1u, kPtTaken = 2u;
+constexpr int kPartnerForced = -1000;  // the two-wave kernel's `deleg` for lead -1 (hand off whenever a slot is free)
 constexpr uint64_t kPartnerWait = 500000;  // 5 ms of s_memrealtime (100 MHz): the consumer's wait for DONE
 __device__ __forceinline__ uint32_t pt_flag(uint32_t e, int k, uint32_t st) { return e << 16 | (uint32_t)k << 2 | st; }
 __device__ unsigned long long g_partner_stats[2];  // tasks stored by the partner / claimed back (diagnostics)
@@ -2519,18 +2527,20 @@ __device__ __forceinline__ void pt_drain(const PartnerLink &pl, uint32_t &cseq, 
 // ends the dealer quietly: a batch posted after that is never dealt, so the rules wave's wait for it
 // runs out and faults the launch (lds_wait_ge).  A faulted workgroup's dealer ends after its batch.
 // the dealer wave's poll of the pair's words for its output wave (a snapshot; tags say which slots)
-__device__ __forceinline__ void pt_poll(DealerLDS &D, const PartnerLink &pl) {
-    const uint32_t ps = lds_poll(&D.pt_seq[0]), cs = lds_poll(&D.pt_seq[1]);
+__device__ __forceinline__ void pt_publish(PtShared &X, uint32_t a, uint32_t b, uint32_t ps, uint32_t c, uint32_t cs) {
+    if (lane_id() == 0) {
+        __hip_atomic_store(&X.in[0], (uint64_t)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&X.in[1], (uint64_t)ps << 32 | b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&X.in[2], (uint64_t)cs << 32 | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+__device__ __forceinline__ void pt_poll(PtShared &X, const PartnerLink &pl) {
+    const uint32_t ps = lds_poll(&X.seq[0]), cs = lds_poll(&X.seq[1]);
     const uint32_t a = flag_load(pl.line(pt_progress_line(pl.side ^ 1)));
     const uint32_t b = flag_load(pl.line(pt_ready_line(pl.side * kPartnerSlots + (int)(ps % kPartnerSlots))));
     const uint32_t c = flag_load(pl.line(pt_ready_line((pl.side ^ 1) * kPartnerSlots + (int)(cs % kPartnerSlots))));
-    const uint32_t ra = (uint32_t)__builtin_amdgcn_readfirstlane(a), rb = (uint32_t)__builtin_amdgcn_readfirstlane(b),
-                   rc = (uint32_t)__builtin_amdgcn_readfirstlane(c);
-    if (lane_id() == 0) {
-        __hip_atomic_store(&D.pt_in[0], (uint64_t)ra, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_store(&D.pt_in[1], (uint64_t)ps << 32 | rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_store(&D.pt_in[2], (uint64_t)cs << 32 | rc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    pt_publish(X, (uint32_t)__builtin_amdgcn_readfirstlane(a), (uint32_t)__builtin_amdgcn_readfirstlane(b), ps,
+               (uint32_t)__builtin_amdgcn_readfirstlane(c), cs);
 }
 __device__ __forceinline__ uint64_t lds_poll64(const uint64_t *p) {
     const uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2540,7 +2550,7 @@ __device__ __forceinline__ uint64_t lds_poll64(const uint64_t *p) {
 }
 
 template <int P>
-__device__ __forceinline__ void dealer_loop(DealerLDS &D, const KArena &A, int t0, const PartnerLink &pl) {
+__device__ __forceinline__ void dealer_loop(DealerLDS &D, const KArena &A, int t0, const PartnerLink &pl, PtShared &X) {
     const int lane = lane_id();
     const uint32_t limit = g_spin_limit;
     uint32_t done = 0;
@@ -2550,7 +2560,7 @@ __device__ __forceinline__ void dealer_loop(DealerLDS &D, const KArena &A, int t
             if (lds_poll(&D.abort)) return;
             req = lds_poll(&D.dreq);
             if (req != done || lds_poll(&D.stop)) break;
-            if (pl.on) pt_poll(D, pl);
+            if (pl.on) pt_poll(X, pl);
             if (spins >= limit) {
                 SPL_CHECK(false, BC_SPIN);
                 break;
@@ -2688,41 +2698,45 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             L.dl.dreq = L.dl.ddone = L.dl.rdone = L.dl.odone = L.dl.stop = L.dl.abort = 0u;
         }
     }
-    // partner hand-off (six-wave dealer, per-step outputs; deleg_every = the lead in steps, 0 = off):
-    // team j of workgroups b and b ^ 1, both full, K < 2^14 (the step fits a flag)
-    PartnerLink pl{false, 0, deleg_every, 0u, nullptr, nullptr, 0};
-    if constexpr (kDealer && kStore) {
-        if (wr.block >= 0 && deleg_every != 0 && K < (1 << 14)) {
+    // partner hand-off (per-step outputs, 64 tables per team; see PartnerLink): the six-wave dealer
+    // passes the lead in steps as deleg_every (0 = off, -1 = forced), the two-wave kernel as -lead
+    // (deleg_every >= 4 is its older static delegation; kPartnerForced = forced).  Team j of workgroups
+    // b and b ^ 1, both full, K < 2^14 (the step fits a flag).
+    PartnerLink pl{false, 0, 0, 0u, nullptr, nullptr, 0};
+    if constexpr (kStore && TPW == 64) {
+        int lead = 0;
+        if constexpr (kDealer) lead = wr.block >= 0 ? deleg_every : 0;
+        else lead = deleg_every < 0 ? (deleg_every == kPartnerForced ? -1 : -deleg_every) : 0;
+        if (lead != 0 && K < (1 << 14)) {
             const uint32_t b = blockIdx.x, pb = b ^ 1u;
-            const int team = wr.block - 2 * wg_block();
-            const int t0p = (2 * wg_block_of(pb) + team) * 64;
-            const int pair = (int)(b >> 1) * 2 + team;
+            const int team = kDealer ? wr.block - 2 * wg_block() : 0;
+            const int t0p = kDealer ? (2 * wg_block_of(pb) + team) * 64 : wg_block_of(pb) * 64;
+            const int pair = kDealer ? (int)(b >> 1) * 2 + team : (int)(b >> 1);
             if (pb < gridDim.x && t0 + 64 <= A.n && t0p + 64 <= A.n && pair < A.n / 128) {
                 pl.on = true;
+                pl.lead = lead;
                 pl.side = (int)(b & 1u);
                 pl.t0p = t0p;
                 pl.fl = A.dflags + (size_t)pair * kDelegFlagWords;
                 pl.pay = A.deleg + (size_t)pair * kDelegTasks * kDelegPayload;
             }
         }
-        if (pl.on && role == 1) {  // this side's launch counter: the output wave counts, the dealer reads it
+        if (pl.on && role == 1) {  // this side's launch counter: the output wave counts, the poller reads it
             uint32_t *el = pl.line(pt_epoch_line(pl.side));
             uint32_t e = ((uint32_t)__builtin_amdgcn_readfirstlane(flag_load(el)) + 1u) & 0xFFFFu;
             e = e == 0u ? 1u : e;
             flag_store(el, e);
             pl.e = e;
             if (lane == 0) {
-                L.dl.pepoch = e;
-                L.dl.pt_seq[0] = L.dl.pt_seq[1] = 0u;
-                L.dl.pt_in[0] = 0ull;
-                L.dl.pt_in[1] = L.dl.pt_in[2] = ~0ull;  // no snapshot yet (tags match no sequence number)
+                L.pt.pepoch = e;
+                L.pt.seq[0] = L.pt.seq[1] = 0u;
+                L.pt.in[0] = 0ull;
+                L.pt.in[1] = L.pt.in[2] = ~0ull;  // no snapshot yet (tags match no sequence number)
             }
         }
     }
     ws_sync();
-    if constexpr (kDealer && kStore) {
-        if (pl.on && role == 2) pl.e = (uint32_t)__builtin_amdgcn_readfirstlane(L.dl.pepoch);
-    }
+    if (pl.on && role != 1) pl.e = (uint32_t)__builtin_amdgcn_readfirstlane(L.pt.pepoch);
 
     // stamp slot of this team (diagnostic builds): its 64-table block for the six-wave dealer, else the workgroup
     const int sid = wr.block >= 0 ? wr.block : (int)blockIdx.x;
@@ -2736,7 +2750,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
 #endif
     if constexpr (kDealer) {
         if (role >= 2) {
-            dealer_loop<P>(L.dl, A, t0, pl);
+            dealer_loop<P>(L.dl, A, t0, pl, L.pt);
             return;
         }
     }
@@ -2761,6 +2775,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         bool pool_dirty = false;
         const uint64_t ply0 = S.ply + (S.ply_base ? *S.ply_base : 0ull);
         uint64_t cur_mask = 0ull;
+        uint32_t pv[3] = {0u, 0u, 0u}, pps = 0u, pcs = 0u;  // two-wave partner poller (loaded a step ahead)
         const uint64_t below = (1ull << lane) - 1ull;
 #ifdef SPL_STAMPS
         int rst_lo[kWsStamps] = {0}, rst_hi[kWsStamps] = {0};
@@ -2828,6 +2843,17 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             if constexpr (kDealer) {
                 lds_publish(&L.dl.rdone, (uint32_t)(k + 1));  // hand-off of step k
             } else {
+                if (pl.on) {  // the partner poller of the two-wave kernel: the words loaded last step, then new loads
+                    if (k > 0)
+                        pt_publish(L.pt, (uint32_t)__builtin_amdgcn_readfirstlane(pv[0]),
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(pv[1]), pps,
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(pv[2]), pcs);
+                    pps = lds_poll(&L.pt.seq[0]);
+                    pcs = lds_poll(&L.pt.seq[1]);
+                    pv[0] = flag_load(pl.line(pt_progress_line(pl.side ^ 1)));
+                    pv[1] = flag_load(pl.line(pt_ready_line(pl.side * kPartnerSlots + (int)(pps % kPartnerSlots))));
+                    pv[2] = flag_load(pl.line(pt_ready_line((pl.side ^ 1) * kPartnerSlots + (int)(pcs % kPartnerSlots))));
+                }
                 ws_sync();  // hand-off of step k
             }
             WSSTAMP(3, k);
@@ -2900,12 +2926,10 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 }
                 // at most one of the partner's tasks per step, between this team's steps (the dealer's
                 // snapshot of its next slot, if it is for the task this wave expects)
-                if constexpr (kDealer) {
-                    const uint64_t nx = lds_poll64(&L.dl.pt_in[2]);
-                    if ((uint32_t)(nx >> 32) == cseq && pt_serve_v<P>(pl, cseq, (uint32_t)nx, L.rows, L, S.obs, A.n) &&
-                        lane == 0)
-                        __hip_atomic_store(&L.dl.pt_seq[1], cseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
+                const uint64_t nx = lds_poll64(&L.pt.in[2]);
+                if ((uint32_t)(nx >> 32) == cseq && pt_serve_v<P>(pl, cseq, (uint32_t)nx, L.rows, L, S.obs, A.n) &&
+                    lane == 0)
+                    __hip_atomic_store(&L.pt.seq[1], cseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             if constexpr (kDealer) {
                 if (!lds_wait_ge(L.dl, &L.dl.rdone, (uint32_t)(k + 1))) {  // hand-off of step k
@@ -2939,15 +2963,13 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             const bool big_moves = __any(valid && get_moves(T.sw) > 255);
             const bool deleg_now = dl.producer && deleg_step(k, K, dl.every);
             bool handed = false;  // partner hand-off of this step's rows
-            if constexpr (kDealer) {
-                if (pl.on && !big_moves) {
-                    const uint32_t pp = (uint32_t)lds_poll64(&L.dl.pt_in[0]);
-                    const uint64_t ms = lds_poll64(&L.dl.pt_in[1]);
-                    const uint32_t sf = (uint32_t)ms;
-                    const bool ahead = pl.lead < 0 || ((pp >> 16) == pl.e && (int)(pp & 0xFFFFu) >= k + pl.lead);
-                    // the slot is free (or stale), by a snapshot taken for this very slot
-                    handed = ahead && (uint32_t)(ms >> 32) == pseq && ((sf & 3u) == 0u || (sf >> 16) != pl.e);
-                }
+            if (pl.on && !big_moves) {
+                const uint32_t pp = (uint32_t)lds_poll64(&L.pt.in[0]);
+                const uint64_t ms = lds_poll64(&L.pt.in[1]);
+                const uint32_t sf = (uint32_t)ms;
+                const bool ahead = pl.lead < 0 || ((pp >> 16) == pl.e && (int)(pp & 0xFFFFu) >= k + pl.lead);
+                // the slot is free (or stale), by a snapshot taken for this very slot
+                handed = ahead && (uint32_t)(ms >> 32) == pseq && ((sf & 3u) == 0u || (sf >> 16) != pl.e);
             }
             if (handed) {
                 const int j = pl.side * kPartnerSlots + (int)(pseq % kPartnerSlots);
@@ -2955,9 +2977,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 ppend = j;
                 ppend_k = k;
                 ++pseq;
-                if constexpr (kDealer) {
-                    if (lane == 0) __hip_atomic_store(&L.dl.pt_seq[0], pseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
+                if (lane == 0) __hip_atomic_store(&L.pt.seq[0], pseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else if (!deleg_now || big_moves) {  // a delegated step's rows are encoded by the partner
                 encode_row(T, L.rows, L);
                 wave_lds_sync();
@@ -4038,8 +4058,14 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     const int64_t resident = ctx->ws_resident[arena->players];
     const int tpw = rollout_tpw(ctx, arena->n, arena->players);
     const bool p_out = per_step_outputs != 0;
-    // delegation pairs must run at the same time: off when the grid exceeds what is resident at once
-    const int deleg = (int64_t)blocks_for(arena->n) <= resident ? ctx->deleg_every : 0;
+    // delegation / partner pairs must run at the same time: off when the grid exceeds what is resident
+    // at once.  The two-wave kernel's `deleg`: the static delegation period (>= 4), else -lead of the
+    // partner hand-off (kPartnerForced for lead -1), else 0
+    int deleg = 0;
+    if ((int64_t)blocks_for(arena->n) <= resident) {
+        if (ctx->deleg_every > 0) deleg = ctx->deleg_every;
+        else if (ctx->partner_lead != 0) deleg = ctx->partner_lead < 0 ? kPartnerForced : -ctx->partner_lead;
+    }
 #define SPL_LAUNCH_WS(TPW, BLOCKS)                                                                           \
     DISPATCH_P(arena->players, if (p_out) {                                                                  \
         hipLaunchKernelGGL((RolloutKernel<PP, TPW, true>::fn), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \

@@ -345,21 +345,24 @@ def _check_rollout_vs_chain(P, K, refill_fused, pipeline, R, partner_lead=None, 
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("P,lead", [(4, -1), (2, -1), (4, 2), (3, 1)])
-def test_dealer2_partner_handoff_equals_step_chain(P, lead):
-    """The six-wave dealer rollout's partner hand-off (spl_ctx_set_partner_lead): with lead -1 every
-    team hands its steps' rows to the same team of the neighbouring-XCC workgroup whenever a task slot
-    is free, so the partner's output wave encodes and stores many row blocks between its own steps (and
-    the poster claims back what is left at the end); every per-step output still equals the chained
-    spl_step bit for bit, and the diagnostic counters show the hand-offs happened.  Lead 1-2: hand-offs
-    only when a partner runs ahead (timing-dependent; same results either way)."""
+@pytest.mark.parametrize("P,lead,pipeline", [(4, -1, "dealer2"), (2, -1, "dealer2"), (4, 2, "dealer2"), (3, 1, "dealer2"),
+                                             (2, -1, "always"), (4, -1, "always"), (2, 2, "always"),
+                                             (3, -1, "always")])
+def test_partner_handoff_equals_step_chain(P, lead, pipeline):
+    """The partner hand-off of the rollout-store kernels (spl_ctx_set_partner_lead; the six-wave dealer,
+    whose dealer wave polls the flags, and the two-wave kernel, whose rules wave does): with lead -1
+    every team hands its steps' rows to the same team of the neighbouring-XCC workgroup whenever a task
+    slot is free, so the partner's output wave encodes and stores many row blocks between its own steps
+    (and the poster claims back what is left at the end); every per-step output still equals the
+    chained spl_step bit for bit, and the diagnostic counters show the hand-offs happened.  Lead 1-2:
+    hand-offs only when a partner runs ahead (timing-dependent; same results either way)."""
     import ctypes
     from splendor_gym import _native
     st = (ctypes.c_uint64 * 2)()
     probe = engine(128, 2)
     _native.check(probe.lib, probe.lib.spl_debug_partner_stats(st, 1))
-    fused = _check_rollout_vs_chain(P, 64, True, "dealer2", 16, partner_lead=lead, launches=3)
-    assert fused.rollout_kernel_name() == f"k_rollout_store_dealer2_{P}p"
+    fused = _check_rollout_vs_chain(P, 64, True, pipeline, 16, partner_lead=lead, launches=3)
+    assert fused.rollout_kernel_name() == (f"k_rollout_store_dealer2_{P}p" if pipeline == "dealer2" else f"k_rollout_store_{P}p")
     _native.check(fused.lib, fused.lib.spl_debug_partner_stats(st, 1))
     if lead < 0:
         assert st[0] > 0, (st[0], st[1])  # the partners stored handed-off blocks

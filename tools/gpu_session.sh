@@ -64,7 +64,7 @@ for step in "$@"; do
       bash tools/pmc.sh ${TAG}_4p_32768 4 32768 store traffic || exit 1
       bash tools/pmc.sh ${TAG}_2p_step 2 65536 step traffic || exit 1 ;;
     partnertests) run pytest_partner 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_faults.py \
-                      -k "partner or dealer2" -x -v --timeout 200 --timeout-method thread ;;
+                      -k "partner or dealer2 or rollout_equals" -x -v --timeout 200 --timeout-method thread ;;
     partnerab)  # the C4 share (4p x 32768, six-wave dealer) with the partner hand-off off / lead 2 / lead 4, alternating
       for i in 1 2; do for ld in 0 2 4; do
         run c4_lead${ld}_$i 300 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 --only --partner-lead $ld
@@ -72,6 +72,10 @@ for step in "$@"; do
     partnerab3)  # lead 0 / 1 / 2, three alternations
       for i in 1 2 3; do for ld in 0 1 2; do
         run c4_lead${ld}_$i 300 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 --only --partner-lead $ld
+      done; done ;;
+    headab)  # the headline (2p x 65536, k_rollout_store_2p) with the partner hand-off off / lead 2 / lead 4, alternating
+      for i in 1 2; do for ld in 0 2 4; do
+        run head_lead${ld}_$i 300 python3 bench.py --no-cpu-baseline --only --partner-lead $ld
       done; done ;;
     pmcstep) bash tools/pmc.sh ${TAG}_2p_step 2 65536 step all || exit 1 ;;
     stamps) run stamps 300 python3 tools/stamps.py --run ;;
@@ -84,7 +88,7 @@ for step in "$@"; do
     wsstamps4gather)  # the same with the deck-top / LUT gathers replaced by constants (-DSPL_ABL=16384 / 32768)
       WS_P=4 WS_T=32768 run wsstamps4nodeck 300 python3 tools/wsstamps.py --run --lib splendor-gym_amd/ablate/lib_wsstamps_nodeck.so
       WS_P=4 WS_T=32768 run wsstamps4nolut 300 python3 tools/wsstamps.py --run --lib splendor-gym_amd/ablate/lib_wsstamps_nolut.so ;;
-    wsstamps2) run wsstamps2 300 python3 tools/wsstamps.py --run ;;
+    wsstamps2) WS_RAW=$O/wsstamps2_raw_$TAG.npz run wsstamps2 300 python3 tools/wsstamps.py --run ;;
     stepab) run bench_step 300 python3 bench.py --mode step --only --no-cpu-baseline --sp-tables 0 ;;
     abl2)  # actor timing ablation: no ring streaming (one weight chunk; wrong results by design)
       run pol_full 200 python tools/bench_policy.py --fused-only --iters 30
