@@ -654,9 +654,14 @@ def main():
     if not args.only:
         variants += [v for v in ("rollout_store", "rollout_inplace", "step") if v != headline]
     recs, k_next = {}, 0
+    handoffs = None
     for v in variants:
+        if v == "rollout_store":
+            partner_stats(lib, clear=True)
         recs[v] = measure(v, k_next)
         k_next = recs[v]["k_next"]
+        if v == "rollout_store" and headline == "rollout_store":  # this line's hand-offs (warm-up included)
+            handoffs = partner_stats(lib)
     sp = None
     if args.sp_tables > 0 and not args.only:
         sp = selfplay_line(dev, rank, world, args.sp_tables, args.sp_iters, warmup=8)
@@ -670,7 +675,6 @@ def main():
     if store is not None:  # every step of the last rollout-store launch
         bad += int(((store["flags"] & errs) != 0).sum().item())
     faults = eng.faults()
-    handoffs = partner_stats(lib) if headline == "rollout_store" else None
     rets, cnts = gather_returns(ep_ret, ep_cnt.to(torch.int64), n_global=T * world)
     episodes = int(cnts.sum().item())
 
@@ -755,8 +759,8 @@ def main():
             "error_flags": bad,
             "launch_faults": faults,
         }
-        if handoffs is not None:  # the rollout store's partner hand-offs over this process (warm-up included)
-            out["partner_handoffs"] = handoffs
+        if handoffs is not None:  # the headline's partner hand-offs (its warm-up and timed launches)
+            out["partner_handoffs"] = dict(handoffs, row_blocks_per_launch=RK * T // 64)
         for v in variants[1:]:
             s = with_traffic(summary(recs[v]))
             s.pop("plan")
