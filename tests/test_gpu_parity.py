@@ -287,9 +287,9 @@ def test_rollout_equals_step_chain(P, K, refill_fused, pipeline, R):
     _check_rollout_vs_chain(P, K, refill_fused, pipeline, R)
 
 
-def _check_rollout_vs_chain(P, K, refill_fused, pipeline, R, partner_lead=None, launches=None):
+def _check_rollout_vs_chain(P, K, refill_fused, pipeline, R, partner_lead=None, launches=None, n=1024):
     import torch
-    n, seed = 1024, 11
+    seed = 11
     launches = launches or (5 if K <= 16 else 3)
     chain = engine(n, P, refill_period=R)
     fused = engine(n, P, refill_period=R, refill_fused=refill_fused, pipeline=pipeline, partner_lead=partner_lead)
@@ -366,6 +366,16 @@ def test_partner_handoff_equals_step_chain(P, lead, pipeline):
     _native.check(fused.lib, fused.lib.spl_debug_partner_stats(st, 1))
     if lead < 0:
         assert st[0] > 0, (st[0], st[1])  # the partners stored handed-off blocks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline,n", [("always", 1000), ("always", 1156), ("dealer2", 1000), ("dealer2", 1156)])
+def test_partner_handoff_ragged_grids_equal_step_chain(pipeline, n):
+    """Forced partner hand-off on grids whose last workgroup is partial or has no neighbour
+    (n = 1000: 16 two-wave workgroups, the last one ragged; 1 156: an odd count of 64-table blocks):
+    those teams keep their rows (pair and neighbour checks), every other team hands off, and the
+    outputs equal the chained spl_step."""
+    _check_rollout_vs_chain(2, 32, True, pipeline, 16, partner_lead=-1, launches=2, n=n)
 
 
 @pytest.mark.parametrize("pipeline", [True, "always", False])
