@@ -277,13 +277,19 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int kChunkBlocks = kChunk / 1024;  // 31: blocks w, w + 8, w + 16, w + 24 of wave w
 constexpr int kBlocksPerWave = (kChunkBlocks + kWaves - 1) / kWaves;  // 4 (3 for the last wave)
-__device__ __forceinline__ void issue_chunk(const uint8_t *W, int chunk, uint8_t *slot, int wave, int lane) {
-    const uint8_t *src = W + (size_t)chunk * kChunk + lane * 16;
+// the image as a buffer resource: the chunk and block offsets go in the scalar offset, the lane's
+// 16 bytes in a constant VGPR, so an LDS-DMA issue costs no VALU (the 64-bit per-lane address of
+// global_load_lds took a v_lshl_add_u64 per load)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc(const uint8_t *W) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(W), (short)0, 0x7FFFFFF0, 0x00020000);
+}
+__device__ __forceinline__ void issue_chunk(__amdgpu_buffer_rsrc_t rs, int chunk, uint8_t *slot, int wave, int lane) {
 #pragma unroll
     for (int i = 0; i < kBlocksPerWave; ++i) {
         const int blk = wave + kWaves * i;
         if (blk < kChunkBlocks)
-            __builtin_amdgcn_global_load_lds(src + blk * 1024, (lds_void *)(slot + blk * 1024), 16, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(slot + blk * 1024), 16, lane * 16,
+                                                     chunk * kChunk + blk * 1024, 0, 0);
     }
 }
 
@@ -519,7 +525,10 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
     constexpr bool kActor = kSample || !kCritic;
     constexpr int kTotal = kCritic ? (kActor ? kAllChunks : kCriticChunks) : kActorChunks;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+    // the wave index made wave-uniform for the compiler (SGPR), so the ring's LDS slot addresses stay
+    // scalar (M0 of the LDS-DMA loads) instead of readfirstlane'd VGPR arithmetic per load
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, r = lane & 15,
+              g = lane >> 4;
     // rows [rbase, rend) of this workgroup: tables rbase.. directly, or positions of the grouped
     // order (one network per workgroup: the group whose workgroup range holds blockIdx.x)
     int64_t rbase = (int64_t)blockIdx.x * kRowsPerBlock, rend = a.n;
@@ -539,9 +548,10 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
     auto table_of = [&](int i) -> int64_t { return a.order ? (int64_t)a.order[tbase + i] : tbase + i; };
     uint8_t *ring = lds;
     uint8_t *ms = lds + kLdsMask + wave * kMaskWave;
+    const __amdgpu_buffer_rsrc_t wrs = image_rsrc(W);
 
 #pragma unroll
-    for (int c = 0; c < kSlots - 1; ++c) issue_chunk(W, c, ring + c * kChunk, wave, lane);
+    for (int c = 0; c < kSlots - 1; ++c) issue_chunk(wrs, c, ring + c * kChunk, wave, lane);
 
     // grouped rows: the wave's table ids, one load (lane i < valid holds row i's), then shuffles
     const int32_t tid_own = (a.order && lane < valid) ? a.order[tbase + lane] : 0;
@@ -592,7 +602,7 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
         __builtin_amdgcn_s_barrier();  // everyone's part landed; slot c-1 is free
         asm volatile("" ::: "memory");
         const int nxt = c + kSlots - 1 < kTotal ? c + kSlots - 1 : kTotal - 1;  // past the end: harmless reload
-        issue_chunk(W, nxt, ring + ((c + kSlots - 1) % kSlots) * kChunk, wave, lane);
+        issue_chunk(wrs, nxt, ring + ((c + kSlots - 1) % kSlots) * kChunk, wave, lane);
         const uint8_t *slot = ring + (c % kSlots) * kChunk;
         ++c;
         return slot;

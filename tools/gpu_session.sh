@@ -105,6 +105,11 @@ for step in "$@"; do
         run pol_fold_$i 200 python tools/bench_policy.py --fused-only --iters 30
         SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_prefold.so run pol_prefold_$i 200 python tools/bench_policy.py --fused-only --iters 30
       done ;;
+    ringab)  # the actor's ring issue (uniform wave index, buffer-resource LDS DMA) vs before (ablate/lib_prering.so)
+      for i in 1 2 3; do
+        run pol_ring_$i 200 python tools/bench_policy.py --fused-only --iters 30
+        SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_prering.so run pol_prering_$i 200 python tools/bench_policy.py --fused-only --iters 30
+      done ;;
     poltest1) run pytest_pol1 300 python -u -m pytest tests/test_gpu_policy.py -x -q --timeout 200 --timeout-method thread ;;
     selfplay) run sp_pool 300 python tools/bench_selfplay.py
               run sp_frozen 300 python tools/bench_selfplay.py --opponent frozen ;;
