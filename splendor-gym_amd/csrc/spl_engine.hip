@@ -2912,9 +2912,8 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         auto slot_of = [&](int j) { return A.deleg + ((size_t)dl.pair * kDelegTasks + j) * kDelegPayload; };
         int pend = -1, pend_k = -1;  // producer: task staged at step pend_k, ready flag not yet set
         uint32_t staged = 0u;        // producer: tasks staged (not stored here)
-        // partner hand-off, producer side: tasks posted, the one staged but not yet READY, and the
-        // partner's progress and this side's next slot flag (loaded one step ahead)
-        // consumer side: the partner's tasks seen and the flag of its next slot (loaded a step ahead)
+        // partner hand-off: tasks posted (pseq) and the one staged but not yet READY (ppend), partner
+        // tasks seen (cseq); the flags and the partner's progress come from the poller's LDS snapshots
         uint32_t pseq = 0u, cseq = 0u;
         int ppend = -1, ppend_k = 0;
         for (int k = 0; k < K; ++k) {
@@ -2924,7 +2923,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                     flag_store(pl.line(pt_ready_line(ppend)), pt_flag(pl.e, ppend_k, kPtReady));
                     ppend = -1;
                 }
-                // at most one of the partner's tasks per step, between this team's steps (the dealer's
+                // at most one of the partner's tasks per step, between this team's steps (the poller's
                 // snapshot of its next slot, if it is for the task this wave expects)
                 const uint64_t nx = lds_poll64(&L.pt.in[2]);
                 if ((uint32_t)(nx >> 32) == cseq && pt_serve_v<P>(pl, cseq, (uint32_t)nx, L.rows, L, S.obs, A.n) &&
@@ -3037,9 +3036,8 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                     L.dl.rnd[b][lane] = uniform_draw(S.policy_seed, (uint64_t)(S.table0 + t), ply0 + (uint64_t)(k + 2));
                 lds_publish(&L.dl.odone, (uint32_t)(k + 1));  // slot b is free again
             }
-            if (pl.on) {  // progress out; the partner's and the next slot's flag in, for the next decision
+            if (pl.on)  // this side's progress, for the partner's decisions (a write-through store, no wait)
                 flag_store(pl.line(pt_progress_line(pl.side)), pl.e << 16 | (uint32_t)(k + 1));
-            }
             WSSTAMP(3, k);
         }
         if (pl.on) {
