@@ -77,6 +77,11 @@ for step in "$@"; do
       for i in 1 2; do for ld in 0 2 4; do
         run head_lead${ld}_$i 300 python3 bench.py --no-cpu-baseline --only --partner-lead $ld
       done; done ;;
+    leadsweep)  # the partner lead for both store kernels: headline and C4 at lead 0 / 4 / 8, alternating
+      for i in 1 2; do for ld in 0 4 8; do
+        run head_lead${ld}_$i 300 python3 bench.py --no-cpu-baseline --only --partner-lead $ld
+        run c4_lead${ld}_$i 300 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 --only --partner-lead $ld
+      done; done ;;
     pmcstep) bash tools/pmc.sh ${TAG}_2p_step 2 65536 step all || exit 1 ;;
     stamps) run stamps 300 python3 tools/stamps.py --run ;;
     wsstamps4) WS_P=4 WS_T=32768 WS_RAW=$O/wsstamps4_raw_$TAG.npz run wsstamps4 300 python3 tools/wsstamps.py --run ;;
