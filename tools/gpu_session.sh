@@ -82,6 +82,11 @@ for step in "$@"; do
         run head_lead${ld}_$i 300 python3 bench.py --no-cpu-baseline --only --partner-lead $ld
         run c4_lead${ld}_$i 300 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 --only --partner-lead $ld
       done; done ;;
+    stepntab)  # k_step_ws row stores non-temporal (-DSPL_STEP_OBS_NT=true, ablate/lib_stepnt.so) vs plain, alternating
+      for i in 1 2 3; do
+        run step_plain_$i 300 python3 bench.py --mode step --only --no-cpu-baseline --sp-tables 0
+        SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_stepnt.so run step_nt_$i 300 python3 bench.py --mode step --only --no-cpu-baseline --sp-tables 0
+      done ;;
     pmcstep) bash tools/pmc.sh ${TAG}_2p_step 2 65536 step all || exit 1 ;;
     stamps) run stamps 300 python3 tools/stamps.py --run ;;
     wsstamps4) WS_P=4 WS_T=32768 WS_RAW=$O/wsstamps4_raw_$TAG.npz run wsstamps4 300 python3 tools/wsstamps.py --run ;;
