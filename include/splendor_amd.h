@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 7  /* 7: spl_ctx_set_partner_lead, spl_debug_partner_stats (six-wave dealer partner hand-off);
+#define SPL_ABI_VERSION 7  /* 7: spl_ctx_set_partner_lead, spl_debug_partner_stats (rollout-store partner hand-off);
                               6: SPL_F_FAULT + spl_ctx_faults (a lost hand-off in a rollout launch is reported);
                               5: spl_step_args_t.obs_u8 (compact observation), gate_terminated / gate_flags */
 

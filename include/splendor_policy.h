@@ -33,7 +33,8 @@ extern "C" {
 #endif
 
 #define SPL_POLICY_ABI 4  /* 2: precision argument, args->image describes the image; 3: obs_u8;
-                             4: fp32 images as two fp16 planes (spl_policy_bytes changed) */
+                             4: fp32 images as two fp16 planes (spl_policy_bytes changed); each chunk also
+                                carries its rows' tanh factors (same size: pack and act from one library) */
 
 #define SPL_PREC_FP32 0
 #define SPL_PREC_BF16 1
