@@ -228,6 +228,19 @@ def load_pmc_traffic(kernel, tables, steps_per_launch):
     return None, None
 
 
+def node_fields(census, metric):
+    """The JSON line's node fields from parallel.device_census: n_gpus = the
+    number of DISTINCT devices the ranks ran on, ranks, the device identities and shared_device; when
+    ranks share a device the metric is relabelled, as that run is a rehearsal, not a node figure."""
+    shared = bool(census["shared_device"])
+    if shared:
+        metric = metric.replace("(whole node)", f"(shared-device rehearsal: {census['ranks']} ranks on "
+                                                f"{census['devices']} GPU{'s' if census['devices'] != 1 else ''}, "
+                                                "not a node figure)")
+    return {"metric": metric, "n_gpus": census["devices"], "ranks": census["ranks"],
+            "devices": census["identities"], "shared_device": shared}
+
+
 def selfplay_line(dev, rank, world, N, iters, warmup):
     """BASELINE config 5 per GPU: the PPO rollout step of ppo_splendor.py:227-269 for N tables —
     the agent's fused fp32 ActorCritic (get_action_and_value: actor + critic + masked sample) and
@@ -332,6 +345,62 @@ def selfplay_line(dev, rank, world, N, iters, warmup):
                                    "DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of 12 frozen "
                                    "snapshots per episode, greedy), reset after done; hipGraph replays",
                        "tables_per_gpu": N, "weights": "reference checkpoint runs/ppo_splendor/ppo_splendor_latest.pt"}}
+
+
+def caller_path_line(n_envs=16, iters=150, warmup=10):
+    """The UNCHANGED ppo_splendor.py rollout loop: `n_envs` envs built by
+    training_utils.make_env (DualStepNativeWrapper(SplendorEnv()) with the random opponent, each reset
+    with its own seed), driven one env at a time in Python exactly as ppo_splendor.py:235-269 does —
+    env.dual_step(action), env.reset() after done.  The agent's actions are uniform over each env's
+    legal mask (numpy), so the line times the env path alone, not the torch agent.  Every
+    SplendorEnv.step here is a one-table spl_step launch + one synchronous device->host copy of its
+    ~1.3 KB of outputs; the line reports env-steps/s (every SplendorEnv.step call: agent, opponent and
+    the openings after resets) and the time per SplendorEnv.step."""
+    import numpy as np
+    from training_utils import make_env
+    np.random.seed(0)
+    envs = [make_env(1000 + i, use_dual_player=True)() for i in range(n_envs)]
+    clock = {"n": 0, "s": 0.0}
+    for w in envs:  # time every SplendorEnv.step (launch + synchronous copy)
+        inner = w.env
+        raw = inner.step
+
+        def timed(action, raw=raw):
+            t = time.perf_counter()
+            r = raw(action)
+            clock["s"] += time.perf_counter() - t
+            clock["n"] += 1
+            return r
+        inner.step = timed
+    masks = [w.env.legal_mask() for w in envs]
+    rng = np.random.default_rng(1)
+
+    def loop(k):
+        for _ in range(k):
+            for i, w in enumerate(envs):
+                legal = np.flatnonzero(masks[i])
+                a = int(rng.choice(legal)) if len(legal) else 0
+                _, _, _, _, done, info = w.dual_step(a)
+                if done:
+                    _, info = w.reset()
+                masks[i] = info["action_mask"]
+
+    loop(warmup)
+    clock.update(n=0, s=0.0)
+    t0 = time.perf_counter()
+    loop(iters)
+    el = time.perf_counter() - t0
+    steps = clock["n"]
+    return {"metric": f"env-steps/sec, unchanged ppo_splendor.py loop: {n_envs} DualStepNativeWrapper(SplendorEnv()) "
+                      "stepped one at a time from Python",
+            "value": round(steps / el, 1), "unit": "env-steps/s", "env_steps": steps, "loop_iterations": iters,
+            "us_per_splendorenv_step": round(clock["s"] / max(1, steps) * 1e6, 2),
+            "us_per_dual_step": round(el / (iters * n_envs) * 1e6, 2),
+            "host_share": round(1.0 - clock["s"] / el, 4),
+            "note": "host-bound: one launch + one synchronous copy per SplendorEnv.step; the batched "
+                    "DualStepVectorEnv (config5_selfplay) steps every table in one launch; agent forward excluded",
+            "config": {"workload": "ppo_splendor.py:151-159,235-269 rollout loop shape, random legal agent actions, "
+                                   "random_opponent", "envs": n_envs}}
 
 
 def partner_stats(lib, clear=False):
@@ -461,6 +530,8 @@ def main():
     ap.add_argument("--sp-tables", type=int, default=65536,
                     help="tables per GPU of the config-5 self-play line (0 = skip it)")
     ap.add_argument("--sp-iters", type=int, default=64, help="timed dual steps of the config-5 line")
+    ap.add_argument("--caller-envs", type=int, default=16,
+                    help="envs of the unchanged ppo_splendor.py caller-path line (0 = skip it)")
     ap.add_argument("--c4-tables", type=int, default=32768,
                     help="tables per GPU of the config-4 share line (4 players; 0 = skip)")
     ap.add_argument("--c4-pipeline", default=True, type=lambda v: {"auto": True}.get(v, v),
@@ -484,13 +555,19 @@ def main():
     import torch
     from splendor_gym import _native
     from splendor_gym.device import Engine
-    from splendor_gym.parallel import barrier, gather_returns, init_distributed, local_device, max_over_ranks
+    from splendor_gym.parallel import (barrier, device_census, device_identity, gather_returns, init_distributed,
+                                       local_device, max_over_ranks)
 
     rank, world, local = init_distributed()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dev = local_device(local)
     torch.cuda.set_device(dev)
+    # which physical GPU each rank drives: n_gpus counts distinct devices, not ranks
+    census = device_census(device_identity(dev))
+    if census["shared_device"] and rank == 0:
+        print(f"warning: {census['ranks']} ranks share {census['devices']} device(s): {census['identities']}",
+              file=sys.stderr)
     T, P = args.tables, args.players
     R = args.refill_every or REFILL_EVERY[P]
     RK = args.rollout_k
@@ -669,6 +746,9 @@ def main():
     if args.c4_tables > 0 and not args.only and args.players == 2:
         c4 = c4_share_line(dev, rank, world, args.c4_tables, launches=8, warmup=2, pipeline=args.c4_pipeline,
                            partner_lead=args.partner_lead)
+    caller = None
+    if args.caller_envs > 0 and not args.only and rank == 0 and args.players == 2:
+        caller = caller_path_line(args.caller_envs)
     # correctness canaries on the measured run: no error flags, episodes completed
     errs = _native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT | _native.F_FAULT
     bad = int(((eng.flags & errs) != 0).sum().item())
@@ -729,11 +809,12 @@ def main():
         main_s = with_traffic(summary(recs[headline]))
         roof = main_s["roofline"]
         plan = main_s["plan"]
+        node = node_fields(census, f"env-steps/sec (whole node), {P}p {T} tables/GPU")
         out = {
-            "metric": f"env-steps/sec (whole node), {P}p {T} tables/GPU",
+            "metric": node.pop("metric"),
             "value": main_s["value"],
             "unit": "env-steps/s",
-            "n_gpus": world,
+            **node,
             "steps": plan["K"],
             "warmup": plan["W"],
             "ms_per_step": main_s["ms_per_step"],
@@ -765,10 +846,12 @@ def main():
             s = with_traffic(summary(recs[v]))
             s.pop("plan")
             out["in_place_l3" if v == "rollout_inplace" else ("other_mode" if v == "step" else v)] = s
-        if sp is not None:
-            out["config5_selfplay"] = sp
-        if c4 is not None:
-            out["config4_share"] = c4
+        if caller is not None:
+            out["caller_path"] = caller
+        for key, line in (("config5_selfplay", sp), ("config4_share", c4)):
+            if line is not None:
+                line["metric"] = node_fields(census, line["metric"])["metric"]
+                out[key] = line
         print(json.dumps(out))
     eng.close()
     if world > 1:

@@ -157,13 +157,14 @@ int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
  * Turned off for grids larger than the resident workgroup capacity (pairs might not run together).
  * Default: SPL_DELEG_EVERY (DESIGN.md §2 gives the measured A/B).  Results are identical either way. */
 int spl_ctx_set_rollout_delegation(spl_ctx_t *ctx, int every);
-/* Partner hand-off of the rollout-store kernels (per-step outputs at 64 tables per team: the two-wave
- * k_rollout_store_<P>p and the six-wave dealer k_rollout_store_dealer2_<P>p, grids resident at once):
- * a 64-table team that falls `lead` or more steps behind the same team of the workgroup on the
- * neighbouring XCC hands whole steps of observation rows (its state words, ~6 KB) to that team's output
- * wave, which encodes and stores them between its own steps (the XCCs drain the rollout store at
- * different rates under load).  0 = off, -1 = hand off whenever a slot is free (tests).
- * Default SPL_PARTNER_LEAD (4; DESIGN.md §2 gives the measured A/B).  Results are identical either way. */
+/* Partner hand-off of the six-wave dealer's rollout store (k_rollout_store_dealer2_<P>p: per-step
+ * outputs, one 384-thread workgroup per CU, grids resident at once; the two-wave kernels have none since
+ * ABI 7's round-5 library): a 64-table team that falls `lead` or more steps behind the same team of the
+ * workgroup on the neighbouring XCC hands whole steps of observation rows (its state words, ~6 KB) to
+ * that team's output wave, which encodes and stores them between its own steps (the XCCs drain the
+ * rollout store at different rates under load).  0 = off, -1 = hand off whenever a slot
+ * is free (tests).  Other kernels ignore it.  Default SPL_PARTNER_LEAD (4; DESIGN.md §2 gives the
+ * measured A/B).  Results are identical either way. */
 int spl_ctx_set_partner_lead(spl_ctx_t *ctx, int lead);
 /* The name of the kernel spl_rollout launches for n tables of `players` players under the context's
  * settings (e.g. "k_rollout_store_2p", "k_rollout_inplace_half_4p"): every instantiation has a name

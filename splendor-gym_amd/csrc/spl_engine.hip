@@ -175,14 +175,15 @@ constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 #define SPL_DELEG_EVERY 0
 #endif
 #ifndef SPL_PARTNER_LEAD
-// partner hand-off of the rollout-store kernels (spl_ctx_set_partner_lead): a team hands a step's
-// rows to its neighbouring-XCC partner when that one is this many steps ahead.  With the flag words
-// polled by a wave that issues no row stores (the dealer, or the two-wave kernel's rules wave) and
-// arms alternating on one box: C4 (six-wave dealer) median launch 1 081-1 084 (lead 4) / 1 076-1 080
-// (lead 2) vs 1 098-1 104 us off (profiles/r04/partner_ab_r04u.txt); the headline (two-wave, 2p x
-// 65 536) 2 027-2 036 (lead 4) / 2 048-2 060 (lead 2) vs 2 055-2 061 us off, ~12 000 of 131 072
-// team-steps handed off per launch (partner_ab_head_r04zb.txt).  Polled by the output wave itself
-// the hand-off was slower than off (partner_ab_r04n.txt).
+// partner hand-off of the six-wave dealer's rollout store (spl_ctx_set_partner_lead): a team hands a
+// step's rows to its neighbouring-XCC partner when that one is this many steps ahead.  With the flag
+// words polled by the dealer wave (it issues no row stores) and arms alternating on one box: C4 median
+// launch 1 081-1 084 (lead 4) / 1 076-1 080 (lead 2) vs 1 098-1 104 us off
+// (profiles/r04/partner_ab_r04u.txt).  Polled by the output wave itself the hand-off was slower than
+// off (partner_ab_r04n.txt).  Round 5: the two-wave kernels (the headline) have no partner hand-off —
+// at four workgroups per CU their sc1-load consumer was outside the guide's measured cross-XCD
+// envelope, and it bought 1.2-1.6 %; the six-wave dealer runs ONE workgroup per CU,
+// the guide's first measured row.
 #define SPL_PARTNER_LEAD 4
 #endif
 #ifndef SPL_XCD_MAP
@@ -2456,7 +2457,6 @@ struct PartnerLink {
     __device__ __forceinline__ uint8_t *slot(int j) const { return pay + (size_t)j * kDelegPayload; }
 };
 constexpr uint32_t kPtReady = 1u, kPtTaken = 2u;
-constexpr int kPartnerForced = -1000;  // the two-wave kernel's `deleg` for lead -1 (hand off whenever a slot is free)
 constexpr uint64_t kPartnerWait = 500000;  // 5 ms of s_memrealtime (100 MHz): the consumer's wait for DONE
 __device__ __forceinline__ uint32_t pt_flag(uint32_t e, int k, uint32_t st) { return e << 16 | (uint32_t)k << 2 | st; }
 __device__ unsigned long long g_partner_stats[2];  // tasks stored by the partner / claimed back (diagnostics)
@@ -2520,6 +2520,35 @@ __device__ __forceinline__ void pt_drain(const PartnerLink &pl, uint32_t &cseq, 
         }
         if (__builtin_amdgcn_s_memrealtime() - t_start > kPartnerWait) return;
         __builtin_amdgcn_s_sleep(8);
+    }
+}
+// producer, at the end of its steps — and on a fault of its workgroup: the task staged
+// last (if any) turns READY, DONE is posted behind every READY flag (the partner's pt_drain stops
+// waiting), then every task the partner has not taken is claimed back by the same compare-and-swap
+// and its rows are stored here: each handed-off step's rows are stored once, whatever happened after
+template <int P>
+__device__ __forceinline__ void pt_close(const PartnerLink &pl, int ppend, int ppend_k, uint32_t pseq, uint8_t *rows,
+                                         const Consts &C, int32_t *obs, int n, int t0) {
+    if (ppend >= 0) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the staged words have completed
+        flag_store(pl.line(pt_ready_line(ppend)), pt_flag(pl.e, ppend_k, kPtReady));
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // every READY flag has completed before DONE
+    flag_store(pl.line(pt_done_line(pl.side)), pl.e);
+    if (pseq == 0u) return;
+    uint32_t mine = 0u;  // lane j: slot j's flag (relaxed agent load: global_load sc1)
+    if (lane_id() < kPartnerSlots)
+        mine = __hip_atomic_load(pl.line(pt_ready_line(pl.side * kPartnerSlots + lane_id())), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t rm = __ballot(lane_id() < kPartnerSlots && (mine & 3u) == kPtReady && (mine >> 16) == pl.e);
+    for (; rm; rm &= rm - 1) {
+        const int j = __ffsll((unsigned long long)rm) - 1;
+        const uint32_t vj = (uint32_t)__builtin_amdgcn_readlane((int)mine, j);
+        uint32_t *f = pl.line(pt_ready_line(pl.side * kPartnerSlots + j));
+        if (!pt_claim(f, vj)) continue;
+        const int kk = (int)((vj >> 2) & 0x3FFFu);
+        pt_store_task<P>(pl.slot(pl.side * kPartnerSlots + j), rows, C, obs + ((size_t)kk * (size_t)n + (size_t)t0) * kObsDim);
+        if (lane_id() == 0) atomicAdd(&g_partner_stats[1], 1ull);
     }
 }
 
@@ -2699,19 +2728,17 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         }
     }
     // partner hand-off (per-step outputs, 64 tables per team; see PartnerLink): the six-wave dealer
-    // passes the lead in steps as deleg_every (0 = off, -1 = forced), the two-wave kernel as -lead
-    // (deleg_every >= 4 is its older static delegation; kPartnerForced = forced).  Team j of workgroups
-    // b and b ^ 1, both full, K < 2^14 (the step fits a flag).
+    // only (one workgroup per CU; round 5: not in the two-wave kernels), which passes the lead in steps
+    // as deleg_every (0 = off, -1 = forced).  Team j of workgroups b and b ^ 1, both full, K < 2^14
+    // (the step fits a flag).
     PartnerLink pl{false, 0, 0, 0u, nullptr, nullptr, 0};
-    if constexpr (kStore && TPW == 64) {
-        int lead = 0;
-        if constexpr (kDealer) lead = wr.block >= 0 ? deleg_every : 0;
-        else lead = deleg_every < 0 ? (deleg_every == kPartnerForced ? -1 : -deleg_every) : 0;
+    if constexpr (kStore && kDealer) {
+        const int lead = wr.block >= 0 ? deleg_every : 0;
         if (lead != 0 && K < (1 << 14)) {
             const uint32_t b = blockIdx.x, pb = b ^ 1u;
-            const int team = kDealer ? wr.block - 2 * wg_block() : 0;
-            const int t0p = kDealer ? (2 * wg_block_of(pb) + team) * 64 : wg_block_of(pb) * 64;
-            const int pair = kDealer ? (int)(b >> 1) * 2 + team : (int)(b >> 1);
+            const int team = wr.block - 2 * wg_block();
+            const int t0p = (2 * wg_block_of(pb) + team) * 64;
+            const int pair = (int)(b >> 1) * 2 + team;
             if (pb < gridDim.x && t0 + 64 <= A.n && t0p + 64 <= A.n && pair < A.n / 128) {
                 pl.on = true;
                 pl.lead = lead;
@@ -2775,7 +2802,6 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         bool pool_dirty = false;
         const uint64_t ply0 = S.ply + (S.ply_base ? *S.ply_base : 0ull);
         uint64_t cur_mask = 0ull;
-        uint32_t pv[3] = {0u, 0u, 0u}, pps = 0u, pcs = 0u;  // two-wave partner poller (loaded a step ahead)
         const uint64_t below = (1ull << lane) - 1ull;
 #ifdef SPL_STAMPS
         int rst_lo[kWsStamps] = {0}, rst_hi[kWsStamps] = {0};
@@ -2843,17 +2869,6 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             if constexpr (kDealer) {
                 lds_publish(&L.dl.rdone, (uint32_t)(k + 1));  // hand-off of step k
             } else {
-                if (pl.on) {  // the partner poller of the two-wave kernel: the words loaded last step, then new loads
-                    if (k > 0)
-                        pt_publish(L.pt, (uint32_t)__builtin_amdgcn_readfirstlane(pv[0]),
-                                   (uint32_t)__builtin_amdgcn_readfirstlane(pv[1]), pps,
-                                   (uint32_t)__builtin_amdgcn_readfirstlane(pv[2]), pcs);
-                    pps = lds_poll(&L.pt.seq[0]);
-                    pcs = lds_poll(&L.pt.seq[1]);
-                    pv[0] = flag_load(pl.line(pt_progress_line(pl.side ^ 1)));
-                    pv[1] = flag_load(pl.line(pt_ready_line(pl.side * kPartnerSlots + (int)(pps % kPartnerSlots))));
-                    pv[2] = flag_load(pl.line(pt_ready_line((pl.side ^ 1) * kPartnerSlots + (int)(pcs % kPartnerSlots))));
-                }
                 ws_sync();  // hand-off of step k
             }
             WSSTAMP(3, k);
@@ -2935,6 +2950,9 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                     // steps k.. are not stored: their flags say so (the blocks keep stale rows)
                     for (int j = per_step ? k : 0; j < K && (per_step || j == 0); ++j)
                         if (valid) S.flags[(per_step ? (size_t)j * (size_t)A.n : 0) + t] = (uint8_t)SPL_F_FAULT;
+                    // steps before k that were handed to the partner: DONE, and those it has not taken are
+                    // stored here (they were stepped before the fault)
+                    if (pl.on) pt_close<P>(pl, ppend, ppend_k, pseq, L.rows, L, S.obs, A.n, t0);
                     signal_fault(S);
                     return;
                 }
@@ -3041,29 +3059,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             WSSTAMP(3, k);
         }
         if (pl.on) {
-            if (ppend >= 0) {
-                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-                flag_store(pl.line(pt_ready_line(ppend)), pt_flag(pl.e, ppend_k, kPtReady));
-            }
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // every READY flag has completed before DONE
-            flag_store(pl.line(pt_done_line(pl.side)), pl.e);
-            if (pseq > 0u) {  // claim back the tasks the partner has not taken, and store them here
-                uint32_t mine = 0u;  // lane j: slot j's flag (relaxed agent load: global_load sc1)
-                if (lane < kPartnerSlots)
-                    mine = __hip_atomic_load(pl.line(pt_ready_line(pl.side * kPartnerSlots + lane)), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-                uint64_t rm = __ballot(lane < kPartnerSlots && (mine & 3u) == kPtReady && (mine >> 16) == pl.e);
-                for (; rm; rm &= rm - 1) {
-                    const int j = __ffsll((unsigned long long)rm) - 1;
-                    const uint32_t vj = (uint32_t)__builtin_amdgcn_readlane((int)mine, j);
-                    uint32_t *f = pl.line(pt_ready_line(pl.side * kPartnerSlots + j));
-                    if (!pt_claim(f, vj)) continue;
-                    const int kk = (int)((vj >> 2) & 0x3FFFu);
-                    pt_store_task<P>(pl.slot(pl.side * kPartnerSlots + j), L.rows, L,
-                                     S.obs + ((size_t)kk * (size_t)A.n + (size_t)t0) * kObsDim);
-                    if (lane == 0) atomicAdd(&g_partner_stats[1], 1ull);
-                }
-            }
+            pt_close<P>(pl, ppend, ppend_k, pseq, L.rows, L, S.obs, A.n, t0);
             pt_drain<P>(pl, cseq, L.rows, L, S.obs, A.n);  // then the partner's, until it is done
         }
 #ifdef SPL_STAMPS
@@ -4057,13 +4053,12 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     const int tpw = rollout_tpw(ctx, arena->n, arena->players);
     const bool p_out = per_step_outputs != 0;
     // delegation / partner pairs must run at the same time: off when the grid exceeds what is resident
-    // at once.  The two-wave kernel's `deleg`: the static delegation period (>= 4), else -lead of the
-    // partner hand-off (kPartnerForced for lead -1), else 0
-    int deleg = 0;
-    if ((int64_t)blocks_for(arena->n) <= resident) {
-        if (ctx->deleg_every > 0) deleg = ctx->deleg_every;
-        else if (ctx->partner_lead != 0) deleg = ctx->partner_lead < 0 ? kPartnerForced : -ctx->partner_lead;
-    }
+    // at once.  The two-wave kernel's `deleg`: the static delegation period (>= 4) or 0 (round 5: the
+    // partner hand-off is the six-wave dealer's only)
+    const int deleg = ((int64_t)blocks_for(arena->n) <= resident && ctx->deleg_every > 0) ? ctx->deleg_every : 0;
+    // the six-wave dealer's partner lead, likewise 0 unless every workgroup is resident (ADVICE r04:
+    // pipeline "dealer2" forced on a larger grid)
+    const int lead2 = (int64_t)((arena->n + 127) / 128) <= ctx->dealer2_resident[arena->players] ? ctx->partner_lead : 0;
 #define SPL_LAUNCH_WS(TPW, BLOCKS)                                                                           \
     DISPATCH_P(arena->players, if (p_out) {                                                                  \
         hipLaunchKernelGGL((RolloutKernel<PP, TPW, true>::fn), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
@@ -4076,7 +4071,7 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
         const unsigned blocks = (unsigned)((arena->n + 127) / 128);
         DISPATCH_P(arena->players, if (p_out) {
             hipLaunchKernelGGL((RolloutDealer2Kernel<PP, true>::fn), dim3(blocks), dim3(384), 0, s, A, ktables(ctx), S,
-                               (int)steps, fused, ctx->partner_lead);
+                               (int)steps, fused, lead2);
         } else {
             hipLaunchKernelGGL((RolloutDealer2Kernel<PP, false>::fn), dim3(blocks), dim3(384), 0, s, A, ktables(ctx), S,
                                (int)steps, fused, 0);

@@ -128,10 +128,15 @@ class Engine:
         """Serial of a launch that faulted since the last clear_faults() (0 = none): a lost internal
         hand-off in a dealer-variant rollout (include/splendor_amd.h spl_ctx_faults).  Reads the
         host-mapped fault word: no synchronisation, covers every launch that has finished."""
+        if self._fault_word is None:  # closed: the word was freed with the context (ADVICE r04)
+            return self._fault_carry
         return self._fault_carry or int(self._fault_word.value)
 
     def check_faults(self):
-        """Raise LaunchFault if a launch of this engine faulted (no synchronisation)."""
+        """Raise LaunchFault if a launch of this engine faulted (no synchronisation); RuntimeError
+        once the engine is closed (its context and fault word are gone)."""
+        if self.ctx is None:
+            raise RuntimeError("splendor engine: used after close()")
         f = self.faults()
         if f:
             raise LaunchFault(f"splendor engine: launch {f} lost an internal hand-off; its outputs from the faulted "
@@ -151,6 +156,8 @@ class Engine:
     def close(self):
         if getattr(self, "ctx", None) is not None and self.ctx.value:
             self.torch.cuda.synchronize(self.device)
+            self._fault_carry = self.faults()  # kept readable after the word is freed
+            self._fault_word = None
             self.lib.spl_ctx_destroy(self.ctx)
             self.ctx = None
 
@@ -219,6 +226,8 @@ class Engine:
         where it ended the game or was not applied get action -1 (written into `actions`) and are not
         moved (spl_step_args_t.gate_*; spl_dual_gate fused into this launch)."""
         torch = self.torch
+        if self.ctx is None:
+            raise RuntimeError("splendor engine: used after close()")
         if actions is None:
             actions = self.actions
         if not (isinstance(actions, torch.Tensor) and actions.device == self.device and actions.dtype == torch.int32

@@ -47,6 +47,35 @@ def local_device(local):
     return torch.device("cuda", local % max(1, torch.cuda.device_count()))
 
 
+def device_identity(device):
+    """The physical GPU behind `device` as a string that two processes on one node compare equal
+    exactly when they drive the same card: host name + PCI domain:bus:device when torch exposes them,
+    else the device UUID, else the visible index (with HIP_VISIBLE_DEVICES, which differs per process)."""
+    import socket
+    props = torch.cuda.get_device_properties(device)
+    pci = [getattr(props, a, None) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id")]
+    if all(isinstance(v, int) for v in pci):
+        ident = "pci %04x:%02x:%02x" % tuple(pci)
+    elif getattr(props, "uuid", None) is not None:
+        ident = f"uuid {props.uuid}"
+    else:
+        ident = f"index {torch.device(device).index} of HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES', '')}"
+    return f"{socket.gethostname()}/{ident}"
+
+
+def device_census(identity):
+    """Every rank's device identity (device_identity), gathered on every rank: how many ranks, how
+    many DISTINCT devices they run on, and whether any two share one (a rehearsal of N ranks on fewer
+    cards is not an N-GPU figure)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        ids = [identity]
+    else:
+        ids = [None] * dist.get_world_size()
+        dist.all_gather_object(ids, identity)
+    distinct = len(set(ids))
+    return {"ranks": len(ids), "devices": distinct, "shared_device": distinct < len(ids), "identities": ids}
+
+
 def _host_collectives():
     """gloo collectives run on host tensors here (its CUDA support is partial)."""
     return dist.get_backend() == "gloo"

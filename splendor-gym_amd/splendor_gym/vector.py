@@ -177,7 +177,10 @@ class SplendorVectorEnv:
         return self._stream
 
     def reset(self, *, seed=None, options=None):
-        self.engine.check_faults()
+        """Reset every table.  This is also the recovery from a faulted launch: a fault seen
+        since the last clear (step() raised LaunchFault for it) is cleared once every table has been
+        re-dealt, and reported as info["recovered_fault"] = the faulted launch's serial."""
+        fault = self.engine.faults()
         if self._unchecked and self.check_actions == "deferred":
             self._queue_check()
         self._raise_pending(block_all=True)
@@ -188,6 +191,9 @@ class SplendorVectorEnv:
         self.engine.reset(seeds=seeds, obs_out=b.obs, mask_out=b.mask)
         self._seeded = True
         info = {"action_mask": self._out(b.mask), "to_play": self._out(b.to_play)}
+        if fault:  # every table was just re-dealt: the undefined state is gone
+            self.engine.clear_faults()
+            info["recovered_fault"] = fault
         if self.to_numpy:
             info["_action_mask"] = np.ones(self.num_envs, bool)
             info["_to_play"] = np.ones(self.num_envs, bool)

@@ -34,16 +34,27 @@ def _forced_fault_rollout(eng, K, a, na, out):
         _native.check(lib, lib.spl_debug_set_spin_limit(-1))
 
 
-@pytest.mark.parametrize("P,pipeline", [(2, "dealer"), (4, "dealer"), (4, "dealer2")])
-def test_dealer_handoff_timeout_is_reported_and_recoverable(P, pipeline):
+@pytest.mark.parametrize("P,pipeline,lead", [(2, "dealer", None), (4, "dealer", None), (4, "dealer2", None),
+                                              (4, "dealer2", -1), (2, "dealer2", -1)])
+def test_dealer_handoff_timeout_is_reported_and_recoverable(P, pipeline, lead):
+    """... and with the six-wave dealer's partner hand-off forced (lead -1): a faulting
+    output wave posts DONE and stores the rows of the steps it had handed to its partner and the partner
+    had not taken, so EVERY step whose flags lack SPL_F_FAULT holds the rows a clean launch writes."""
     import torch
     from splendor_gym import _native
     from splendor_gym.device import Engine
     n, K = 1024, 16
-    eng = Engine(n, P, refill_period=16, pipeline=pipeline)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    # the clean launch from the same deals (three-wave dealer, no partner hand-off)
+    clean = Engine(n, P, refill_period=16, pipeline="dealer")
+    clean.reset(seeds=range(n))
+    a_c = torch.zeros(n, dtype=torch.int32, device=dev)
+    clean.sample_uniform(out=a_c, seed=1, ply=0)
+    out_c = _out(torch, K, n, dev)
+    clean.rollout(K, actions=a_c, next_actions=torch.empty_like(a_c), policy_seed=1, ply=1, out=out_c)
+    eng = Engine(n, P, refill_period=16, pipeline=pipeline, partner_lead=lead)
     assert eng.rollout_kernel_name(per_step=True) == f"k_rollout_store_{pipeline}_{P}p"
     eng.reset(seeds=range(n))
-    dev = eng.device
     a = torch.zeros(n, dtype=torch.int32, device=dev)
     na = torch.empty_like(a)
     eng.sample_uniform(out=a, seed=1, ply=0)
@@ -58,6 +69,12 @@ def test_dealer_handoff_timeout_is_reported_and_recoverable(P, pipeline):
     first = faulted.to(torch.int32).argmax(dim=0)
     tail = torch.arange(K, device=dev)[:, None] >= first[None, :]
     assert bool((faulted == (tail & faulted.any(dim=0)[None, :])).all())
+    # every step not flagged was stored, whoever stored its rows
+    ok = ~faulted
+    for name in ("obs", "mask", "reward", "terminated", "winner"):
+        assert torch.equal(out[name][ok], out_c[name][ok]), name
+    assert torch.equal(out["flags"][ok], out_c["flags"][ok])
+    clean.close()
     # Engine reports it loudly on the next use, without a synchronisation of its own
     with pytest.raises(_native.LaunchFault):
         eng.rollout(K, actions=a, next_actions=na, policy_seed=1, ply=1 + K, out=out)
@@ -87,7 +104,9 @@ def test_dealer_handoff_timeout_is_reported_and_recoverable(P, pipeline):
 
 
 def test_vector_env_raises_on_a_faulted_launch():
-    """SplendorVectorEnv checks its engine's fault word on every step and reset (no sync)."""
+    """SplendorVectorEnv checks its engine's fault word on every step (no sync) and raises; reset() is
+    the recovery: it re-deals every table, clears the fault and reports its serial in
+    info["recovered_fault"], and the env steps cleanly afterwards."""
     import torch
     from splendor_gym import _native
     from splendor_gym.vector import SplendorVectorEnv
@@ -102,8 +121,12 @@ def test_vector_env_raises_on_a_faulted_launch():
         a = torch.zeros(n, dtype=torch.int32, device=env.device)
         env.engine.sample_uniform(out=a, seed=3, ply=0)
         _forced_fault_rollout(env.engine, K, a, torch.empty_like(a), _out(torch, K, n, env.device))
+        serial = env.engine.faults()
+        assert serial != 0
         with pytest.raises(_native.LaunchFault):
             env.step(env.sample_actions(seed=4))
-        with pytest.raises(_native.LaunchFault):
-            env.reset(seed=0)
+        _, info = env.reset(seed=0)
+        assert info["recovered_fault"] == serial and env.engine.faults() == 0
+        obs, rew, term, trunc, info = env.step(env.sample_actions(seed=5))
+        assert env.engine.faults() == 0 and "recovered_fault" not in info
         env.close()

@@ -39,17 +39,27 @@ def store(K, n, dev):
             "final_obs": torch.zeros((K, n, 297), dtype=torch.int32, device=dev)}
 
 
-@pytest.mark.parametrize("P,n,R", [(2, 65536, 64), (4, 32768, 16)])
-def test_headline_rollout_65536_equals_step_chain_and_oracle(P, n, R):
-    """bench.py's headline (2p x 65 536: two-wave kernel at 64 tables per workgroup, fused refills) and
-    C4's per-GPU share (4p x 32 768 of 262 144 on 8 GPUs: the three-wave dealer variant) at full size:
-    two 128-step rollout launches equal the spl_step chain bit for bit; every 256th table is
-    replayed through the CPU oracle."""
+@pytest.mark.parametrize("P,n,R,lead,pipeline", [(2, 65536, 64, None, True), (2, 65536, 64, -1, True),
+                                                 (4, 32768, 16, None, True), (4, 32768, 16, -1, True),
+                                                 (2, 32768, 64, -1, "dealer2")])
+def test_headline_rollout_65536_equals_step_chain_and_oracle(P, n, R, lead, pipeline):
+    """bench.py's headline (2p x 65 536: two-wave kernel at 64 tables per workgroup, four workgroups per
+    CU, fused refills) and C4's per-GPU share (4p x 32 768 of 262 144 on 8 GPUs: the six-wave dealer,
+    one workgroup per CU) at full size: two 128-step rollout launches equal the spl_step chain bit for
+    bit; every 256th table is replayed through the CPU oracle.  lead -1 forces the partner hand-off
+    whenever a task slot is free: the six-wave dealer then hands rows between
+    every pair of workgroups with the most slot reuse its ring allows (also 2p x 32 768 on it), and the
+    two-wave headline kernel, which has no partner hand-off since round 5, must hand off nothing."""
+    import ctypes
     import torch
+    from splendor_gym import _native
     K, seed, launches = 128, 0, 2
     chain = engine(n, P, refill_period=R)
-    roll = engine(n, P, refill_period=R, refill_fused=True, pipeline=True)  # bench.py defaults
-    assert roll.rollout_kernel_name() == ("k_rollout_store_2p" if P == 2 else "k_rollout_store_dealer2_4p")
+    roll = engine(n, P, refill_period=R, refill_fused=True, pipeline=pipeline, partner_lead=lead)  # bench.py defaults
+    want = "k_rollout_store_2p" if (P == 2 and pipeline is True) else f"k_rollout_store_dealer2_{P}p"
+    assert roll.rollout_kernel_name() == want
+    pst = (ctypes.c_uint64 * 2)()
+    _native.check(roll.lib, roll.lib.spl_debug_partner_stats(pst, 1))
     chain.reset(seeds=range(n))
     roll.reset(seeds=range(n))
     dev = chain.device
@@ -84,8 +94,13 @@ def test_headline_rollout_65536_equals_step_chain_and_oracle(P, n, R):
             a_c = na
         assert torch.equal(a_r, a_c), launch
     assert torch.equal(st["c"][0], st["r"][0]) and torch.equal(st["c"][1], st["r"][1])
-    assert int(st["c"][1].sum()) > (100_000 if P == 2 else 200_000)  # one episode per ~77 (2p) / ~29 (4p) plies
+    assert int(st["c"][1].sum()) > (100_000 if n == 65536 else 50_000 if P == 2 else 200_000)  # one episode per ~77 (2p) / ~29 (4p) plies
     assert chain.download().tobytes() == roll.download().tobytes()
+    _native.check(roll.lib, roll.lib.spl_debug_partner_stats(pst, 0))
+    if want.startswith("k_rollout_store_dealer2") and lead == -1:
+        assert pst[0] > 1000, (pst[0], pst[1])  # many row blocks were stored by the partner
+    elif not want.startswith("k_rollout_store_dealer2"):
+        assert pst[0] == 0 and pst[1] == 0, (pst[0], pst[1])
 
 
 def test_sharded_equals_whole_4p():

@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -221,6 +222,42 @@ def test_gloo_two_ranks_gather_returns():
         assert ret == [i * 0.5 for i in range(1001)]
         assert cnt == [i % 7 for i in range(1001)]
         assert t == 1.25
+
+
+def _census_worker(rank, world, port, same, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.path.insert(0, REPO)
+    import bench
+    from splendor_gym.parallel import device_census, init_distributed
+    init_distributed(backend="gloo")
+    census = device_census("hostA/pci 0000:05:00" if same else f"hostA/pci 0000:0{rank + 5}:00")
+    rec = bench.node_fields(census, "env-steps/sec (whole node), 2p 65536 tables/GPU")
+    q.put((rank, census, rec))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("same", [True, False])
+def test_gloo_device_census_flags_shared_devices(same):
+    """two ranks on ONE card (the one-GPU rehearsal) report n_gpus 1, ranks 2,
+    shared_device true and a metric that is not a whole-node figure; two ranks on two cards report 2."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29400 + os.getpid() % 150 + (150 if same else 0)
+    procs = [ctx.Process(target=_census_worker, args=(r, 2, port, same, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, census, rec in res:
+        assert census["ranks"] == 2 and census["shared_device"] is same
+        assert rec["n_gpus"] == (1 if same else 2) and rec["ranks"] == 2 and rec["shared_device"] is same
+        assert ("whole node" in rec["metric"]) is (not same)
+        assert len(rec["devices"]) == 2
 
 
 def test_single_hip_runtime_after_load():

@@ -148,6 +148,9 @@ for step in "$@"; do
         run c4ab_${pl}_$i 300 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 --only --pipeline $pl
       done; done ;;
     abl32) bash tools/ablate_policy32.sh || exit 1 ;;  # k_act32 timing ablations (BUILD=1 here first)
+    chains) run step_chains 300 python3 tools/bench_step_chains.py ;;  # step mode as 1/2/4 independent chains
+    faultpart) run pytest_faultpart 600 python -u -m pytest tests/test_gpu_faults.py tests/test_gpu_parity.py \
+                   tests/test_gpu_headline.py -k "fault or partner or headline_rollout" -x -v --timeout 300 --timeout-method thread ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
