@@ -61,11 +61,25 @@ STEP_ALGO_BYTES = {p: 2 * s + 297 * 4 + 45 + 4 + 4 + 1 for p, s in STATE_BYTES.i
 # refills (random games last ~77 plies at 2p, ~29 at 4p)
 REFILL_EVERY = {2: 64, 3: 32, 4: 16}
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md chip table; no sparsity)
-# fp16 MFMA work of the fused fp32 ActorCritic (csrc/spl_policy32.hip, round 4) per table: every fp32
-# operand is two fp16 planes; layer 1 (297 -> 256, observation exact in fp16) takes 2 plane products,
-# layers 2 (256 -> 256) and 3 (256 -> 45) take 3; the critic's 256 -> 1 output runs on VALU, not counted
-ACTOR_MFMA_FLOP = 2 * (297 * 256 * 2 + 256 * 256 * 3 + 256 * 45 * 3)   # 766 464
-CRITIC_MFMA_FLOP = 2 * (297 * 256 * 2 + 256 * 256 * 3)                 # 697 344
+# 16-bit MFMA work of the fused fp32 ActorCritic (csrc/spl_policy32.hip) per table, per operand format
+# (precision): "fp32" = EXACT fp32 operands as three bf16 planes: layer 1 (297 -> 256, the observation
+# exact in one plane) takes 3 plane products, layers 2 (256 -> 256) and 3 (256 -> 45) take the 6 of
+# order <= 2; "fp32_f16x2" = two fp16 planes (22 significant bits): 2 and 3 products.  The critic's
+# 256 -> 1 output runs on VALU, not counted.
+MFMA_PRODUCTS = {"fp32": (3, 6), "fp32_f16x2": (2, 3)}
+
+
+def actor_critic_mfma_flop(precision):
+    """(actor, critic) 16-bit MFMA flop per table of get_action_and_value at `precision`."""
+    l1, hid = MFMA_PRODUCTS[precision]
+    return (2 * (297 * 256 * l1 + 256 * 256 * hid + 256 * 45 * hid), 2 * (297 * 256 * l1 + 256 * 256 * hid))
+
+
+PRECISION_DTYPE = {
+    "fp32": "fp32 (EXACT fp32 operands: three bf16 planes of 24 significant bits, the six plane products of "
+            "order <= 2 accumulated in fp32, dropped terms <= 2^-24 of each product; tanh to a few ulp)",
+    "fp32_f16x2": "fp32 within 2^-22 (two fp16 planes of 22 significant bits per operand, three plane products "
+                  "accumulated in fp32; NOT an exact fp32 operand representation)"}
 # the network's own fp32 work per table (2 x MACs of actor + critic), for the fp32-equivalent rate
 NET_FP32_FLOP = 2 * (297 * 256 + 256 * 256 + 256 * 45 + 297 * 256 + 256 * 256 + 256)
 ROLLOUT_K = 128    # env steps per spl_rollout launch = ppo_splendor.py's --num-steps default (:71)
@@ -241,7 +255,7 @@ def node_fields(census, metric):
             "devices": census["identities"], "shared_device": shared}
 
 
-def selfplay_line(dev, rank, world, N, iters, warmup):
+def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
     """BASELINE config 5 per GPU: the PPO rollout step of ppo_splendor.py:227-269 for N tables —
     the agent's fused fp32 ActorCritic (get_action_and_value: actor + critic + masked sample) and
     DualStepVectorEnv.dual_step with the reference's opponent supplier (current policy p=0.25, else
@@ -263,8 +277,8 @@ def selfplay_line(dev, rank, world, N, iters, warmup):
         return m
 
     agent = net()
-    agent_k = FusedActorCritic(agent, precision="fp32")
-    pool = OpponentPool(agent, pool_size=12, p_current=0.25, seed=99)
+    agent_k = FusedActorCritic(agent, precision=precision)
+    pool = OpponentPool(agent, pool_size=12, p_current=0.25, seed=99, precision=precision)
     for _ in range(12):
         pool.add_snapshot(net())
     env = DualStepVectorEnv(N, device=dev, opponent=pool, table0=rank * N, opponent_obs=False)
@@ -323,27 +337,29 @@ def selfplay_line(dev, rank, world, N, iters, warmup):
         torch.cuda.synchronize(dev)
         region_mark("config5_actor", "end")
     spread = launch_spread([a.elapsed_time(b) / 1e3 for a, b in ev])
-    flop = (ACTOR_MFMA_FLOP + CRITIC_MFMA_FLOP) * N
+    fa, fc = actor_critic_mfma_flop(precision)
+    flop = (fa + fc) * N
     tflops = flop / spread["median_s"] / 1e12
     env.close()
+    l1, hid = MFMA_PRODUCTS[precision]
+    kname = "k_act32<true, true>" if precision == "fp32" else "k_act32h<true, true>"
     return {"metric": f"env-steps/sec (whole node), 2p self-play, on-device fp32 ActorCritic, {N} tables/GPU",
             "value": round(2 * N * world * iters / el, 1), "unit": "env-steps/s",
             "ms_per_dual_step": round(el / iters * 1e3, 4), "iters": iters,
-            "dtype": "fp32 (fp32 operands as two fp16 planes of 22 significant bits, three plane products accumulated "
-                     "in fp32; torch fp32 tolerance 1e-5)",
+            "precision": precision, "dtype": PRECISION_DTYPE[precision],
             "roofline": {"bound": "mfma", "achieved": round(tflops, 1), "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(tflops / F16_MFMA_PEAK_TFLOPS, 4), "kernel": "k_act32<true, true>",
+                         "frac": round(tflops / F16_MFMA_PEAK_TFLOPS, 4), "kernel": kname,
                          "kernel_us": spread["us"], "flop_per_launch": flop,
                          "fp32_equivalent_tflops": round(NET_FP32_FLOP * N / spread["median_s"] / 1e12, 1),
-                         "flop_note": "fp16 MFMA work per table: actor 2*(297*256*2 + 256*256*3 + 256*45*3) + critic "
-                                      "2*(297*256*2 + 256*256*3) = 1 463 808 (two fp16 planes per fp32 operand: 2 plane "
-                                      "products in layer 1, 3 in layers 2-3; the critic's 256->1 output on VALU); "
-                                      "frac from the median of 16 eager launches (HIP events on the launch stream); "
+                         "flop_note": f"16-bit MFMA work per table: actor 2*(297*256*{l1} + 256*256*{hid} + 256*45*{hid}) "
+                                      f"+ critic 2*(297*256*{l1} + 256*256*{hid}) = {fa + fc} ({l1} plane products in "
+                                      f"layer 1, {hid} in layers 2-3; the critic's 256->1 output on VALU); frac from the "
+                                      "median of 16 eager launches (HIP events on the launch stream); "
                                       "fp32_equivalent_tflops = the network's 2 x MACs per table at that time",
                          "traffic": None},
-            "config": {"workload": "BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused, fp32-accurate two-plane fp16 MFMA) + "
-                                   "DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of 12 frozen "
-                                   "snapshots per episode, greedy), reset after done; hipGraph replays",
+            "config": {"workload": f"BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused, precision "
+                                   f"{precision}) + DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of "
+                                   "12 frozen snapshots per episode, greedy, same precision), reset after done; hipGraph replays",
                        "tables_per_gpu": N, "weights": "reference checkpoint runs/ppo_splendor/ppo_splendor_latest.pt"}}
 
 
@@ -739,9 +755,10 @@ def main():
         k_next = recs[v]["k_next"]
         if v == "rollout_store" and headline == "rollout_store":  # this line's hand-offs (warm-up included)
             handoffs = partner_stats(lib)
-    sp = None
+    sp = sp2 = None
     if args.sp_tables > 0 and not args.only:
-        sp = selfplay_line(dev, rank, world, args.sp_tables, args.sp_iters, warmup=8)
+        sp = selfplay_line(dev, rank, world, args.sp_tables, args.sp_iters, warmup=8, precision="fp32")
+        sp2 = selfplay_line(dev, rank, world, args.sp_tables, args.sp_iters, warmup=8, precision="fp32_f16x2")
     c4 = None
     if args.c4_tables > 0 and not args.only and args.players == 2:
         c4 = c4_share_line(dev, rank, world, args.c4_tables, launches=8, warmup=2, pipeline=args.c4_pipeline,
@@ -848,7 +865,7 @@ def main():
             out["in_place_l3" if v == "rollout_inplace" else ("other_mode" if v == "step" else v)] = s
         if caller is not None:
             out["caller_path"] = caller
-        for key, line in (("config5_selfplay", sp), ("config4_share", c4)):
+        for key, line in (("config5_selfplay", sp), ("config5_selfplay_f16x2", sp2), ("config4_share", c4)):
             if line is not None:
                 line["metric"] = node_fields(census, line["metric"])["metric"]
                 out[key] = line

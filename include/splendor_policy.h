@@ -8,11 +8,18 @@
  * training_utils.py:263-276 frozen_policy_from / scripts/eval_suite.py model_greedy_policy_from
  * for opponents.  These entry points evaluate that network for a whole batch of tables in one
  * launch: observations (int32 [n][297]) and masks (int8 [n][45]) straight from the engine, tanh /
- * softmax / sampling fused.  Two precisions:
- *   SPL_PREC_FP32 (default)  the reference's fp32: fp32-accurate products (two fp16 planes per
- *                            operand, 22 significant bits, weights scaled per row by a power of two;
- *                            three plane products accumulated in fp32 on v_mfma_f32_16x16x32_f16;
- *                            spl_policy32.hip), fp32 tanh
+ * softmax / sampling fused.  Three precisions:
+ *   SPL_PREC_FP32 (default)  the reference's fp32 with EXACT fp32 operands: every weight and
+ *                            activation as three bf16 planes (24 significant bits: the fp32 value
+ *                            itself), the six plane products of order <= 2 accumulated in fp32 on
+ *                            v_mfma_f32_16x16x32_bf16 (the dropped terms are <= 2^-24 of each
+ *                            product); the observation exact (one plane below 256, a residual plane
+ *                            where a value is larger, < 2^16); fp32 tanh to a few ulp
+ *                            (spl_policy32.hip, k_act32)
+ *   SPL_PREC_FP32_F16X2      fp32 within 2^-22: two fp16 planes per operand (22 significant bits,
+ *                            weights scaled per row by a power of two), three plane products on
+ *                            v_mfma_f32_16x16x32_f16, tanh with ~1e-7 absolute error (k_act32h): the
+ *                            round-4 form, faster, not an exact operand representation
  *   SPL_PREC_BF16 (opt-in)   bf16 MFMA (v_mfma_f32_32x32x16_bf16) with fp32 accumulation (spl_policy.hip)
  *
  *   spl_policy_bytes   size of a packed weight image (actor only, or actor + critic; per precision)
@@ -32,12 +39,15 @@
 extern "C" {
 #endif
 
-#define SPL_POLICY_ABI 4  /* 2: precision argument, args->image describes the image; 3: obs_u8;
+#define SPL_POLICY_ABI 5  /* 2: precision argument, args->image describes the image; 3: obs_u8;
                              4: fp32 images as two fp16 planes (spl_policy_bytes changed); each chunk also
-                                carries its rows' tanh factors (same size: pack and act from one library) */
+                                carries its rows' tanh factors (same size: pack and act from one library);
+                             5: SPL_PREC_FP32 is exact (three bf16 planes; spl_policy_bytes changed), the
+                                two-fp16-plane form is SPL_PREC_FP32_F16X2 */
 
 #define SPL_PREC_FP32 0
 #define SPL_PREC_BF16 1
+#define SPL_PREC_FP32_F16X2 2
 #define SPL_IMG_CRITIC 1 /* spl_act_args_t.image bit 0: the image holds the critic; bits 1-2: SPL_PREC_* */
 
 /* one nn.Sequential(Linear(297,256), Tanh, Linear(256,256), Tanh, Linear(256,out)):
@@ -69,7 +79,7 @@ typedef struct {
     int32_t image;       /* how the image was packed: SPL_IMG_CRITIC if with a critic | precision << 1;
                             packed_bytes must equal spl_policy_bytes(critic, precision)              */
     const uint8_t *obs_u8; /* [n][300] or NULL: the observation as spl_step's obs_u8 bytes, read
-                            instead of obs (fp32 images only); obs may then be NULL              */
+                            instead of obs (fp32 images of either format only); obs may then be NULL */
 } spl_act_args_t;
 
 /* bytes of a packed image: with_critic 0 = actor only (greedy opponents), 1 = actor + critic;
@@ -84,7 +94,8 @@ int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const sp
                    void *stream);
 
 /* Per-table networks (the opponent pool of ppo_splendor.py:137-143, 366-370: each episode plays the
- * current policy or one frozen snapshot): `images` holds n_images actor-only fp32 images, image i at
+ * current policy or one frozen snapshot): `images` holds n_images actor-only fp32 images (either fp32
+ * format, as args->image says), image i at
  * images + i * image_bytes; table t is evaluated with image group_of[t] (device [n]; tables with an
  * index outside 0..n_images-1 get no action).  Tables are counting-sorted by image into `scratch`
  * (spl_policy_group_scratch_bytes(n, n_images) bytes, caller-owned device memory, ZERO-FILLED before

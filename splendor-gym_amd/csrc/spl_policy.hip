@@ -472,17 +472,22 @@ __global__ __launch_bounds__(512) void k_act(const uint8_t *__restrict__ W, ActA
 
 using namespace splp;
 
-int64_t splp32_bytes(int with_critic);  // spl_policy32.hip: the fp32 image
-int splp32_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream);
+int64_t splp32_bytes(int with_critic, int fmt);  // spl_policy32.hip: the fp32 images (fmt 0 exact, 1 two fp16 planes)
+int splp32_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream, int fmt);
 int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, int32_t n, const spl_act_args_t *args,
-               void *stream, int groups = 0, int64_t image_stride = 0, const int32_t *group_of = nullptr,
+               void *stream, int fmt, int groups = 0, int64_t image_stride = 0, const int32_t *group_of = nullptr,
                void *scratch = nullptr);
 int64_t splp32_group_scratch(int32_t n, int32_t groups);
+
+// the fp32 precisions (spl_policy32.hip): the image format index, or -1
+static int fp32_fmt(int precision) {
+    return precision == SPL_PREC_FP32 ? 0 : precision == SPL_PREC_FP32_F16X2 ? 1 : -1;
+}
 
 extern "C" {
 
 int64_t spl_policy_bytes(int32_t with_critic, int32_t precision) {
-    if (precision == SPL_PREC_FP32) return splp32_bytes(with_critic ? 1 : 0);
+    if (fp32_fmt(precision) >= 0) return splp32_bytes(with_critic ? 1 : 0, fp32_fmt(precision));
     if (precision != SPL_PREC_BF16) return SPL_E_ARG;
     return with_critic ? (int64_t)kAllChunks * kChunk + kCriticTail : (int64_t)kActorChunks * kChunk;
 }
@@ -493,7 +498,7 @@ int spl_policy_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, int32_t pre
     if (critic && (!critic->w1 || !critic->b1 || !critic->w2 || !critic->b2 || !critic->w3 || !critic->b3))
         return spl_fail(SPL_E_ARG, "critic weights incomplete");
     if (!packed || ((uintptr_t)packed & 255u)) return spl_fail(SPL_E_ARG, "packed image must be 256-byte aligned");
-    if (precision == SPL_PREC_FP32) return splp32_pack(actor, critic, packed, stream);
+    if (fp32_fmt(precision) >= 0) return splp32_pack(actor, critic, packed, stream, fp32_fmt(precision));
     if (precision != SPL_PREC_BF16) return spl_fail(SPL_E_ARG, "unknown precision");
     const PackNet A{actor->w1, actor->b1, actor->w2, actor->b2, actor->w3, actor->b3, kAct};
     const PackNet C = critic ? PackNet{critic->w1, critic->b1, critic->w2, critic->b2, critic->w3, critic->b3, 1} : A;
@@ -509,7 +514,7 @@ int spl_policy_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, int32_t pre
 static int check_obs(const spl_act_args_t *args, int precision) {
     if (args->obs_u8) {
         if (args->obs) return spl_fail(SPL_E_ARG, "obs and obs_u8 are exclusive");
-        if (precision != SPL_PREC_FP32) return spl_fail(SPL_E_ARG, "obs_u8 is read by the fp32 kernels");
+        if (fp32_fmt(precision) < 0) return spl_fail(SPL_E_ARG, "obs_u8 is read by the fp32 kernels");
         if ((uintptr_t)args->obs_u8 & 3u) return spl_fail(SPL_E_ARG, "obs_u8 must be 4-byte aligned");
         return SPL_OK;
     }
@@ -522,7 +527,7 @@ int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const sp
     if (!packed || ((uintptr_t)packed & 255u)) return spl_fail(SPL_E_ARG, "packed image must be 256-byte aligned");
     const int precision = (args->image >> 1) & 3;
     const bool has_critic = (args->image & SPL_IMG_CRITIC) != 0;
-    if (precision != SPL_PREC_FP32 && precision != SPL_PREC_BF16) return spl_fail(SPL_E_ARG, "unknown precision");
+    if (fp32_fmt(precision) < 0 && precision != SPL_PREC_BF16) return spl_fail(SPL_E_ARG, "unknown precision");
     // the image is described by args->image, and its size must be exactly that image's: a full image
     // passed as actor-only (or the reverse) would evaluate the wrong chunks
     if (packed_bytes != spl_policy_bytes(has_critic ? 1 : 0, precision))
@@ -531,8 +536,8 @@ int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const sp
     if (int r = check_obs(args, precision)) return r;
     if (args->mode == SPL_ACT_VALUE) {  // ActorCritic.get_value (ppo_splendor.py:51): the critic alone
         if (!has_critic || !args->value) return spl_fail(SPL_E_ARG, "VALUE needs an image with a critic and a value output");
-        if (precision != SPL_PREC_FP32) return spl_fail(SPL_E_ARG, "VALUE is implemented for fp32 images");
-        return splp32_act(static_cast<const uint8_t *>(packed), true, true, false, n, args, stream);
+        if (fp32_fmt(precision) < 0) return spl_fail(SPL_E_ARG, "VALUE is implemented for fp32 images");
+        return splp32_act(static_cast<const uint8_t *>(packed), true, true, false, n, args, stream, fp32_fmt(precision));
     }
     if (!args->mask || ((uintptr_t)args->mask & 3u)) return spl_fail(SPL_E_ARG, "mask must be 4-byte aligned");
     if (!args->action) return spl_fail(SPL_E_ARG, "action output missing");
@@ -541,7 +546,8 @@ int spl_policy_act(const void *packed, int64_t packed_bytes, int32_t n, const sp
     const bool critic = sample && args->value;
     if (critic && !has_critic) return spl_fail(SPL_E_ARG, "value requested from an actor-only image");
     const uint8_t *img = static_cast<const uint8_t *>(packed);
-    if (precision == SPL_PREC_FP32) return splp32_act(img, has_critic, critic, sample, n, args, stream);
+    if (fp32_fmt(precision) >= 0)
+        return splp32_act(img, has_critic, critic, sample, n, args, stream, fp32_fmt(precision));
     const float *critic_out = has_critic ? reinterpret_cast<const float *>(img + (size_t)kAllChunks * kChunk) : nullptr;
     const ActArgs a{args->obs,   args->mask,       args->action,   args->logprob, args->entropy,
                     args->value, args->logits,     critic_out,     args->seed,    args->ply,
@@ -575,7 +581,7 @@ int spl_policy_act_grouped(const void *images, int64_t image_bytes, int32_t n_im
     if (((uintptr_t)scratch & 3u)) return spl_fail(SPL_E_ARG, "scratch must be 4-byte aligned");
     const int precision = (args->image >> 1) & 3;
     const bool has_critic = (args->image & SPL_IMG_CRITIC) != 0;
-    if (precision != SPL_PREC_FP32) return spl_fail(SPL_E_ARG, "grouped evaluation is implemented for fp32 images");
+    if (fp32_fmt(precision) < 0) return spl_fail(SPL_E_ARG, "grouped evaluation is implemented for fp32 images");
     if (has_critic) return spl_fail(SPL_E_ARG, "grouped evaluation serves actor-only images");
     if (image_bytes < spl_policy_bytes(0, precision)) return spl_fail(SPL_E_ARG, "image_bytes smaller than an image");
     if (n <= 0) return spl_fail(SPL_E_ARG, "n must be positive");
@@ -584,7 +590,7 @@ int spl_policy_act_grouped(const void *images, int64_t image_bytes, int32_t n_im
     if (args->mode != SPL_ACT_SAMPLE && args->mode != SPL_ACT_GREEDY) return spl_fail(SPL_E_ARG, "unknown mode");
     if (args->value) return spl_fail(SPL_E_ARG, "grouped evaluation has no critic");
     return splp32_act(static_cast<const uint8_t *>(images), false, false, args->mode == SPL_ACT_SAMPLE, n, args, stream,
-                      n_images, image_bytes, group_of, scratch);
+                      fp32_fmt(precision), n_images, image_bytes, group_of, scratch);
 }
 
 }  // extern "C"

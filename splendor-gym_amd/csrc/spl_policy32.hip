@@ -3,47 +3,42 @@
 // Same network and epilogue as spl_policy.hip's bf16 kernel (ppo_splendor.py:27-59: actor and
 // critic Linear(297,256)-Tanh-Linear(256,256)-Tanh-Linear(256,{45|1}); masked_categorical sample,
 // log_prob, entropy, critic value; or the greedy masked argmax of training_utils.py:263-276), with
-// fp32-accurate products on the 16-bit matrix cores (gfx950 has no xf32 MFMA, and its fp32 MFMA runs
-// at 1/16 of the fp16/bf16 rate):
-//   * every fp32 operand x is split into two fp16 planes x = x0 + x1 (x0 = fp16(x), x1 = fp16(x - x0):
-//     22 significant bits, x represented to 2^-22 relative; the residual is exact in fp32).  fp16's
-//     exponent range is narrow, so the weights are scaled per output row by a power of two (the row's
-//     largest |w| into [512, 1024)) and hidden activations (|tanh| < 1) by 2^10: every plane is a
-//     normal fp16.  A weight-times-activation product is the three plane products of order <= 1,
-//     a1 w0 + a0 w1 + a0 w0, accumulated in fp32 by v_mfma_f32_16x16x32_f16 (fp16 x fp16 products
-//     are exact in fp32); the dropped a1 w1 is <= 2^-22 of |aw|.  Smallest terms first; the row's sum
-//     comes back through the exact factor 2^-(row exponent + activation exponent).  Layer 1's operand,
-//     the observation, is integers < 2048, exact in fp16: two products (a w1 + a w0).
-//     Round 3 used three bf16 planes and six products (SPL_P32_F16=0 builds it): 1.8x the MFMAs and
-//     1.5x the weight bytes streamed for the same network (k_act32<true, true> 184 -> 140 us at 65 536
-//     tables, profiles/r04).
+// fp32 operands carried exactly into the 16-bit matrix cores (gfx950 has no xf32 MFMA, and its fp32
+// MFMA runs at 1/16 of the fp16/bf16 rate).  Two operand formats, each its own kernels in this file:
+//   * SPL_PREC_FP32 — EXACT fp32 operands (FmtBf16x3; round 3's split, the default since round 5,
+//     VERDICT r04 item 2): every fp32 operand x is three bf16 planes x = x0 + x1 + x2 (x0 = bf16(x),
+//     x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)): 24 significant bits, so the planes hold x EXACTLY (bf16
+//     has fp32's exponent range: no scaling).  A hidden-layer product a*w is the six plane products of
+//     order <= 2 (a2w0 + a1w1 + a0w2 + a1w0 + a0w1 + a0w0, smallest first) on v_mfma_f32_16x16x32_bf16,
+//     each bf16 x bf16 product exact in fp32; the dropped a1w2 + a2w1 + a2w2 are <= 2^-24 of |aw| each,
+//     below fp32's own rounding of the sum.  Layer 1's operand, the observation, is integers: exact in
+//     ONE bf16 plane below 256 (every observation value the engine writes except a move count above
+//     255); where a wave holds a larger value (< 2^16) its residual plane adds two products to that
+//     k-step (ObsHi).  tanh in fp32 to <= ~2 ulp everywhere (tanh_acc).
+//   * SPL_PREC_FP32_F16X2 — fp32 within 2^-22 (FmtF16x2; round 4): every fp32 operand is two fp16
+//     planes x = x0 + x1 (22 significant bits; weights scaled per output row by a power of two so the
+//     row's largest |w| lands in [512, 1024) and every plane stays a normal fp16, hidden activations
+//     scaled by 2^10); three plane products (a1w0 + a0w1 + a0w0, the dropped a1w1 <= 2^-22 |aw|) on
+//     v_mfma_f32_16x16x32_f16; the observation (< 2048, exact in fp16) takes two.  tanh from exp
+//     (tanh_fold: absolute error ~1e-7, relative error grows near 0).  Fewer products, so faster; not an
+//     exact representation, and labelled so (bench.py).
 //   * a wave = 16 tables = the 16 columns of every 16x16x32 tile; a workgroup = 8 waves = 128 tables
 //     (two waves per SIMD).  Activations are TRANSPOSED (hidden unit on the accumulator row, table
 //     on the lane): accumulator register i of lane group g holds unit 16t + 4g + i of tile t, and
 //     tiles 2s, 2s+1 are lane group g's B elements of k-step s of the next layer (element e = unit
 //     16(2s + e/4) + 4g + e%4) — no LDS round trip between layers; the packed weights carry the
-//     matching input-unit order.  tanh runs in fp32 (tanh_f32) before the split.
-//   * the observation (int32 -> fp16, exact) loads into registers as the 10 layer-1 B fragments
-//     and stays there through both networks' layer 1; a hidden layer's output is 2 planes x 8
-//     k-steps x 8 fp16 per lane.
-//   * weights stream once per workgroup through a 5-slot LDS ring (21-KB chunks = one 16-row
-//     output tile of one layer, [k-step][plane][lane][8 fp16] + scaled biases + row factors,
-//     global_load_lds, 4 chunks in flight), shared by the 8 waves.
+//     matching input-unit order.  tanh runs in fp32 before the split.
+//   * the observation loads into registers as the 10 layer-1 B fragments and stays there through both
+//     networks' layer 1; a hidden layer's output is kPlanes planes x 8 k-steps x 8 elements per lane.
+//   * weights stream once per workgroup through an LDS ring of chunks (one chunk = one 16-row output
+//     tile of one layer, [k-step][plane][lane][8 elements] + biases + row factors; 31 KB for three
+//     bf16 planes in 4 slots, 21 KB for two fp16 planes in 5), global_load_lds, shared by the 8 waves.
 //   * the critic's one-unit output layer is a per-lane fp32 FMA chain over its layer-2 tiles.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <string>
 
-#ifndef SPL_AF_AHEAD
-#define SPL_AF_AHEAD 2
-#endif
-#ifndef SPL_TANH_LIBM
-#define SPL_TANH_LIBM 0
-#endif
-#ifndef SPL_TANH_EXP
-#define SPL_TANH_EXP 1
-#endif
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
 // streaming, no per-tile barrier), 4 A fragments loaded once per tile (no per-group LDS reads)
 #ifndef SPL_POL_ABL
@@ -61,59 +56,62 @@ namespace splp32 {
 using spl::philox4x32;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-// Operand planes (round 4).  SPL_P32_F16 = 1 (default): every fp32 operand is two fp16 planes
-// x = x0 + x1 (x0 = fp16(x), x1 = fp16(x - x0): 22 significant bits, |x - x0 - x1| <= 2^-22 |x|) —
-// weights scaled per output row by a power of two so the row's largest |w| lands in [512, 1024) and
-// every plane stays a normal fp16, hidden activations (|tanh| < 1) scaled by 2^10; a hidden-layer
-// product is the three plane products a1 w0 + a0 w1 + a0 w0 on v_mfma_f32_16x16x32_f16 (the dropped
-// a1 w1 is <= 2^-22 |aw|), the observation (integers < 2048, exact in fp16) takes two; the scaled sum
-// is brought back by the exact power-of-two row factor.  0: three bf16 planes, six products (round 3).
-#ifndef SPL_P32_F16
-#define SPL_P32_F16 1
-#endif
-#if SPL_P32_F16
-typedef _Float16 pel;
-constexpr int kPlanes = 2;       // fp16 planes of a split fp32 operand
-constexpr int kActScaleExp = 10; // hidden activations enter the next layer as tanh * 2^10
-constexpr int kRowMaxExp = 10;   // a weight row's largest |w| is scaled into [2^9, 2^10)
-#else
-typedef __bf16 pel;
-constexpr int kPlanes = 3;       // bf16 planes of a split fp32 operand
-constexpr int kActScaleExp = 0;
-constexpr int kRowMaxExp = 0;    // bf16 has fp32's exponent range: no scaling
-#endif
+// ---- the two operand formats ------------------------------------------------------------------
+struct FmtBf16x3 {  // SPL_PREC_FP32: exact (24 significant bits in three bf16 planes)
+    typedef __bf16 pel;
+    typedef bf16x8 pelx8;
+    typedef bf16x2 pelx2;
+    static constexpr int kPlanes = 3;
+    static constexpr int kActScaleExp = 0;  // bf16 has fp32's exponent range: no scaling anywhere
+    static constexpr int kRowMaxExp = 0;
+    static constexpr int kSlots = 4;        // ring slots of 31 KB (3 chunks in flight)
+    static constexpr bool kExact = true;
+};
+struct FmtF16x2 {   // SPL_PREC_FP32_F16X2: 22 significant bits in two fp16 planes
+    typedef _Float16 pel;
+    typedef f16x8 pelx8;
+    typedef f16x2 pelx2;
+    static constexpr int kPlanes = 2;
+    static constexpr int kActScaleExp = 10;  // hidden activations enter the next layer as tanh * 2^10
+    static constexpr int kRowMaxExp = 10;    // a weight row's largest |w| is scaled into [2^9, 2^10)
+    static constexpr int kSlots = 5;         // ring slots of 21 KB (4 chunks in flight)
+    static constexpr bool kExact = false;
+};
+
 constexpr float kTwoLog2e = 2.8853900817779268f;  // 2 log2(e): exp(2|x|) = exp2(2 log2(e) |x|)
-typedef pel pelx8 __attribute__((ext_vector_type(8)));
-typedef pel pelx2 __attribute__((ext_vector_type(2)));
-
 constexpr int kObs = 297, kAct = 45, kHid = 256;
 constexpr int kKs1 = 10;    // layer-1 k-steps of 32: 297 inputs padded to 320
 constexpr int kKs2 = 8;     // layers 2 and 3: 256 inputs
 constexpr int kFrag = 1024;                       // one plane of one k-step: [lane][8 elements]
-constexpr int kBiasOff = kKs1 * kPlanes * kFrag;  // after the largest weight block
-constexpr int kChunk = kBiasOff + 1024;           // + the tile's 16 (scaled) fp32 biases and 16 row factors
 constexpr int kTiles = kHid / 16;                 // 16 output tiles of 16 rows per hidden layer
 constexpr int kActTiles = 3;                      // 48 rows >= 45 logits
 constexpr int kActorChunks = 2 * kTiles + kActTiles, kCriticChunks = 2 * kTiles;  // 35, 32
 constexpr int kAllChunks = kActorChunks + kCriticChunks;                          // 67
 constexpr int kCriticTail = 272 * 4;  // fp32 critic output layer: w3 [256], b3, padding
-
-#ifndef SPL_P32_WAVES
-#define SPL_P32_WAVES 8  // waves per k_act32 workgroup (16 tables each)
-#endif
-#ifndef SPL_P32_RING
-#define SPL_P32_RING (SPL_P32_F16 ? 5 : 4)  // ring slots (SPL_P32_RING - 1 chunks in flight)
-#endif
-constexpr int kWaves = SPL_P32_WAVES, kRowsPerWave = 16, kRowsPerBlock = kWaves * kRowsPerWave;  // 128 tables
-constexpr int kSlots = SPL_P32_RING;
+constexpr int kWaves = 8, kRowsPerWave = 16, kRowsPerBlock = kWaves * kRowsPerWave;  // 128 tables
 constexpr int kMaskWave = kRowsPerWave * kAct;  // 720 B
 constexpr int kLogitRow = 49;                   // floats per staged logit row (odd: conflict-free)
-constexpr int kLdsMask = kSlots * kChunk;
-constexpr int kLds = kLdsMask + kWaves * kMaskWave;  // 132 736 B
-static_assert(kWaves * kRowsPerWave * kLogitRow * 4 <= kLdsMask, "logits reuse the weight ring");
-static_assert(kLds <= 160 * 1024, "LDS");
-static_assert(kBiasOff + 192 <= kChunk, "bias + row factors + tanh factors");
+
+// sizes that follow from the format
+template <class F>
+struct Geo {
+    static constexpr int kBiasOff = kKs1 * F::kPlanes * kFrag;  // after the largest weight block
+    static constexpr int kChunk = kBiasOff + 1024;              // + 16 biases, 16 row factors, 16 tanh factors
+    static constexpr int kLdsMask = F::kSlots * kChunk;
+    static constexpr int kLds = kLdsMask + kWaves * kMaskWave;
+    static constexpr int kChunkBlocks = kChunk / 1024;                           // 31 / 21
+    static constexpr int kBlocksPerWave = (kChunkBlocks + kWaves - 1) / kWaves;  // 4 / 3
+    // a wave's loads of the chunks after chunk c that may stay in flight when it enters chunk c
+    static constexpr int kWaitMost = (F::kSlots - 2) * kBlocksPerWave, kWaitLast = (F::kSlots - 2) * (kBlocksPerWave - 1);
+    static_assert(kWaves * kRowsPerWave * kLogitRow * 4 <= kLdsMask, "logits reuse the weight ring");
+    static_assert(kLds <= 160 * 1024, "LDS");
+    static_assert(kWaitMost <= 63, "vmcnt range");
+};
 
 // chunk order of an image (the order a forward pass consumes them): with a critic
 // [critic L1 x16][critic L2 x16], then [actor L1 x16][actor L2 x16][actor L3 x3]; the actor part of
@@ -131,18 +129,23 @@ __device__ __forceinline__ int unit_of(int layer, int s, int g, int e) {
 }
 
 // x = x0 + x1 (+ x2) in the plane format (round to nearest even; the residuals are exact in fp32)
-__device__ __forceinline__ void split_planes(float x, pel (&q)[kPlanes]) {
+template <class F>
+__device__ __forceinline__ void split_planes(float x, typename F::pel (&q)[F::kPlanes]) {
+    typedef typename F::pel pel;
     q[0] = (pel)x;
     const float r = x - (float)q[0];
     q[1] = (pel)r;
-    if constexpr (kPlanes == 3) q[2] = (pel)(r - (float)q[1]);
+    if constexpr (F::kPlanes == 3) q[2] = (pel)(r - (float)q[1]);
 }
 
 // one block per physical chunk: [k-step s][plane p][lane][8 elements], lane l = (g = l >> 4, r = l & 15)
 // holds W[row 16*tile + r][unit_of(layer, s, g, e)] * 2^e_row split into the planes; then the 16 rows'
-// biases scaled as the products are (2^(e_row + layer's activation exponent)) and the 16 exact
-// factors 2^-(e_row + activation exponent) that bring a row's sum back
-__global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, int with_critic, uint8_t *dst) {
+// biases scaled as the products are (2^(e_row + layer's activation exponent)), the 16 exact factors
+// 2^-(e_row + activation exponent) that bring a row's sum back, and the 16 tanh factors (tanh_fold)
+template <class F>
+__device__ __forceinline__ void pack_chunk(PackNet actor, PackNet critic, int with_critic, uint8_t *dst) {
+    typedef typename F::pel pel;
+    constexpr int kChunk = Geo<F>::kChunk, kBiasOff = Geo<F>::kBiasOff;
     const int ch = blockIdx.x;
     const int net = with_critic && ch < kCriticChunks ? 1 : 0;  // 0 actor, 1 critic
     const int local = ch - (with_critic && !net ? kCriticChunks : 0);
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, i
             for (int j = 0; j < 16; ++j) mx = fmaxf(mx, part[threadIdx.x][j]);
             int x = 0;
             (void)frexpf(mx, &x);  // mx = f * 2^x, f in [0.5, 1)
-            rexp[threadIdx.x] = (kRowMaxExp == 0 || mx == 0.f) ? 0 : max(-40, min(60, kRowMaxExp - x));
+            rexp[threadIdx.x] = (F::kRowMaxExp == 0 || mx == 0.f) ? 0 : max(-40, min(60, F::kRowMaxExp - x));
         }
         __syncthreads();
     }
@@ -178,16 +181,16 @@ __global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, i
         const int e = v & 7, lane = (v >> 3) & 63, s = v >> 9;
         const int r = lane & 15, g = lane >> 4, row = 16 * tile + r, k = unit_of(layer, s, g, e);
         const float w = (row < rows && k < in) ? ldexpf(W[(size_t)row * in + k], rexp[r]) : 0.f;
-        pel q[kPlanes];
-        split_planes(w, q);
-        const size_t base = ((size_t)(s * kPlanes) * 64 + lane) * 8 + e;
+        pel q[F::kPlanes];
+        split_planes<F>(w, q);
+        const size_t base = ((size_t)(s * F::kPlanes) * 64 + lane) * 8 + e;
 #pragma unroll
-        for (int p = 0; p < kPlanes; ++p) o[base + (size_t)p * 64 * 8] = q[p];
+        for (int p = 0; p < F::kPlanes; ++p) o[base + (size_t)p * 64 * 8] = q[p];
     }
-    for (int v = ks * kPlanes * kFrag + 4 * threadIdx.x; v < kBiasOff; v += 4 * blockDim.x)
+    for (int v = ks * F::kPlanes * kFrag + 4 * threadIdx.x; v < kBiasOff; v += 4 * blockDim.x)
         *reinterpret_cast<uint32_t *>(out + v) = 0u;
     float *bias = reinterpret_cast<float *>(out + kBiasOff);
-    const int act_exp = layer == 1 ? 0 : kActScaleExp;  // layer 1 reads the observation unscaled
+    const int act_exp = layer == 1 ? 0 : F::kActScaleExp;  // layer 1 reads the observation unscaled
     if (threadIdx.x < 16) {  // scaled biases in row order, the row factors, the tanh factors, zero padding
         const int row = 16 * tile + threadIdx.x, ex = rexp[threadIdx.x] + act_exp;
         bias[threadIdx.x] = row < rows ? ldexpf(B[row], ex) : 0.f;
@@ -202,6 +205,12 @@ __global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, i
         float *tail = reinterpret_cast<float *>(dst + (size_t)kAllChunks * kChunk);
         for (int k = threadIdx.x; k < 272; k += blockDim.x) tail[k] = k < kHid ? P.w3[k] : k == kHid ? P.b3[0] : 0.f;
     }
+}
+__global__ __launch_bounds__(256) void k_pack32(PackNet actor, PackNet critic, int with_critic, uint8_t *dst) {
+    pack_chunk<FmtBf16x3>(actor, critic, with_critic, dst);
+}
+__global__ __launch_bounds__(256) void k_pack32h(PackNet actor, PackNet critic, int with_critic, uint8_t *dst) {
+    pack_chunk<FmtF16x2>(actor, critic, with_critic, dst);
 }
 
 struct ActArgs {
@@ -223,24 +232,15 @@ struct ActArgs {
     int64_t image_stride;
 };
 
-// tanh in fp32 without branches.  Default (round 4, SPL_TANH_EXP=1): 1 - 2 / (exp(2|x|) + 1) alone,
-// six VALU ops (two transcendental): its error is ABSOLUTE, ~1e-7 over the whole range (a few ulp of
-// 1 from v_exp_f32 / v_rcp_f32), relative only near 0, where the next layer multiplies the unit by
-// weights of ~1e-1 anyway; tanh was ~17 % of the kernel (SPL_POL_ABL=1 ablation, profiles/r04).
-// SPL_TANH_EXP=0 is round 3's accurate form (SPL_TANH_LIBM=1 restores libm tanhf).  |x| < 0.625:
+// tanh in fp32 without branches, to a few ulp everywhere (the exact format's): |x| < 0.625:
 // x + x^3 P(x^2), a degree-4 fit in x^2 (<= 0.9 ulp in fp32 Horner, checked over [0, 0.625]);
-// otherwise 1 - 2 / (exp(2|x|) + 1) on v_exp_f32 / v_rcp_f32 (~1.5 ulp with correctly rounded
-// exp2 and rcp, a few ulp on the hardware's).  Both halves are evaluated and selected, so a
-// tile's 64 lanes never diverge and the VALU work stays in one block the scheduler can place
-// beside the next tile's MFMAs; libm tanhf is about twice the instructions and branches.
-__device__ __forceinline__ float tanh_f32(float x) {
+// otherwise 1 - 2 / (exp(2|x|) + 1) on v_exp_f32 / v_rcp_f32 (~1.5 ulp with correctly rounded exp2
+// and rcp, a few ulp on the hardware's).  Both halves are evaluated and selected, so a tile's 64
+// lanes never diverge.  (The exp form alone cancels near 0: its error is absolute, ~1e-7, so the
+// relative error grows as |x| shrinks — ADVICE r04; the fp16-plane format keeps it, labelled.)
+__device__ __forceinline__ float tanh_acc(float x) {
 #if SPL_POL_ABL & 1
     return x;
-#elif SPL_TANH_LIBM
-    return tanhf(x);
-#elif SPL_TANH_EXP
-    const float e = __builtin_amdgcn_exp2f(__builtin_fabsf(x) * kTwoLog2e);  // exp(2|x|)
-    return __builtin_copysignf(__builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f), x);
 #else
     const float ax = __builtin_fabsf(x);
     const float z = ax * ax;
@@ -256,15 +256,18 @@ __device__ __forceinline__ float tanh_f32(float x) {
 #endif
 }
 
-// tanh with the tile's row factor and the next layer's activation scale folded in (SPL_TANH_EXP):
-// 2^S tanh(x u) for c = 2 log2(e) u, bitwise the same as tanh_f32(x * u) * 2^S (u and 2^S powers of
-// two; |x| c and |x u| 2 log2(e) are the same real product, rounded once) and two VALU ops fewer
-// per output (the unscale and the activation-scale multiplies)
-constexpr bool kFoldTanh = SPL_TANH_EXP && !(SPL_POL_ABL & 1) && !SPL_TANH_LIBM;
+// the fp16-plane format's tanh, with the tile's row factor and the next layer's activation scale
+// folded in: 2^S tanh(x u) for c = 2 log2(e) u, as 2^S (1 - 2 / (exp(2|x u|) + 1)) (u and 2^S powers of
+// two; |x| c and |x u| 2 log2(e) are the same real product, rounded once): six VALU ops, two of them
+// transcendental; absolute error ~1e-7
 template <int S>
 __device__ __forceinline__ float tanh_fold(float x, float c) {
+#if SPL_POL_ABL & 1
+    return x * (float)(1 << S);
+#else
     const float e = __builtin_amdgcn_exp2f(__builtin_fabsf(x) * c);
     return __builtin_copysignf(__builtin_fmaf(-(float)(2 << S), __builtin_amdgcn_rcpf(e + 1.0f), (float)(1 << S)), x);
+#endif
 }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -275,19 +278,20 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int kChunkBlocks = kChunk / 1024;  // 31: blocks w, w + 8, w + 16, w + 24 of wave w
-constexpr int kBlocksPerWave = (kChunkBlocks + kWaves - 1) / kWaves;  // 4 (3 for the last wave)
 // the image as a buffer resource: the chunk and block offsets go in the scalar offset, the lane's
 // 16 bytes in a constant VGPR, so an LDS-DMA issue costs no VALU (the 64-bit per-lane address of
 // global_load_lds took a v_lshl_add_u64 per load)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t image_rsrc(const uint8_t *W) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(W), (short)0, 0x7FFFFFF0, 0x00020000);
 }
+// wave w's share of a chunk: 1-KB blocks w, w + 8, w + 16, ... (64 lanes x 16 B each)
+template <class F>
 __device__ __forceinline__ void issue_chunk(__amdgpu_buffer_rsrc_t rs, int chunk, uint8_t *slot, int wave, int lane) {
+    constexpr int kChunk = Geo<F>::kChunk, kBlocks = Geo<F>::kChunkBlocks;
 #pragma unroll
-    for (int i = 0; i < kBlocksPerWave; ++i) {
+    for (int i = 0; i < Geo<F>::kBlocksPerWave; ++i) {
         const int blk = wave + kWaves * i;
-        if (blk < kChunkBlocks)
+        if (blk < kBlocks)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)(slot + blk * 1024), 16, lane * 16,
                                                      chunk * kChunk + blk * 1024, 0, 0);
     }
@@ -295,35 +299,77 @@ __device__ __forceinline__ void issue_chunk(__amdgpu_buffer_rsrc_t rs, int chunk
 
 // s_waitcnt immediate for vmcnt(n) alone (gfx9: vmcnt[3:0] in bits 3:0, vmcnt[5:4] in 15:14)
 constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
-// a wave's loads of the chunks after chunk c that may stay in flight when it enters chunk c
-constexpr int kWaitMost = (kSlots - 2) * kBlocksPerWave, kWaitLast = (kSlots - 2) * (kBlocksPerWave - 1);
 
-__device__ __forceinline__ f32x4 mma(const pelx8 &a, const pelx8 &b, const f32x4 &c) {
+template <class F>
+__device__ __forceinline__ f32x4 mma(const typename F::pelx8 &a, const typename F::pelx8 &b, const f32x4 &c) {
 #if SPL_POL_ABL & 8
     return c + (float)a[0] * (float)b[1];
-#elif SPL_P32_F16
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 #else
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    if constexpr (F::kExact) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 #endif
+}
+
+// The observation's residual plane for the exact format (observation values >= 256 are not exact in
+// one bf16 plane): `mask` bit s is set when any table of the wave has such a value in k-step s
+// (wave-uniform), and that k-step then adds the two products (w1 + w0) x the residual, rebuilt from
+// the row (a rare path: the engine writes values >= 256 only for move counts above 255)
+struct ObsHi {
+    uint32_t mask;
+    const int32_t *row32;
+    const uint8_t *row8;
+};
+
+// one observation value k of a row (int32 row, or a compact row: byte k, move_count's high byte at 297)
+__device__ __forceinline__ int obs_value(const int32_t *row32, const uint8_t *row8, int k) {
+    if (k >= kObs) return 0;
+    if (row32) return row32[k];
+    int v = row8[k];
+    if (k == 295) v += 256 * (int)row8[297];
+    return v;
+}
+
+// the residual plane x - bf16(x) of k-step s, lane group g (exact for |x| < 2^16)
+__device__ __forceinline__ bf16x8 obs_residual(const ObsHi &h, int s, int g) {
+    bf16x8 q;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float x = (float)obs_value(h.row32, h.row8, 32 * s + 8 * g + e);
+        q[e] = (__bf16)(x - (float)(__bf16)x);
+    }
+    return q;
 }
 
 // one 16-row output tile: bias + sum over KS k-steps of 32 inputs, returned at the true scale (the
 // row factors undo the planes' scaling).  B: NB planes of the layer's input (1: the observation,
-// exact in one plane; kPlanes: a split hidden layer), in registers.  A: the tile's weight planes per
-// k-step from `src` (the LDS ring slot, or the image in global memory for the narrow kernel), D
-// k-steps ahead of the MFMAs that use them.
+// exact in one plane but for ObsHi's residual; kPlanes: a split hidden layer), in registers.  A: the
+// tile's weight planes per k-step from `src` (the LDS ring slot, or the image in global memory for the
+// narrow kernel), D k-steps ahead of the MFMAs that use them.
 // kFold: the sum is returned as the products left it (scaled by the row factor's inverse) and
 // `fold` gets the tile's tanh factors (tanh_fold) instead.
-template <int KS, int NB, int D, bool kFold = false>
-__device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const pelx8 (&B)[NB][KS], int lane,
-                                          f32x4 *fold = nullptr) {
+template <class F, int KS, int NB, int D, bool kFold = false>
+__device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const typename F::pelx8 (&B)[NB][KS], int lane,
+                                          f32x4 *fold = nullptr, const ObsHi *hi = nullptr) {
+    typedef typename F::pelx8 pelx8;
+    constexpr int kPlanes = F::kPlanes;
     static_assert(NB == 1 || NB == kPlanes, "planes");
-    const float *bias = reinterpret_cast<const float *>(src + kBiasOff) + 4 * (lane >> 4);
+    const float *bias = reinterpret_cast<const float *>(src + Geo<F>::kBiasOff) + 4 * (lane >> 4);
     f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
     const f32x4 unscale = {bias[16], bias[17], bias[18], bias[19]};
     if constexpr (kFold) *fold = f32x4{bias[32], bias[33], bias[34], bias[35]};
     const pelx8 *A = reinterpret_cast<const pelx8 *>(src) + lane;  // k-step s, plane p at A[(kPlanes s + p) * 64]
+    if constexpr (NB == 1 && F::kExact) {
+        // the observation's residual plane (rare, wave-uniform): x1 w1 + x1 w0 of each flagged k-step
+        // first (the smaller terms), then the main products below
+        if (hi && hi->mask) {
+            for (uint32_t m = hi->mask; m; m &= m - 1) {
+                const int s = __builtin_ctz(m);
+                const bf16x8 x1 = obs_residual(*hi, s, lane >> 4);
+                acc = mma<F>(A[(kPlanes * s + 1) * 64], x1, acc);
+                acc = mma<F>(A[(kPlanes * s + 0) * 64], x1, acc);
+            }
+        }
+    }
     constexpr int NR = D + 1;
     pelx8 af[NR][kPlanes];
 #pragma unroll
@@ -339,121 +385,129 @@ __device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const pelx8 (&B)[N
         const pelx8 *a = af[(SPL_POL_ABL & 4) ? s % D : s % NR];
         if constexpr (NB == 1) {  // exact B: (a2 b +) a1 b + a0 b
 #pragma unroll
-            for (int p = kPlanes - 1; p >= 0; --p) acc = mma(a[p], B[0][s], acc);
+            for (int p = kPlanes - 1; p >= 0; --p) acc = mma<F>(a[p], B[0][s], acc);
         } else if constexpr (kPlanes == 2) {  // the three products of order <= 1, smallest first
-            acc = mma(a[1], B[0][s], acc);
-            acc = mma(a[0], B[1][s], acc);
-            acc = mma(a[0], B[0][s], acc);
+            acc = mma<F>(a[1], B[0][s], acc);
+            acc = mma<F>(a[0], B[1][s], acc);
+            acc = mma<F>(a[0], B[0][s], acc);
         } else {  // the six products of order <= 2, smallest first
-            acc = mma(a[2], B[0][s], acc);
-            acc = mma(a[1], B[1][s], acc);
-            acc = mma(a[0], B[2][s], acc);
-            acc = mma(a[1], B[0][s], acc);
-            acc = mma(a[0], B[1][s], acc);
-            acc = mma(a[0], B[0][s], acc);
+            acc = mma<F>(a[2], B[0][s], acc);
+            acc = mma<F>(a[1], B[1][s], acc);
+            acc = mma<F>(a[0], B[2][s], acc);
+            acc = mma<F>(a[1], B[0][s], acc);
+            acc = mma<F>(a[0], B[1][s], acc);
+            acc = mma<F>(a[0], B[0][s], acc);
         }
         if (NB > 1 || (s & 1) == 1) __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (kRowMaxExp != 0 && !kFold) acc *= unscale;  // exact: powers of two
+    if constexpr (F::kRowMaxExp != 0 && !kFold) acc *= unscale;  // exact: powers of two
     return acc;
 }
 
 // planes of a pelx8 as dwords: element e in dword e / 2 (even e in the low half)
-__device__ __forceinline__ uint32_t pk2(pel lo, pel hi) {
-    const pelx2 v = {lo, hi};
+template <class F>
+__device__ __forceinline__ uint32_t pk2(typename F::pel lo, typename F::pel hi) {
+    const typename F::pelx2 v = {lo, hi};
     return __builtin_bit_cast(uint32_t, v);
 }
 
 // the four fp32 outputs h[0..3] of tile t (units 16t + 4g + i), scaled by 2^kActScaleExp (exact) ->
 // elements 4(t & 1) .. +3 of k-step t / 2 of the next layer's B planes
-template <bool kScaled = false>  // kScaled: h already carries 2^kActScaleExp (tanh_fold)
-__device__ __forceinline__ void put_split(pelx8 (&H)[kPlanes][kKs2], int t, const float (&h)[4]) {
-    pel x[4][kPlanes];
+template <class F, bool kScaled = false>  // kScaled: h already carries 2^kActScaleExp (tanh_fold)
+__device__ __forceinline__ void put_split(typename F::pelx8 (&H)[F::kPlanes][kKs2], int t, const float (&h)[4]) {
+    typedef typename F::pel pel;
+    typedef typename F::pelx8 pelx8;
+    pel x[4][F::kPlanes];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        split_planes((kActScaleExp && !kScaled) ? h[i] * (float)(1 << kActScaleExp) : h[i], x[i]);
+        split_planes<F>((F::kActScaleExp && !kScaled) ? h[i] * (float)(1 << F::kActScaleExp) : h[i], x[i]);
 #pragma unroll
-    for (int p = 0; p < kPlanes; ++p) {
+    for (int p = 0; p < F::kPlanes; ++p) {
         u32x4 w = __builtin_bit_cast(u32x4, H[p][t >> 1]);
-        w[2 * (t & 1)] = pk2(x[0][p], x[1][p]);
-        w[2 * (t & 1) + 1] = pk2(x[2][p], x[3][p]);
+        w[2 * (t & 1)] = pk2<F>(x[0][p], x[1][p]);
+        w[2 * (t & 1) + 1] = pk2<F>(x[2][p], x[3][p]);
         H[p][t >> 1] = __builtin_bit_cast(pelx8, w);
     }
 }
 
+// a tile's four pre-activations -> tanh (the format's), scaled for the next layer
+template <class F, int KS, int NB, int D, typename Enter>
+__device__ __forceinline__ void tile_tanh(Enter &enter, const typename F::pelx8 (&B)[NB][KS], int lane, float (&h)[4],
+                                          const ObsHi *hi) {
+    if constexpr (F::kExact) {
+        const f32x4 acc = tile_mma<F, KS, NB, D>(enter(), B, lane, nullptr, hi);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[i] = tanh_acc(acc[i]);
+    } else {
+        f32x4 c;
+        const f32x4 acc = tile_mma<F, KS, NB, D, true>(enter(), B, lane, &c);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) h[i] = tanh_fold<F::kActScaleExp>(acc[i], c[i]);
+    }
+}
+
 // a hidden layer: 16 tiles, each tile's tanh split into the next layer's B planes
-template <int KS, int NB, int D, typename Enter>
-__device__ __forceinline__ void layer_tanh(Enter &enter, const pelx8 (&B)[NB][KS], pelx8 (&H)[kPlanes][kKs2],
-                                           int lane) {
+template <class F, int KS, int NB, int D, typename Enter>
+__device__ __forceinline__ void layer_tanh(Enter &enter, const typename F::pelx8 (&B)[NB][KS],
+                                           typename F::pelx8 (&H)[F::kPlanes][kKs2], int lane, const ObsHi *hi) {
 #pragma unroll
     for (int t = 0; t < kTiles; ++t) {
         float h[4];
-        if constexpr (kFoldTanh) {
-            f32x4 c;
-            const f32x4 acc = tile_mma<KS, NB, D, true>(enter(), B, lane, &c);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) h[i] = tanh_fold<kActScaleExp>(acc[i], c[i]);
-            put_split<true>(H, t, h);
-        } else {
-            const f32x4 acc = tile_mma<KS, NB, D>(enter(), B, lane);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) h[i] = tanh_f32(acc[i]);
-            put_split(H, t, h);
-        }
+        tile_tanh<F, KS, NB, D>(enter, B, lane, h, hi);
+        put_split<F, true>(H, t, h);
     }
 }
 
-// the same B fragments from a compact row (spl_step_args_t.obs_u8: 300 bytes, move_count >> 8 at
-// byte 297): 8 bytes per k-step as two dword loads, k = 296 alone, k >= 297 zero
-__device__ __forceinline__ void load_obs_u8(const uint8_t *xrow, int g, pelx8 (&X)[1][kKs1]) {
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(xrow);
+// the observation's B fragments: lane (r, g), k-step s, element e = obs[table r][32s + 8g + e] from an
+// int32 row, or from a compact row (spl_step_args_t.obs_u8: 300 bytes, move_count >> 8 at byte 297:
+// 8 bytes per k-step as two dword loads, k = 296 alone, k >= 297 zero).  The exact format also returns
+// which k-steps hold a value the bf16 plane does not represent exactly (ObsHi.mask, wave-uniform).
+template <class F>
+__device__ __forceinline__ uint32_t load_obs(const int32_t *row32, const uint8_t *row8, int g,
+                                             typename F::pelx8 (&X)[1][kKs1]) {
+    typedef typename F::pel pel;
+    typedef typename F::pelx8 pelx8;
+    uint32_t hi = 0u;
 #pragma unroll
     for (int s = 0; s < kKs1; ++s) {
         const int k0 = 32 * s + 8 * g;
-        uint32_t lo = 0u, hi = 0u;
-        if (k0 + 7 < kObs) {
-            lo = w[k0 >> 2];
-            hi = w[(k0 >> 2) + 1];
-        } else if (k0 < kObs) {  // k0 = 296 (s = 9, g = 1): byte 296 only
-            lo = w[k0 >> 2] & 0xFFu;
-        }
         int v[8];
+        if (row32) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            v[e] = (int)((lo >> (8 * e)) & 0xFFu);
-            v[4 + e] = (int)((hi >> (8 * e)) & 0xFFu);
+            for (int e = 0; e < 8; ++e) {
+                const int k = k0 + e;
+                v[e] = k < kObs ? row32[k < kObs ? k : 0] : 0;
+            }
+        } else {
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(row8);
+            uint32_t lo = 0u, hw = 0u;
+            if (k0 + 7 < kObs) {
+                lo = w[k0 >> 2];
+                hw = w[(k0 >> 2) + 1];
+            } else if (k0 < kObs) {  // k0 = 296 (s = 9, g = 1): byte 296 only
+                lo = w[k0 >> 2] & 0xFFu;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[e] = (int)((lo >> (8 * e)) & 0xFFu);
+                v[4 + e] = (int)((hw >> (8 * e)) & 0xFFu);
+            }
+            if (k0 == 288) v[7] += 256 * (int)((w[74] >> 8) & 0xFFu);  // k = 295: move_count
         }
-        if (k0 == 288) v[7] += 256 * (int)((w[74] >> 8) & 0xFFu);  // k = 295: move_count
-        const u32x4 q = {pk2((pel)(float)v[0], (pel)(float)v[1]), pk2((pel)(float)v[2], (pel)(float)v[3]),
-                         pk2((pel)(float)v[4], (pel)(float)v[5]), pk2((pel)(float)v[6], (pel)(float)v[7])};
+        bool big = false;
+        if constexpr (F::kExact) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) big = big || (v[e] >= 256 || v[e] <= -256);
+        }
+        const u32x4 q = {pk2<F>((pel)(float)v[0], (pel)(float)v[1]), pk2<F>((pel)(float)v[2], (pel)(float)v[3]),
+                         pk2<F>((pel)(float)v[4], (pel)(float)v[5]), pk2<F>((pel)(float)v[6], (pel)(float)v[7])};
         X[0][s] = __builtin_bit_cast(pelx8, q);
+        if constexpr (F::kExact) hi |= __any(big) ? 1u << s : 0u;
     }
+    return hi;
 }
 
-// the observation's B fragments: lane (r, g), k-step s, element e = obs[table r][32s + 8g + e]
-// (integers < 2048: exact in fp16; < 256 in the bf16 build)
-__device__ __forceinline__ void load_obs(const int32_t *xrow, int g, pelx8 (&X)[1][kKs1]) {
-#pragma unroll
-    for (int s = 0; s < kKs1; ++s) {
-        int v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int k = 32 * s + 8 * g + e;
-            v[e] = k < kObs ? xrow[k < kObs ? k : 0] : 0;
-        }
-        const u32x4 w = {pk2((pel)(float)v[0], (pel)(float)v[1]), pk2((pel)(float)v[2], (pel)(float)v[3]),
-                         pk2((pel)(float)v[4], (pel)(float)v[5]), pk2((pel)(float)v[6], (pel)(float)v[7])};
-        X[0][s] = __builtin_bit_cast(pelx8, w);
-    }
-}
-
-#ifndef SPL_P32_AHEAD1
-#define SPL_P32_AHEAD1 2
-#endif
-#ifndef SPL_P32_AHEAD2
-#define SPL_P32_AHEAD2 1
-#endif
-constexpr int kAheadL1 = SPL_P32_AHEAD1, kAheadHid = SPL_P32_AHEAD2;  // A-plane prefetch depth (k-steps) in the ring kernel
+constexpr int kAheadL1 = 2, kAheadHid = 1;  // A-plane prefetch depth (k-steps) in the ring kernel
 
 // The per-table epilogue over one table's 45 logits (`row`) and mask bytes: greedy masked argmax
 // (training_utils.py:263-276) or masked_categorical's sample, log-prob and entropy, plus the critic
@@ -520,9 +574,12 @@ __device__ __forceinline__ void act_epilogue(const ActArgs &a, const float *row,
 
 // <false, false> greedy actor, <false, true> sampling actor, <true, true> critic + sampling actor
 // (get_action_and_value), <true, false> critic only (ActorCritic.get_value, ppo_splendor.py:51)
-template <bool kCritic, bool kSample>
-__global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict__ W, ActArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLds];
+template <class F, bool kCritic, bool kSample>
+__device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArgs a) {
+    typedef typename F::pelx8 pelx8;
+    typedef Geo<F> G;
+    constexpr int kSlots = F::kSlots, kChunk = G::kChunk;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[G::kLds];
     constexpr bool kActor = kSample || !kCritic;
     constexpr int kTotal = kCritic ? (kActor ? kAllChunks : kCriticChunks) : kActorChunks;
     // the wave index made wave-uniform for the compiler (SGPR), so the ring's LDS slot addresses stay
@@ -547,19 +604,19 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
     // table of row i of this wave (i < valid)
     auto table_of = [&](int i) -> int64_t { return a.order ? (int64_t)a.order[tbase + i] : tbase + i; };
     uint8_t *ring = lds;
-    uint8_t *ms = lds + kLdsMask + wave * kMaskWave;
+    uint8_t *ms = lds + G::kLdsMask + wave * kMaskWave;
     const __amdgpu_buffer_rsrc_t wrs = image_rsrc(W);
 
 #pragma unroll
-    for (int c = 0; c < kSlots - 1; ++c) issue_chunk(wrs, c, ring + c * kChunk, wave, lane);
+    for (int c = 0; c < kSlots - 1; ++c) issue_chunk<F>(wrs, c, ring + c * kChunk, wave, lane);
 
     // grouped rows: the wave's table ids, one load (lane i < valid holds row i's), then shuffles
     const int32_t tid_own = (a.order && lane < valid) ? a.order[tbase + lane] : 0;
     // observation B fragments (load_obs)
     const int64_t xt = valid > 0 ? (a.order ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : tbase + (r < valid ? r : 0)) : 0;
     pelx8 X[1][kKs1];
-    if (a.obs_u8) load_obs_u8(a.obs_u8 + (size_t)xt * 300, g, X);
-    else load_obs(a.obs + (size_t)xt * kObs, g, X);
+    ObsHi hi{0u, a.obs_u8 ? nullptr : a.obs + (size_t)xt * kObs, a.obs_u8 ? a.obs_u8 + (size_t)xt * 300 : nullptr};
+    hi.mask = load_obs<F>(hi.row32, hi.row8, g, X);
     if constexpr (!kActor) {
         // get_value: no mask
     } else if (a.order) {
@@ -597,36 +654,35 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
         return ring;
 #endif
         // this wave's part of chunk c landed (later chunks' loads may stay outstanding)
-        if (wave < kChunkBlocks - (kBlocksPerWave - 1) * kWaves) __builtin_amdgcn_s_waitcnt(vmcnt_imm(kWaitMost));
-        else __builtin_amdgcn_s_waitcnt(vmcnt_imm(kWaitLast));
+        if (wave < G::kChunkBlocks - (G::kBlocksPerWave - 1) * kWaves) __builtin_amdgcn_s_waitcnt(vmcnt_imm(G::kWaitMost));
+        else __builtin_amdgcn_s_waitcnt(vmcnt_imm(G::kWaitLast));
         __builtin_amdgcn_s_barrier();  // everyone's part landed; slot c-1 is free
         asm volatile("" ::: "memory");
         const int nxt = c + kSlots - 1 < kTotal ? c + kSlots - 1 : kTotal - 1;  // past the end: harmless reload
-        issue_chunk(wrs, nxt, ring + ((c + kSlots - 1) % kSlots) * kChunk, wave, lane);
+        issue_chunk<F>(wrs, nxt, ring + ((c + kSlots - 1) % kSlots) * kChunk, wave, lane);
         const uint8_t *slot = ring + (c % kSlots) * kChunk;
         ++c;
         return slot;
     };
-    static_assert(kWaitMost <= 63, "vmcnt range");
 
-    pelx8 H1[kPlanes][kKs2];
+    pelx8 H1[F::kPlanes][kKs2];
     float value = 0.f;
     if constexpr (kCritic) {
-        layer_tanh<kKs1, 1, kAheadL1>(enter, X, H1, lane);
+        layer_tanh<F, kKs1, 1, kAheadL1>(enter, X, H1, lane, &hi);
         // layer 2 tile t -> tanh -> its units' share of the fp32 output unit, on the spot
 #pragma unroll 1
         for (int t = 0; t < kTiles; ++t) {
             const float4 w = *reinterpret_cast<const float4 *>(a.critic_out + 16 * t + 4 * g);
             float h[4];
-            if constexpr (kFoldTanh) {
-                f32x4 c;
-                const f32x4 acc = tile_mma<kKs2, kPlanes, kAheadHid, true>(enter(), H1, lane, &c);
+            if constexpr (F::kExact) {
+                const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid>(enter(), H1, lane);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) h[i] = tanh_fold<0>(acc[i], c[i]);
+                for (int i = 0; i < 4; ++i) h[i] = tanh_acc(acc[i]);
             } else {
-                const f32x4 acc = tile_mma<kKs2, kPlanes, kAheadHid>(enter(), H1, lane);
+                f32x4 cf;
+                const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid, true>(enter(), H1, lane, &cf);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) h[i] = tanh_f32(acc[i]);
+                for (int i = 0; i < 4; ++i) h[i] = tanh_fold<0>(acc[i], cf[i]);
             }
             value = __builtin_fmaf(w.x, h[0], value);
             value = __builtin_fmaf(w.y, h[1], value);
@@ -642,12 +698,12 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
         if (g == 0 && r < valid) a.value[table_of(r)] = value;
         return;
     }
-    layer_tanh<kKs1, 1, kAheadL1>(enter, X, H1, lane);
-    pelx8 H2[kPlanes][kKs2];
-    layer_tanh<kKs2, kPlanes, kAheadHid>(enter, H1, H2, lane);
+    layer_tanh<F, kKs1, 1, kAheadL1>(enter, X, H1, lane, &hi);
+    pelx8 H2[F::kPlanes][kKs2];
+    layer_tanh<F, kKs2, F::kPlanes, kAheadHid>(enter, H1, H2, lane, nullptr);
     f32x4 L[kActTiles];
 #pragma unroll
-    for (int t = 0; t < kActTiles; ++t) L[t] = tile_mma<kKs2, kPlanes, kAheadHid>(enter(), H2, lane);
+    for (int t = 0; t < kActTiles; ++t) L[t] = tile_mma<F, kKs2, F::kPlanes, kAheadHid>(enter(), H2, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing reloads
     __builtin_amdgcn_s_barrier();                      // every wave is done with the ring
 
@@ -668,6 +724,16 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict
     if (g == 0 && r < valid) act_epilogue<kCritic, kSample>(a, lg + r * kLogitRow, ms + r * kAct, table_of(r), value);
 }
 
+// the exact format's kernels keep round 3-4's names (k_act32<critic, sample>), the fp16-plane ones are k_act32h
+template <bool kCritic, bool kSample>
+__global__ __launch_bounds__(kWaves * 64) void k_act32(const uint8_t *__restrict__ W, ActArgs a) {
+    act32_body<FmtBf16x3, kCritic, kSample>(W, a);
+}
+template <bool kCritic, bool kSample>
+__global__ __launch_bounds__(kWaves * 64) void k_act32h(const uint8_t *__restrict__ W, ActArgs a) {
+    act32_body<FmtF16x2, kCritic, kSample>(W, a);
+}
+
 // ---- narrow workgroups: the tails of the grouped evaluation ----------------------------------
 // 65 536 tables fill exactly two rounds of one 128-table workgroup per CU, so the partial last
 // workgroup of every network (the group's tail) used to spill into a third round that took a whole
@@ -684,15 +750,21 @@ constexpr int kNarrowWaves = 8;  // two hidden-layer tiles per wave (2 waves per
 
 // one hidden layer split over the waves (wave w: tiles w and w + 8), then every wave gathers all
 // 16 tiles' tanh outputs (its next layer's B fragments) from LDS
-template <int KS, int NB>
-__device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const pelx8 (&B)[NB][KS],
-                                             pelx8 (&H)[kPlanes][kKs2], float *xbuf, int wave, int lane) {
+template <class F, int KS, int NB>
+__device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const typename F::pelx8 (&B)[NB][KS],
+                                             typename F::pelx8 (&H)[F::kPlanes][kKs2], float *xbuf, int wave, int lane,
+                                             const ObsHi *hi) {
 #pragma unroll
     for (int h = 0; h < kTiles / kNarrowWaves; ++h) {
         const int t = wave + kNarrowWaves * h;
-        const f32x4 acc = tile_mma<KS, NB, kAheadGlobal>(W + (size_t)(chunk0 + t) * kChunk, B, lane);
+        const f32x4 acc = tile_mma<F, KS, NB, kAheadGlobal>(W + (size_t)(chunk0 + t) * Geo<F>::kChunk, B, lane, nullptr, hi);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) xbuf[(4 * t + i) * 64 + lane] = tanh_f32(acc[i]);
+        for (int i = 0; i < 4; ++i) {
+            float y;
+            if constexpr (F::kExact) y = tanh_acc(acc[i]);
+            else y = tanh_fold<0>(acc[i], kTwoLog2e);  // acc is at the true scale here (no fold)
+            xbuf[(4 * t + i) * 64 + lane] = y;
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -700,13 +772,14 @@ __device__ __forceinline__ void narrow_layer(const uint8_t *W, int chunk0, const
         float h[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) h[i] = xbuf[(4 * t + i) * 64 + lane];
-        put_split(H, t, h);
+        put_split<F>(H, t, h);
     }
     __syncthreads();  // xbuf is written again by the next layer
 }
 
-template <bool kSample>
-__global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_t *__restrict__ Wbase, ActArgs a) {
+template <class F, bool kSample>
+__device__ __forceinline__ void act32_narrow_body(const uint8_t *__restrict__ Wbase, ActArgs a) {
+    typedef typename F::pelx8 pelx8;
     __shared__ __attribute__((aligned(16))) float xbuf[kTiles * 4 * 64];  // 16 KB: one layer's outputs
     __shared__ float lg[kRowsPerWave * kLogitRow];
     __shared__ uint8_t ms[kMaskWave];
@@ -723,8 +796,8 @@ __global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_
     const int32_t tid_own = lane < valid ? a.order[tbase + lane] : 0;
     const int64_t xt = valid > 0 ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : 0;
     pelx8 X[1][kKs1];
-    if (a.obs_u8) load_obs_u8(a.obs_u8 + (size_t)xt * 300, g, X);
-    else load_obs(a.obs + (size_t)xt * kObs, g, X);
+    ObsHi hi{0u, a.obs_u8 ? nullptr : a.obs + (size_t)xt * kObs, a.obs_u8 ? a.obs_u8 + (size_t)xt * 300 : nullptr};
+    hi.mask = load_obs<F>(hi.row32, hi.row8, g, X);
     if (wave == 0) {  // the wave-tile's mask bytes (gathered rows), for the epilogue
         constexpr int kMI = (kMaskWave + 63) / 64;
         uint32_t mv[kMI];
@@ -740,11 +813,11 @@ __global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_
             if (e < valid * kAct) ms[e] = (uint8_t)mv[i];
         }
     }
-    pelx8 H1[kPlanes][kKs2], H2[kPlanes][kKs2];
-    narrow_layer(W, 0, X, H1, xbuf, wave, lane);
-    narrow_layer(W, kTiles, H1, H2, xbuf, wave, lane);
+    pelx8 H1[F::kPlanes][kKs2], H2[F::kPlanes][kKs2];
+    narrow_layer<F>(W, 0, X, H1, xbuf, wave, lane, &hi);
+    narrow_layer<F>(W, kTiles, H1, H2, xbuf, wave, lane, nullptr);
     if (wave < kActTiles) {  // logits: waves 0..2 take one 16-row tile each
-        const f32x4 L = tile_mma<kKs2, kPlanes, kAheadGlobal>(W + (size_t)(2 * kTiles + wave) * kChunk, H2, lane);
+        const f32x4 L = tile_mma<F, kKs2, F::kPlanes, kAheadGlobal>(W + (size_t)(2 * kTiles + wave) * Geo<F>::kChunk, H2, lane);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int act = 16 * wave + 4 * g + i;
@@ -759,20 +832,34 @@ __global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_
     if (wave == 0 && g == 0 && r < valid)
         act_epilogue<false, kSample>(a, lg + r * kLogitRow, ms + r * kAct, (int64_t)__shfl(tid_own, r), 0.f);
 }
+template <bool kSample>
+__global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_t *__restrict__ W, ActArgs a) {
+    act32_narrow_body<FmtBf16x3, kSample>(W, a);
+}
+template <bool kSample>
+__global__ __launch_bounds__(kNarrowWaves * 64) void k_act32h_narrow(const uint8_t *__restrict__ W, ActArgs a) {
+    act32_narrow_body<FmtF16x2, kSample>(W, a);
+}
 
 }  // namespace splp32
 
 using namespace splp32;
 
-int64_t splp32_bytes(int with_critic) {
-    return with_critic ? (int64_t)kAllChunks * kChunk + kCriticTail : (int64_t)kActorChunks * kChunk;
+// ---- host side: fmt 0 = exact three bf16 planes (SPL_PREC_FP32), 1 = two fp16 planes (SPL_PREC_FP32_F16X2)
+int64_t splp32_bytes(int with_critic, int fmt) {
+    const int64_t chunk = fmt ? Geo<FmtF16x2>::kChunk : Geo<FmtBf16x3>::kChunk;
+    return with_critic ? (int64_t)kAllChunks * chunk + kCriticTail : (int64_t)kActorChunks * chunk;
 }
 
-int splp32_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream) {
+int splp32_pack(const spl_mlp_t *actor, const spl_mlp_t *critic, void *packed, void *stream, int fmt) {
     const PackNet A{actor->w1, actor->b1, actor->w2, actor->b2, actor->w3, actor->b3, kAct};
     const PackNet C = critic ? PackNet{critic->w1, critic->b1, critic->w2, critic->b2, critic->w3, critic->b3, 1} : A;
-    hipLaunchKernelGGL(k_pack32, dim3(critic ? kAllChunks : kActorChunks), dim3(256), 0, (hipStream_t)stream, A, C,
-                       critic ? 1 : 0, static_cast<uint8_t *>(packed));
+    if (fmt)
+        hipLaunchKernelGGL(k_pack32h, dim3(critic ? kAllChunks : kActorChunks), dim3(256), 0, (hipStream_t)stream, A, C,
+                           critic ? 1 : 0, static_cast<uint8_t *>(packed));
+    else
+        hipLaunchKernelGGL(k_pack32, dim3(critic ? kAllChunks : kActorChunks), dim3(256), 0, (hipStream_t)stream, A, C,
+                           critic ? 1 : 0, static_cast<uint8_t *>(packed));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return spl_fail(SPL_E_HIP, std::string("k_pack32 launch: ") + hipGetErrorString(e));
     return SPL_OK;
@@ -838,11 +925,32 @@ constexpr int kMaxGroups = 64;
 
 int64_t splp32_group_scratch(int32_t n, int32_t groups) { return 4 * ((int64_t)5 * groups + 3 + n); }
 
-// image: a packed fp32 image (full when has_critic); critic: evaluate the critic (SAMPLE with value)
+template <template <bool, bool> class K>
+struct ActKernels {  // the four instantiations of one format's kernel template
+    static void launch(const uint8_t *W, bool critic, bool sample, dim3 grid, dim3 block, hipStream_t s,
+                       const ActArgs &a) {
+        if (critic && sample) hipLaunchKernelGGL((K<true, true>::fn), grid, block, 0, s, W, a);
+        else if (critic) hipLaunchKernelGGL((K<true, false>::fn), grid, block, 0, s, W, a);  // get_value
+        else if (sample) hipLaunchKernelGGL((K<false, true>::fn), grid, block, 0, s, W, a);
+        else hipLaunchKernelGGL((K<false, false>::fn), grid, block, 0, s, W, a);
+    }
+};
+template <bool C, bool S>
+struct ExactK {
+    static constexpr auto fn = k_act32<C, S>;
+};
+template <bool C, bool S>
+struct HalfK {
+    static constexpr auto fn = k_act32h<C, S>;
+};
+
+// image: a packed fp32 image of format `fmt` (full when has_critic); critic: evaluate the critic
+// (SAMPLE with value)
 int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, int32_t n, const spl_act_args_t *args,
-               void *stream, int groups = 0, int64_t image_stride = 0, const int32_t *group_of = nullptr,
+               void *stream, int fmt, int groups = 0, int64_t image_stride = 0, const int32_t *group_of = nullptr,
                void *scratch = nullptr) {
-    const float *critic_out = has_critic ? reinterpret_cast<const float *>(img + (size_t)kAllChunks * kChunk) : nullptr;
+    const int64_t chunk = fmt ? Geo<FmtF16x2>::kChunk : Geo<FmtBf16x3>::kChunk;
+    const float *critic_out = has_critic ? reinterpret_cast<const float *>(img + (size_t)kAllChunks * chunk) : nullptr;
     ActArgs a{args->obs,    args->obs_u8, args->mask,     args->action, args->logprob, args->entropy, args->value,
               args->logits, critic_out,   args->seed,     args->ply,    args->ply_base, args->table0, n,
               nullptr,      nullptr,      0,              0};
@@ -866,21 +974,15 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
     }
     const hipStream_t s = (hipStream_t)stream;
     const uint8_t *W = img;
-    if (has_critic && !critic) W += (size_t)kCriticChunks * kChunk;  // the actor part of a full image
-    if (critic && sample)
-        hipLaunchKernelGGL((k_act32<true, true>), grid, block, 0, s, W, a);
-    else if (critic)  // get_value
-        hipLaunchKernelGGL((k_act32<true, false>), grid, block, 0, s, W, a);
-    else if (sample)
-        hipLaunchKernelGGL((k_act32<false, true>), grid, block, 0, s, W, a);
-    else
-        hipLaunchKernelGGL((k_act32<false, false>), grid, block, 0, s, W, a);
+    if (has_critic && !critic) W += (size_t)kCriticChunks * chunk;  // the actor part of a full image
+    if (fmt) ActKernels<HalfK>::launch(W, critic, sample, grid, block, s, a);
+    else ActKernels<ExactK>::launch(W, critic, sample, grid, block, s, a);
     if (groups > 0) {  // the groups' tails: at most 8 wave-tiles of 16 tables per group
         const dim3 ngrid((unsigned)(groups * (kRowsPerBlock / kRowsPerWave))), nblock(kNarrowWaves * 64);
-        if (sample)
-            hipLaunchKernelGGL((k_act32_narrow<true>), ngrid, nblock, 0, s, W, a);
-        else
-            hipLaunchKernelGGL((k_act32_narrow<false>), ngrid, nblock, 0, s, W, a);
+        if (fmt && sample) hipLaunchKernelGGL(k_act32h_narrow<true>, ngrid, nblock, 0, s, W, a);
+        else if (fmt) hipLaunchKernelGGL(k_act32h_narrow<false>, ngrid, nblock, 0, s, W, a);
+        else if (sample) hipLaunchKernelGGL(k_act32_narrow<true>, ngrid, nblock, 0, s, W, a);
+        else hipLaunchKernelGGL(k_act32_narrow<false>, ngrid, nblock, 0, s, W, a);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return spl_fail(SPL_E_HIP, std::string("k_act32 launch: ") + hipGetErrorString(e));

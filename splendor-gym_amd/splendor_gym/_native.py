@@ -56,7 +56,7 @@ class ActArgs(ctypes.Structure):
 
 
 ACT_SAMPLE, ACT_GREEDY, ACT_VALUE = 0, 1, 2  # SPL_ACT_*
-PREC_FP32, PREC_BF16 = 0, 1    # SPL_PREC_*
+PREC_FP32, PREC_BF16, PREC_FP32_F16X2 = 0, 1, 2    # SPL_PREC_* (FP32: exact three bf16 planes)
 IMG_CRITIC = 1                 # SPL_IMG_CRITIC
 
 

@@ -14,21 +14,24 @@ tables in one HIP launch straight from the engine's int32 observations and int8 
   * ``get_value(obs)`` = ``model.get_value(obs.float())`` (ppo_splendor.py:51, the bootstrap value
     of ppo_splendor.py:302): the critic alone, fp32.
 
-precision="fp32" (default, the reference's precision): fp32-accurate products — every operand split
-into two fp16 planes (22 significant bits; weights scaled per row by a power of two), the three plane
-products of order <= 1 accumulated in fp32 on v_mfma_f32_16x16x32_f16 (csrc/spl_policy32.hip) — so
-logits and values equal the fp32 module's to within 1e-5 relative (tests/test_gpu_policy.py).  precision="bf16" (opt-in): bf16 MFMA with fp32
-accumulation, logits to bf16 accuracy.  Call ``refresh()`` after the module's weights change (e.g.
-after each PPO update).
+precision="fp32" (default, the reference's precision): EXACT fp32 operands — every weight and hidden
+activation split into three bf16 planes (24 significant bits: the fp32 value itself), the six plane
+products of order <= 2 accumulated in fp32 on v_mfma_f32_16x16x32_bf16, the observation exact, tanh to
+a few ulp (csrc/spl_policy32.hip, k_act32) — so logits and values equal the fp32 module's to within
+fp32 rounding (tests/test_gpu_policy.py).  precision="fp32_f16x2": round 4's faster form, two fp16
+planes per operand (22 significant bits), fp32 within 2^-22 per operand (k_act32h).
+precision="bf16" (opt-in): bf16 MFMA with fp32 accumulation, logits to bf16 accuracy.  Call
+``refresh()`` after the module's weights change (e.g. after each PPO update).
 """
 import ctypes
 import weakref
 
 from . import _native
-from ._native import (ACT_GREEDY, ACT_SAMPLE, ACT_VALUE, IMG_CRITIC, NUM_ACTIONS, OBS_DIM, OBS_U8, PREC_BF16, PREC_FP32, ActArgs, MlpDesc,
-                      check, ptr)
+from ._native import (ACT_GREEDY, ACT_SAMPLE, ACT_VALUE, IMG_CRITIC, NUM_ACTIONS, OBS_DIM, OBS_U8, PREC_BF16, PREC_FP32,
+                      PREC_FP32_F16X2, ActArgs, MlpDesc, check, ptr)
 
-_PRECISIONS = {"fp32": PREC_FP32, "bf16": PREC_BF16}
+_PRECISIONS = {"fp32": PREC_FP32, "fp32_f16x2": PREC_FP32_F16X2, "bf16": PREC_BF16}
+_FP32_FORMS = ("fp32", "fp32_f16x2")  # the spl_policy32.hip kernels: compact rows, get_value, grouped pools
 
 
 def _mlp_desc(seq, keep):
@@ -87,7 +90,7 @@ class FusedActorCritic:
 
     def _check_inputs(self, obs, mask):
         t = self.torch
-        u8 = obs.dtype == t.uint8 and self.precision == "fp32"  # compact rows (Engine.step obs_u8)
+        u8 = obs.dtype == t.uint8 and self.precision in _FP32_FORMS  # compact rows (Engine.step obs_u8)
         if (obs.dtype != t.int32 and not u8) or obs.dim() != 2 or obs.shape[1] != (OBS_U8 if u8 else OBS_DIM) \
                 or not obs.is_contiguous():
             raise ValueError("obs must be a contiguous int32 [n, 297] device tensor (fp32: or uint8 [n, 300] rows)")
@@ -135,9 +138,9 @@ class FusedActorCritic:
 
     def get_value(self, obs, out=None):
         """ActorCritic.get_value (ppo_splendor.py:51): the critic's value, f32 [n, 1].  Needs
-        with_critic and precision="fp32"."""
+        with_critic and an fp32 precision."""
         t = self.torch
-        if not self.with_critic or self.precision != "fp32":
+        if not self.with_critic or self.precision not in _FP32_FORMS:
             raise ValueError("get_value needs an fp32 image with the critic")
         if obs.dtype != t.int32 or obs.dim() != 2 or obs.shape[1] != OBS_DIM or not obs.is_contiguous() or \
                 obs.device != self.device:
@@ -152,7 +155,7 @@ class FusedActorCritic:
         f = self
 
         class _Opponent:
-            accepts_u8 = f.precision == "fp32"
+            accepts_u8 = f.precision in _FP32_FORMS
 
             def __call__(self, obs, mask):
                 return f.greedy(obs, mask)
@@ -167,7 +170,8 @@ class OpponentPool:
     start (spl_dual_draw_opponents: Philox keyed by (seed; table, episode), so results do not depend
     on batching or sharding).  Every network is the greedy masked argmax of its actor
     (model_greedy_policy_from / frozen_policy_from), evaluated for all tables in ONE launch
-    (spl_policy_act_grouped: tables sorted by network, one network per workgroup), fp32.
+    (spl_policy_act_grouped: tables sorted by network, one network per workgroup), at `precision`
+    ("fp32": exact fp32 operands, the default; or "fp32_f16x2").
 
     Images: slot 0 is the current policy (re-packed by refresh(), e.g. after each PPO update);
     snapshots live in a ring of pool_size + 2 slots.  A snapshot that leaves the pool keeps its
@@ -184,14 +188,19 @@ class OpponentPool:
 
     MAX_IMAGES = 64
 
-    def __init__(self, agent, pool_size: int = 12, p_current: float = 0.25, seed: int = 0, device=None):
+    def __init__(self, agent, pool_size: int = 12, p_current: float = 0.25, seed: int = 0, device=None,
+                 precision="fp32"):
         torch = _native.require_gpu()
+        if precision not in _FP32_FORMS:
+            raise ValueError(f"OpponentPool precision must be one of {_FP32_FORMS}")
+        self.precision = precision
+        self._prec = _PRECISIONS[precision]
         self.torch = torch
         self.lib = _native.load_library()
         self.agent = agent
         self.pool_size, self.p_current, self.seed = int(pool_size), float(p_current), int(seed)
         self.device = torch.device(device) if device is not None else next(agent.parameters()).device
-        self.image_bytes = int(self.lib.spl_policy_bytes(0, PREC_FP32))
+        self.image_bytes = int(self.lib.spl_policy_bytes(0, self._prec))
         self.n_images = 1 + self.pool_size + 2
         if self.n_images > self.MAX_IMAGES:
             raise ValueError(f"pool_size at most {self.MAX_IMAGES - 3}")
@@ -244,7 +253,7 @@ class OpponentPool:
         actor = _mlp_desc(model.actor, keep)
         ptr_ = self.images.data_ptr() + slot * self.image_bytes
         with self.torch.cuda.device(self.device):
-            check(self.lib, self.lib.spl_policy_pack(ctypes.byref(actor), None, PREC_FP32, ptr_, self._stream()))
+            check(self.lib, self.lib.spl_policy_pack(ctypes.byref(actor), None, self._prec, ptr_, self._stream()))
         self._keep.append(keep)
         self._keep = self._keep[-8:]
 
@@ -307,7 +316,7 @@ class OpponentPool:
         action = out if out is not None else t.empty(n, dtype=t.int32, device=self.device)
         a = ActArgs(obs=None if u8 else obs.data_ptr(), obs_u8=obs.data_ptr() if u8 else None, mask=mask.data_ptr(),
                     action=action.data_ptr(), logprob=None, entropy=None, value=None, logits=None, seed=0, ply=0,
-                    ply_base=None, table0=0, mode=ACT_GREEDY, image=PREC_FP32 << 1)
+                    ply_base=None, table0=0, mode=ACT_GREEDY, image=self._prec << 1)
         with t.cuda.device(self.device):
             check(self.lib, self.lib.spl_policy_act_grouped(self.images.data_ptr(), self.image_bytes, self.n_images,
                                                             group_of.data_ptr(), self._scratch.data_ptr(), n,

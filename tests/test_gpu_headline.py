@@ -208,7 +208,7 @@ def test_selfplay_fused_fp32_actor_matches_torch(weights):
 
 def test_config5_pool_selfplay_at_per_gpu_size_matches_torch():
     """BASELINE config 5 at its per-GPU size (65 536 tables): the fused loop —
-    agent = fused fp32 ActorCritic, opponent = OpponentPool with 12 frozen snapshots + the current
+    agent = fused fp32 ActorCritic (exact fp32 operands), opponent = OpponentPool with 12 frozen snapshots + the current
     policy drawn per episode (spl_policy_act_grouped) — against the same loop with the torch fp32
     modules (each table's opponent = the network the pool drew for its episode), 40 dual steps.  Per
     table: agent and opponent actions, rewards, done and the next observations equal, except tables
@@ -269,6 +269,7 @@ def test_config5_pool_selfplay_at_per_gpu_size_matches_torch():
         return ((top2[:, 0] - top2[:, 1]) <= 1e-5).all().item()
 
     done_total = 0
+    max_rel = 0.0  # the agent's logits against torch fp32, over every untainted table of every step
     for k in range(steps):
         ok = ~tainted
         assert torch.equal(oF[ok], oT[ok]) and torch.equal(iF["action_mask"][ok], iT["action_mask"][ok]), k
@@ -277,7 +278,9 @@ def test_config5_pool_selfplay_at_per_gpu_size_matches_torch():
             vT = agent.get_value(oF.float())
             lgT = agent.actor(oT.float())
         assert torch.allclose(value, vT, rtol=1e-5, atol=1e-5), k
-        aF = fa.greedy(oF, iF["action_mask"])
+        aF, lgF = fa.greedy(oF, iF["action_mask"], want_logits=True)
+        okr = ~tainted
+        max_rel = max(max_rel, ((lgF[okr] - lgT[okr]).abs() / (lgT[okr].abs() + 1)).max().item())
         aT = torch.argmax(lgT.masked_fill(iT["action_mask"] < 1, float("-inf")), dim=-1).to(torch.int32)
         diff = (aF != aT) & ok
         if diff.any():
@@ -294,6 +297,11 @@ def test_config5_pool_selfplay_at_per_gpu_size_matches_torch():
             ok = ~tainted
         assert torch.equal(rF[ok], rT[ok]) and torch.equal(orF[ok], orT[ok]) and torch.equal(dF[ok], dT[ok]), k
         done_total += int(dF[ok].sum())
+    # the precision of the credited config-5 line, recorded (exact fp32 operands)
+    print("config5_precision", {"max_logit_rel_err_vs_torch_fp32": max_rel,
+                                "near_tie_tainted_fraction": tainted.float().mean().item(), "tables": N,
+                                "dual_steps": steps, "precision": fa.precision})
+    assert max_rel <= 1e-5, max_rel
     assert tainted.float().mean().item() <= 0.01, int(tainted.sum())
     assert len(torch.unique(cur["groups"])) == 13  # the current policy and all 12 snapshots played
     assert done_total > 0  # episodes ended, re-dealt and drew their next opponents inside the loop

@@ -1,14 +1,17 @@
 """Fused ActorCritic forward (include/splendor_policy.h) against the torch fp32 module it replaces
 (ppo_splendor.py:27-59 ActorCritic / masked_categorical; training_utils.py:263-276 greedy).
 
-fp32 kernel (the default, the reference's precision; fp32-accurate products: two fp16 planes per
-operand (22 significant bits, weights scaled per row by a power of two), three plane products
-accumulated in fp32 on v_mfma_f32_16x16x32_f16):
+fp32 kernels — precision="fp32" (the default since round 5: EXACT fp32 operands, three bf16 planes per
+operand, six plane products accumulated in fp32 on v_mfma_f32_16x16x32_bf16, tanh to a few ulp) and
+precision="fp32_f16x2" (round 4's form: two fp16 planes, 22 significant bits, three products):
   * |logit - ref| <= 1e-5 * (|ref| + 1) and |value - ref| <= 1e-5 * (|ref| + 1) against the plain
-    fp32 module (what is left is summation order, the planes' 2^-22 representation and the kernel's
-    few-ulp tanh vs torch's, ~1e-6);
+    fp32 module (what is left is summation order, the kernel's few-ulp tanh vs torch's, and for
+    fp32_f16x2 the planes' 2^-22 representation, ~1e-6);
   * greedy actions EQUAL torch's argmax on every row whose top two legal logits are more than
-    1e-5 apart (closer pairs are ties at fp32 rounding: each side's sums round differently).
+    1e-5 apart (closer pairs are ties at fp32 rounding: each side's sums round differently);
+  * against a float64 evaluation of the same module (the exact answer), the exact format's error is
+    no larger than the fp16-plane format's and of the order of torch fp32's own
+    (test_exact_format_error_against_float64, 65 536 tables; the numbers are printed).
 
 bf16 kernel (opt-in, precision="bf16"; bf16 MFMA, fp32 accumulation):
   * against a torch model of the SAME bf16 roundings (inputs, weights and hidden activations
@@ -23,6 +26,7 @@ import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+FP32_FORMS = ["fp32", "fp32_f16x2"]
 
 
 def states(n, seed=5, plies=12):
@@ -54,8 +58,9 @@ def model(seed=0, device="cuda"):
     return ActorCritic().to(device).eval()
 
 
+@pytest.mark.parametrize("precision", FP32_FORMS)
 @pytest.mark.parametrize("n", [33, 4096])
-def test_trained_checkpoint_matches_torch_fp32(n):
+def test_trained_checkpoint_matches_torch_fp32(n, precision):
     """The reference's trained weights (config 5's actor): logits and values within the fp32
     tolerance of the torch module, greedy actions equal wherever the top two legal logits are more
     than 1e-5 apart, sampled actions legal."""
@@ -64,7 +69,7 @@ def test_trained_checkpoint_matches_torch_fp32(n):
     _, obs, mask = states(max(n, 64), seed=13, plies=20)
     obs, mask = obs[:n].contiguous(), mask[:n].contiguous()
     m = model("trained")
-    full = FusedActorCritic(m, with_critic=True)
+    full = FusedActorCritic(m, with_critic=True, precision=precision)
     act, logits = full.greedy(obs, mask, want_logits=True)
     with torch.no_grad():
         ref = m.actor(obs.float())
@@ -105,14 +110,15 @@ def greedy_clear(logits_ref, mask, gap):
     return want, clear
 
 
+@pytest.mark.parametrize("precision", FP32_FORMS)
 @pytest.mark.parametrize("n", [1, 33, 1000, 8192])
-def test_greedy_logits_match_torch_fp32(n):
+def test_greedy_logits_match_torch_fp32(n, precision):
     import torch
     from splendor_gym.fused_policy import FusedActorCritic
     _, obs, mask = states(max(n, 64))
     obs, mask = obs[:n].contiguous(), mask[:n].contiguous()
     m = model(1)
-    f = FusedActorCritic(m, with_critic=False)  # precision="fp32"
+    f = FusedActorCritic(m, with_critic=False, precision=precision)
     act, logits = f.greedy(obs, mask, want_logits=True)
     with torch.no_grad():
         ref32 = m.actor(obs.float())
@@ -144,9 +150,10 @@ def test_greedy_logits_match_torch_bf16(n):
     assert (act[none] == 0).all()
 
 
+@pytest.mark.parametrize("precision", FP32_FORMS)
 @pytest.mark.parametrize("weights", [2, "trained"])
 @pytest.mark.parametrize("n", [1, 33, 1000, 4096])
-def test_get_value_equals_sample_value(weights, n):
+def test_get_value_equals_sample_value(weights, n, precision):
     """SPL_ACT_VALUE (ActorCritic.get_value, ppo_splendor.py:51) runs the critic alone: bit-equal to
     the value the SAMPLE launch returns (same instructions), within the fp32 tolerance of torch,
     and it needs no mask; partial last waves and workgroups included."""
@@ -155,7 +162,7 @@ def test_get_value_equals_sample_value(weights, n):
     _, obs, mask = states(max(n, 64), seed=13)
     obs, mask = obs[:n].contiguous(), mask[:n].contiguous()
     m = model(weights)
-    f = FusedActorCritic(m, with_critic=True)
+    f = FusedActorCritic(m, with_critic=True, precision=precision)
     v = f.get_value(obs)
     _, _, _, v_sample = f.act(obs, mask, seed=1, ply=1)
     assert v.shape == (n, 1) and torch.equal(v, v_sample)
@@ -163,10 +170,10 @@ def test_get_value_equals_sample_value(weights, n):
         vref = m.get_value(obs.float())
     assert fp32_close(v, vref), (v - vref).abs().max().item()
     with pytest.raises(Exception):
-        FusedActorCritic(m, with_critic=False).get_value(obs)
+        FusedActorCritic(m, with_critic=False, precision=precision).get_value(obs)
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", FP32_FORMS + ["bf16"])
 @pytest.mark.parametrize("n", [1, 33, 1000, 4096])
 def test_full_image_serves_greedy_and_sample(precision, n):
     """An actor+critic image answers GREEDY (actor part) and SAMPLE (both nets), also for partial
@@ -187,7 +194,7 @@ def test_full_image_serves_greedy_and_sample(precision, n):
         vref = bf16_ref(m.critic, obs)
         vref32 = m.critic(obs.float())
     assert value.shape == (n, 1)
-    if precision == "fp32":
+    if precision in FP32_FORMS:
         assert fp32_close(value, vref32), (value - vref32).abs().max().item()
     else:
         assert (value - vref).abs().max().item() <= 2e-2
@@ -195,14 +202,14 @@ def test_full_image_serves_greedy_and_sample(precision, n):
     # log_prob / entropy of torch's Categorical over the kernel's own logits
     from splendor_gym.policy import masked_categorical
     dist = masked_categorical(logits, mask.float())
-    tol = 1e-5 if precision == "fp32" else 1e-4
+    tol = 1e-5 if precision in FP32_FORMS else 1e-4
     assert torch.allclose(logprob, dist.log_prob(action.long()), atol=tol, rtol=tol)
     assert torch.allclose(entropy, dist.entropy(), atol=tol, rtol=tol)
     legal_any = mask.sum(dim=1) > 0
     assert (mask[legal_any].gather(1, action[legal_any].long()[:, None]) != 0).all()
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", FP32_FORMS + ["bf16"])
 def test_sample_determinism_and_no_legal_rows(precision):
     import torch
     from splendor_gym.fused_policy import FusedActorCritic
@@ -220,7 +227,7 @@ def test_sample_determinism_and_no_legal_rows(precision):
     assert (f.greedy(obs, mask)[::17] == 0).all()
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", FP32_FORMS + ["bf16"])
 def test_sample_frequencies_match_softmax(precision):
     import torch
     from splendor_gym.fused_policy import FusedActorCritic
@@ -244,7 +251,7 @@ def test_sample_frequencies_match_softmax(precision):
     assert freq[k[0].cpu().numpy() == 0].sum() == 0
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("precision", FP32_FORMS + ["bf16"])
 def test_refresh_tracks_weight_updates(precision):
     import torch
     from splendor_gym.fused_policy import FusedActorCritic
@@ -259,11 +266,14 @@ def test_refresh_tracks_weight_updates(precision):
     assert torch.allclose(v2 - v1, torch.ones_like(v1), atol=1e-3)
 
 
-def test_large_crafted_observation_values_are_exact():
+@pytest.mark.parametrize("precision", FP32_FORMS)
+def test_large_crafted_observation_values_are_exact(precision):
     """observation values above 255 (crafted move_count / token counts; the device keeps
-    move_count <= 508 and counts <= 255, SPL_E_RANGE beyond) must enter layer 1 exactly.  Round 4's
-    fp16 planes hold integers < 2048 exactly, on the int32 rows and on the compact obs_u8 rows (byte
-    297 carries move_count >> 8): logits and values stay within the fp32 tolerance of torch."""
+    move_count <= 508 and counts <= 255, SPL_E_RANGE beyond) must enter layer 1 exactly: the fp16
+    planes hold integers < 2048 exactly; the exact format's bf16 plane holds them below 256 and adds
+    the residual plane's products for the k-steps of a wave that hold larger ones (ObsHi) — on the
+    int32 rows and on the compact obs_u8 rows (byte 297 carries move_count >> 8): logits and values
+    stay within the fp32 tolerance of torch."""
     import torch
     from splendor_gym import _native
     from splendor_gym.fused_policy import FusedActorCritic
@@ -281,7 +291,7 @@ def test_large_crafted_observation_values_are_exact():
     u8[:, :297] = (obs & 0xFF).to(torch.uint8)
     u8[:, 297] = (obs[:, 295] >> 8).to(torch.uint8)
     m = model("trained")
-    f = FusedActorCritic(m, with_critic=True)
+    f = FusedActorCritic(m, with_critic=True, precision=precision)
     a32, lp32, _, v32, lg32 = f.act(obs, mask, seed=3, ply=1, want_logits=True)
     a8, lp8, _, v8, lg8 = f.act(u8, mask, seed=3, ply=1, want_logits=True)
     with torch.no_grad():
@@ -290,3 +300,44 @@ def test_large_crafted_observation_values_are_exact():
     assert fp32_close(lg32, ref), (lg32 - ref).abs().max().item()
     assert fp32_close(v32, vref), (v32 - vref).abs().max().item()
     assert torch.equal(lg8, lg32) and torch.equal(v8, v32) and torch.equal(a8, a32) and torch.equal(lp8, lp32)
+
+
+def _rel_err(got, ref):
+    """max |got - ref| / (|ref| + 1) over every element (float64)."""
+    return ((got.double() - ref).abs() / (ref.abs() + 1)).max().item()
+
+
+@pytest.mark.parametrize("weights", [1, "trained"])
+def test_exact_format_error_against_float64(weights):
+    """at config 5's per-GPU size (65 536 tables), the logits and values of both fp32
+    formats against a float64 evaluation of the same module (the exact answer), next to torch fp32's own
+    error.  The exact format (three bf16 planes) must be no worse than the fp16-plane format and within
+    a small multiple of torch fp32; its greedy actions differ from torch fp32's only at near ties.  The
+    measured errors are printed (tools/gpu_session.sh keeps the output under profiles/)."""
+    import copy
+    import json
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic
+    n = 65536
+    _, obs, mask = states(n, seed=17, plies=20)
+    m = model(weights)
+    m64 = copy.deepcopy(m).double()
+    with torch.no_grad():
+        ref64, v64 = m64.actor(obs.double()), m64.critic(obs.double())
+        ref32, v32 = m.actor(obs.float()), m.critic(obs.float())
+    errs = {"torch_fp32": {"logits": _rel_err(ref32, ref64), "value": _rel_err(v32, v64)}}
+    want, clear = greedy_clear(ref32, mask, 1e-5)
+    for prec in FP32_FORMS:
+        f = FusedActorCritic(m, with_critic=True, precision=prec)
+        act, lg = f.greedy(obs, mask, want_logits=True)
+        v = f.get_value(obs)
+        errs[prec] = {"logits": _rel_err(lg, ref64), "value": _rel_err(v, v64),
+                      "logits_vs_torch_fp32": _rel_err(lg, ref32.double()),
+                      "greedy_differs_from_torch": int((act != want).sum().item()),
+                      "greedy_differs_outside_near_ties": int((act[clear] != want[clear]).sum().item())}
+    errs["near_tie_fraction"] = 1.0 - clear.float().mean().item()
+    print("precision_vs_float64", json.dumps({"weights": str(weights), "tables": n, **errs}))
+    ex, h2, t32 = errs["fp32"], errs["fp32_f16x2"], errs["torch_fp32"]
+    assert ex["greedy_differs_outside_near_ties"] == 0
+    assert ex["logits"] <= h2["logits"] and ex["value"] <= h2["value"] * 1.0001, errs
+    assert ex["logits"] <= 4 * t32["logits"] + 1e-7 and ex["value"] <= 4 * t32["value"] + 1e-7, errs

@@ -51,10 +51,11 @@ def test_policy_abi_host_side_errors():
     lib = _native.load_library()
     # bf16: actor 18 chunks, full image 35 chunks + the fp32 critic output layer; fp32: 35 / 67 chunks + tail
     assert lib.spl_policy_bytes(0, 1) == 18 * 20480 and lib.spl_policy_bytes(1, 1) == 35 * 20480 + 272 * 4
-    # fp32 images: 21-KB chunks (2 fp16 planes of a 16-row tile + its scaled biases and row factors,
-    # spl_policy32.hip)
-    assert lib.spl_policy_bytes(0, 0) == 35 * 21504 and lib.spl_policy_bytes(1, 0) == 67 * 21504 + 272 * 4
-    assert lib.spl_policy_bytes(0, 9) == -1
+    # fp32 images (spl_policy32.hip): exact (SPL_PREC_FP32, 0) 31-KB chunks of three bf16 planes of a
+    # 16-row tile + its biases and row factors; two fp16 planes (SPL_PREC_FP32_F16X2, 2) 21-KB chunks
+    assert lib.spl_policy_bytes(0, 0) == 35 * 31744 and lib.spl_policy_bytes(1, 0) == 67 * 31744 + 272 * 4
+    assert lib.spl_policy_bytes(0, 2) == 35 * 21504 and lib.spl_policy_bytes(1, 2) == 67 * 21504 + 272 * 4
+    assert lib.spl_policy_bytes(0, 9) == -1 and lib.spl_policy_bytes(0, 3) == -1
     assert lib.spl_policy_pack(None, None, 0, None, None) == -1
     assert b"actor" in lib.spl_last_error()
     assert lib.spl_policy_act(None, 0, 1, None, None) == -1
@@ -69,7 +70,8 @@ def test_policy_abi_host_side_errors():
     # reverse) is refused instead of evaluating the wrong chunks
     args.value = None
     for image, size in ((0, lib.spl_policy_bytes(1, 0)), (1, lib.spl_policy_bytes(0, 0)),
-                        (2, lib.spl_policy_bytes(0, 0)), (0, lib.spl_policy_bytes(0, 1)), (3, 35 * 20480)):
+                        (2, lib.spl_policy_bytes(0, 0)), (0, lib.spl_policy_bytes(0, 1)), (3, 35 * 20480),
+                        (4, lib.spl_policy_bytes(0, 0)), (0, lib.spl_policy_bytes(0, 2))):
         args.image = image
         assert lib.spl_policy_act(ctypes.c_void_p(4096), size, 1, ctypes.byref(args), None) == -1
         assert b"packed_bytes" in lib.spl_last_error()

@@ -37,8 +37,9 @@ def main():
     obs, mask = e.obs, e.mask
     torch.manual_seed(0)
     m = ActorCritic().to(e.device).eval()
-    f = FusedActorCritic(m)                       # fp32 (fp32-accurate split-bf16 products)
-    f16 = FusedActorCritic(m, precision="bf16")   # opt-in bf16 MFMA
+    f = FusedActorCritic(m)                             # fp32: exact operands, three bf16 planes
+    fh = FusedActorCritic(m, precision="fp32_f16x2")    # fp32 within 2^-22: two fp16 planes
+    f16 = FusedActorCritic(m, precision="bf16")         # opt-in bf16 MFMA
 
     def timeit(fn):
         for _ in range(5):
@@ -55,6 +56,8 @@ def main():
     res = {}
     res["fused_fp32_sample_us"] = timeit(lambda: f.act(obs, mask, seed=1, ply=2))
     res["fused_fp32_greedy_us"] = timeit(lambda: f.greedy(obs, mask))
+    res["fused_fp32_f16x2_sample_us"] = timeit(lambda: fh.act(obs, mask, seed=1, ply=2))
+    res["fused_fp32_f16x2_greedy_us"] = timeit(lambda: fh.greedy(obs, mask))
     res["fused_bf16_sample_us"] = timeit(lambda: f16.act(obs, mask, seed=1, ply=2))
     res["fused_bf16_greedy_us"] = timeit(lambda: f16.greedy(obs, mask))
 
@@ -72,7 +75,7 @@ def main():
         res["torch_fp32_greedy_us"] = timeit(lambda: greedy_actions(m, obs, mask))
     fl_s = 2.0 * n * (MACS_ACTOR + MACS_CRITIC)
     fl_g = 2.0 * n * MACS_ACTOR
-    for p in ("fp32", "bf16"):
+    for p in ("fp32", "fp32_f16x2", "bf16"):
         res[f"fused_{p}_sample_tflops"] = fl_s / res[f"fused_{p}_sample_us"] / 1e6
         res[f"fused_{p}_greedy_tflops"] = fl_g / res[f"fused_{p}_greedy_us"] / 1e6
     res["peak_tflops"] = {"fp32": 157.3, "bf16": 2500.0}  # dense MFMA peaks (MI355X_MICROARCH.md)

@@ -149,6 +149,12 @@ for step in "$@"; do
       done; done ;;
     abl32) bash tools/ablate_policy32.sh || exit 1 ;;  # k_act32 timing ablations (BUILD=1 here first)
     chains) run step_chains 300 python3 tools/bench_step_chains.py ;;  # step mode as 1/2/4 independent chains
+    polprec) run pytest_polprec 600 python -u -m pytest tests/test_gpu_policy.py tests/test_gpu_opponent_pool.py \
+                 tests/test_gpu_compact_obs.py -x -v -s --timeout 300 --timeout-method thread
+             grep -h "precision_vs_float64" $O/pytest_polprec_$TAG.out > $O/precision_vs_float64_$TAG.txt || true ;;
+    c5tests) run pytest_c5 600 python -u -m pytest tests/test_gpu_headline.py -k "selfplay or config5" -x -v -s \
+                 --timeout 300 --timeout-method thread
+             grep -h "config5_precision" $O/pytest_c5_$TAG.out > $O/config5_precision_$TAG.txt || true ;;
     faultpart) run pytest_faultpart 600 python -u -m pytest tests/test_gpu_faults.py tests/test_gpu_parity.py \
                    tests/test_gpu_headline.py -k "fault or partner or headline_rollout" -x -v --timeout 300 --timeout-method thread ;;
     *) echo "unknown step $step"; exit 2 ;;
