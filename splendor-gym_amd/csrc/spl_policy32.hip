@@ -39,6 +39,11 @@
 
 #include <string>
 
+// SPL_P32_PIPE (default 1): each tile's epilogue is issued in stages inside the next tile's k-steps
+// (PendTile below); 0: after its own tile's MFMA chain (round 4's order).  Same results either way.
+#ifndef SPL_P32_PIPE
+#define SPL_P32_PIPE 1
+#endif
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
 // streaming, no per-tile barrier), 4 A fragments loaded once per tile (no per-group LDS reads)
 #ifndef SPL_POL_ABL
@@ -103,7 +108,8 @@ struct Geo {
     static constexpr int kBiasOff = kKs1 * F::kPlanes * kFrag;  // after the largest weight block
     static constexpr int kChunk = kBiasOff + 1024;              // + 16 biases, 16 row factors, 16 tanh factors
     static constexpr int kLdsMask = F::kSlots * kChunk;
-    static constexpr int kLds = kLdsMask + kWaves * kMaskWave;
+    static constexpr int kLdsCritic = kLdsMask + kWaves * kMaskWave;  // the critic's fp32 output layer (1 KB)
+    static constexpr int kLds = kLdsCritic + kCriticTail;
     static constexpr int kChunkBlocks = kChunk / 1024;                           // 31 / 21
     static constexpr int kBlocksPerWave = (kChunkBlocks + kWaves - 1) / kWaves;  // 4 / 3
     // a wave's loads of the chunks after chunk c that may stay in flight when it enters chunk c
@@ -347,9 +353,14 @@ __device__ __forceinline__ bf16x8 obs_residual(const ObsHi &h, int s, int g) {
 // narrow kernel), D k-steps ahead of the MFMAs that use them.
 // kFold: the sum is returned as the products left it (scaled by the row factor's inverse) and
 // `fold` gets the tile's tanh factors (tanh_fold) instead.
-template <class F, int KS, int NB, int D, bool kFold = false>
+// `stage(s)` runs after k-step s's MFMAs, inside the same scheduling segment (SPL_P32_PIPE: the previous
+// tile's epilogue, one stage per k-step, so its VALU work issues between this tile's MFMAs).
+struct NoStage {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+template <class F, int KS, int NB, int D, bool kFold = false, class Stage = NoStage>
 __device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const typename F::pelx8 (&B)[NB][KS], int lane,
-                                          f32x4 *fold = nullptr, const ObsHi *hi = nullptr) {
+                                          f32x4 *fold = nullptr, const ObsHi *hi = nullptr, Stage &&stage = Stage()) {
     typedef typename F::pelx8 pelx8;
     constexpr int kPlanes = F::kPlanes;
     static_assert(NB == 1 || NB == kPlanes, "planes");
@@ -398,6 +409,7 @@ __device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const typename F::
             acc = mma<F>(a[0], B[1][s], acc);
             acc = mma<F>(a[0], B[0][s], acc);
         }
+        stage(s);
         if (NB > 1 || (s & 1) == 1) __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (F::kRowMaxExp != 0 && !kFold) acc *= unscale;  // exact: powers of two
@@ -427,6 +439,73 @@ __device__ __forceinline__ void put_split(typename F::pelx8 (&H)[F::kPlanes][kKs
         w[2 * (t & 1)] = pk2<F>(x[0][p], x[1][p]);
         w[2 * (t & 1) + 1] = pk2<F>(x[2][p], x[3][p]);
         H[p][t >> 1] = __builtin_bit_cast(pelx8, w);
+    }
+}
+
+// ---- the staged epilogue (SPL_P32_PIPE) ------------------------------------------------------------
+// A tile's epilogue (tanh of its four pre-activations per lane, the split of the results into the next
+// layer's B planes, or the critic's value FMAs) is issued in stages inside the NEXT tile's k-step loop:
+// stage s after k-step s's MFMAs, so that its VALU work fills the MFMA pipe's issue gaps instead of
+// following the tile's MFMA chain (where both waves of a SIMD would do VALU at once while the matrix
+// core idles).  Same instructions, same results: a stage only reorders independent work.
+// stages 0-3: tanh of value s; 4-5: the split of values (0, 1) / (2, 3) into the planes of tile t
+template <class F>
+struct PendTile {
+    f32x4 acc, c;  // pre-activations as the products left them; tanh factors (fp16-plane format)
+    float h[4];
+};
+template <class F>
+__device__ __forceinline__ float pend_tanh(const PendTile<F> &q, int i) {
+    if constexpr (F::kExact) return tanh_acc(q.acc[i]);
+    else return tanh_fold<F::kActScaleExp>(q.acc[i], q.c[i]);
+}
+// values (2 pair, 2 pair + 1) of tile t -> dword 2 (t & 1) + pair of k-step t / 2 of every plane
+template <class F>
+__device__ __forceinline__ void put_pair(typename F::pelx8 (&H)[F::kPlanes][kKs2], int t, int pair, float ha, float hb) {
+    typedef typename F::pel pel;
+    typedef typename F::pelx8 pelx8;
+    pel xa[F::kPlanes], xb[F::kPlanes];
+    split_planes<F>(ha, xa);  // h carries 2^kActScaleExp already (tanh_fold) or needs none (exact)
+    split_planes<F>(hb, xb);
+#pragma unroll
+    for (int p = 0; p < F::kPlanes; ++p) {
+        u32x4 w = __builtin_bit_cast(u32x4, H[p][t >> 1]);
+        w[2 * (t & 1) + pair] = pk2<F>(xa[p], xb[p]);
+        H[p][t >> 1] = __builtin_bit_cast(pelx8, w);
+    }
+}
+// Each stage's results are pinned where the stage stands (an empty asm that reads and rewrites them):
+// left alone, the compiler sinks every tile's epilogue of a layer to the first use of its results — all
+// 16 of them into the NEXT layer's first tile, one ~1 000-instruction VALU block during which the matrix
+// cores idle (the round-4 kernel's schedule too, seen in its ISA: 16 MFMA-only tiles, then 385 VALU +
+// 128 transcendental ops at the start of the next layer).
+template <class F>
+__device__ __forceinline__ void pin(typename F::pelx8 &x) {
+    asm volatile("" : "+v"(x));
+}
+__device__ __forceinline__ void pin(float &x) { asm volatile("" : "+v"(x)); }
+template <class F>
+__device__ __forceinline__ void split_stage(typename F::pelx8 (&H)[F::kPlanes][kKs2], int t, PendTile<F> &q, int s) {
+    if (s < 4) {
+        q.h[s] = pend_tanh<F>(q, s);
+        pin(q.h[s]);
+    } else if (s == 4 || s == 5) {
+        put_pair<F>(H, t, s - 4, q.h[2 * (s - 4)], q.h[2 * (s - 4) + 1]);
+#pragma unroll
+        for (int p = 0; p < F::kPlanes; ++p) pin<F>(H[p][t >> 1]);
+    }
+}
+// the critic's output unit: value += w[s] tanh(pre-activation s), w = the tile's output weights of this
+// lane group's units (16 t + 4 g ..; staged in LDS once per workgroup: loaded per tile from global
+// memory the compiler hoisted all 16 tiles' loads and spilled)
+template <class F>
+__device__ __forceinline__ void value_stage(PendTile<F> &q, const float *w, float &value, int s) {
+    if (s < 4) {
+        float y;
+        if constexpr (F::kExact) y = tanh_acc(q.acc[s]);
+        else y = tanh_fold<0>(q.acc[s], q.c[s]);  // the critic's layer-2 units unscaled
+        value = __builtin_fmaf(w[s], y, value);
+        pin(value);
     }
 }
 
@@ -507,7 +586,13 @@ __device__ __forceinline__ uint32_t load_obs(const int32_t *row32, const uint8_t
     return hi;
 }
 
-constexpr int kAheadL1 = 2, kAheadHid = 1;  // A-plane prefetch depth (k-steps) in the ring kernel
+// A-plane prefetch depth (k-steps) in the ring kernel.  The scheduler places a k-step's LDS reads
+// anywhere inside the previous k-step's segment (often after half its MFMAs), so one k-step ahead left
+// ~3 MFMAs of distance to cover the LDS latency in the hidden layers
+#ifndef SPL_P32_AHEAD2
+#define SPL_P32_AHEAD2 2
+#endif
+constexpr int kAheadL1 = 2, kAheadHid = SPL_P32_AHEAD2;
 
 // The per-table epilogue over one table's 45 logits (`row`) and mask bytes: greedy masked argmax
 // (training_utils.py:263-276) or masked_categorical's sample, log-prob and entropy, plus the critic
@@ -667,6 +752,86 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
 
     pelx8 H1[F::kPlanes][kKs2];
     float value = 0.f;
+#if SPL_P32_PIPE
+    // each tile's epilogue runs in stages inside the next tile's k-steps (PendTile; the last tile of a
+    // layer inside the next layer's first tile, before that tile's k-step 7 reads the planes it writes)
+    constexpr bool kFoldP = !F::kExact;
+    PendTile<F> q;
+    const float *crit = reinterpret_cast<const float *>(lds + G::kLdsCritic);  // the critic's output layer
+    if constexpr (kCritic) {
+        float *cw = reinterpret_cast<float *>(lds + G::kLdsCritic);
+        for (int k = threadIdx.x; k < kCriticTail / 4; k += kWaves * 64) cw[k] = a.critic_out[k];
+        // visible to every wave after the first ring barrier (enter)
+#pragma unroll
+        for (int t = 0; t < kTiles; ++t) {  // critic layer 1 -> H1
+            f32x4 cf;
+            const f32x4 acc = tile_mma<F, kKs1, 1, kAheadL1, kFoldP>(enter(), X, lane, &cf, &hi, [&](int s) {
+                if (t > 0) split_stage<F>(H1, t - 1, q, s);
+            });
+            q.acc = acc;
+            q.c = cf;
+        }
+        {  // critic layer 2 -> its tiles' shares of the output unit; tile 0 finishes layer 1's last tile
+            f32x4 cf;
+            const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid, kFoldP>(enter(), H1, lane, &cf, nullptr, [&](int s) {
+                split_stage<F>(H1, kTiles - 1, q, s);
+            });
+            q.acc = acc;
+            q.c = cf;
+        }
+#pragma unroll 1
+        for (int t = 1; t < kTiles; ++t) {  // one loop body (as round 4's critic layer 2): no register
+            f32x4 cf;                       // array is indexed by t here
+            const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid, kFoldP>(enter(), H1, lane, &cf, nullptr, [&](int s) {
+                value_stage<F>(q, crit + 16 * (t - 1) + 4 * g, value, s);
+            });
+            q.acc = acc;
+            q.c = cf;
+        }
+    }
+    if constexpr (!kActor) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) value_stage<F>(q, crit + 16 * (kTiles - 1) + 4 * g, value, s);  // the last tile's share
+        value += __shfl_xor(value, 16);  // the other lane groups' units, then the bias
+        value += __shfl_xor(value, 32);
+        value += crit[kHid];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing reloads land while the LDS is ours
+        if (g == 0 && r < valid) a.value[table_of(r)] = value;
+        return;
+    }
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) {  // actor layer 1 -> H1 (the critic's layer 2 has read H1 by now)
+        f32x4 cf;
+        const f32x4 acc = tile_mma<F, kKs1, 1, kAheadL1, kFoldP>(enter(), X, lane, &cf, &hi, [&](int s) {
+            if (t > 0) split_stage<F>(H1, t - 1, q, s);
+            else if (kCritic) value_stage<F>(q, crit + 16 * (kTiles - 1) + 4 * g, value, s);
+        });
+        q.acc = acc;
+        q.c = cf;
+    }
+    if constexpr (kCritic) {
+        value += __shfl_xor(value, 16);
+        value += __shfl_xor(value, 32);
+        value += crit[kHid];
+    }
+    pelx8 H2[F::kPlanes][kKs2];
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) {  // actor layer 2 -> H2
+        f32x4 cf;
+        const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid, kFoldP>(enter(), H1, lane, &cf, nullptr, [&](int s) {
+            if (t == 0) split_stage<F>(H1, kTiles - 1, q, s);
+            else split_stage<F>(H2, t - 1, q, s);
+        });
+        q.acc = acc;
+        q.c = cf;
+    }
+    f32x4 L[kActTiles];
+#pragma unroll
+    for (int t = 0; t < kActTiles; ++t)  // the logits (true scale)
+        L[t] = tile_mma<F, kKs2, F::kPlanes, kAheadHid>(enter(), H2, lane, nullptr, nullptr, [&](int s) {
+            if (t == 0) split_stage<F>(H2, kTiles - 1, q, s);
+        });
+#else
     if constexpr (kCritic) {
         layer_tanh<F, kKs1, 1, kAheadL1>(enter, X, H1, lane, &hi);
         // layer 2 tile t -> tanh -> its units' share of the fp32 output unit, on the spot
@@ -704,6 +869,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     f32x4 L[kActTiles];
 #pragma unroll
     for (int t = 0; t < kActTiles; ++t) L[t] = tile_mma<F, kKs2, F::kPlanes, kAheadHid>(enter(), H2, lane);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing reloads
     __builtin_amdgcn_s_barrier();                      // every wave is done with the ring
 

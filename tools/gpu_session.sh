@@ -148,7 +148,12 @@ for step in "$@"; do
         run c4ab_${pl}_$i 300 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 --only --pipeline $pl
       done; done ;;
     abl32) bash tools/ablate_policy32.sh || exit 1 ;;  # k_act32 timing ablations (BUILD=1 here first)
-    chains) run step_chains 300 python3 tools/bench_step_chains.py ;;  # step mode as 1/2/4 independent chains
+    chains) run step_chains 300 python3 tools/bench_step_chains.py ;;
+    polab)  # the fp32 actor: staged epilogue (product) vs after each tile (ablate/lib_nopipe.so), alternating
+      for i in 1 2; do
+        run pol_pipe_$i 200 python tools/bench_policy.py --fused-only --iters 30
+        SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_nopipe.so run pol_nopipe_$i 200 python tools/bench_policy.py --fused-only --iters 30
+      done ;;  # step mode as 1/2/4 independent chains
     polprec) run pytest_polprec 600 python -u -m pytest tests/test_gpu_policy.py tests/test_gpu_opponent_pool.py \
                  tests/test_gpu_compact_obs.py -x -v -s --timeout 300 --timeout-method thread
              grep -h "precision_vs_float64" $O/pytest_polprec_$TAG.out > $O/precision_vs_float64_$TAG.txt || true ;;
