@@ -311,9 +311,12 @@ def _rel_err(got, ref):
 def test_exact_format_error_against_float64(weights):
     """at config 5's per-GPU size (65 536 tables), the logits and values of both fp32
     formats against a float64 evaluation of the same module (the exact answer), next to torch fp32's own
-    error.  The exact format (three bf16 planes) must be no worse than the fp16-plane format and within
-    a small multiple of torch fp32; its greedy actions differ from torch fp32's only at near ties.  The
-    measured errors are printed (tools/gpu_session.sh keeps the output under profiles/)."""
+    error.  Both must stay within twice torch fp32's own error (the end-to-end error of either format is
+    the fp32 rounding of the sums, which the exact format's six products per k-step round as often as
+    the fp16-plane format's three or more: its max error is NOT smaller — round 5's first measurement:
+    4.7e-7 exact, 3.0e-7 fp16 planes, 5.4e-7 torch fp32 itself, random-init weights); greedy actions
+    differ from torch fp32's only at near ties.  The measured errors are printed
+    (tools/gpu_session.sh keeps the output under profiles/)."""
     import copy
     import json
     import torch
@@ -337,7 +340,8 @@ def test_exact_format_error_against_float64(weights):
                       "greedy_differs_outside_near_ties": int((act[clear] != want[clear]).sum().item())}
     errs["near_tie_fraction"] = 1.0 - clear.float().mean().item()
     print("precision_vs_float64", json.dumps({"weights": str(weights), "tables": n, **errs}))
-    ex, h2, t32 = errs["fp32"], errs["fp32_f16x2"], errs["torch_fp32"]
-    assert ex["greedy_differs_outside_near_ties"] == 0
-    assert ex["logits"] <= h2["logits"] and ex["value"] <= h2["value"] * 1.0001, errs
-    assert ex["logits"] <= 4 * t32["logits"] + 1e-7 and ex["value"] <= 4 * t32["value"] + 1e-7, errs
+    t32 = errs["torch_fp32"]
+    for prec in FP32_FORMS:
+        e = errs[prec]
+        assert e["greedy_differs_outside_near_ties"] == 0, (prec, errs)
+        assert e["logits"] <= 2 * t32["logits"] + 1e-7 and e["value"] <= 2 * t32["value"] + 1e-7, (prec, errs)

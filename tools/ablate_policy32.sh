@@ -6,11 +6,12 @@
 set -o pipefail
 D=splendor-gym_amd/ablate
 C=splendor-gym_amd/csrc
-VARIANTS=${VARIANTS:-"full:0 notanh:1 noring:2 noafrd:4 mfma_only:7"}
+VARIANTS=${VARIANTS:-"full:0 notanh:1 noring:2 noafrd:4 noring_notanh:3 mfma_only:7"}
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950"
 if [ "${BUILD:-0}" = "1" ]; then
   mkdir -p $D/obj
   for s in spl_engine spl_policy spl_dual; do
+    if [ $C/obj/$s.o -nt $C/$s.hip ]; then cp $C/obj/$s.o $D/obj/$s.o; fi  # the product build's objects (csrc/Makefile)
     [ $D/obj/$s.o -nt $C/$s.hip ] || /opt/rocm/bin/hipcc $F -c -o $D/obj/$s.o $C/$s.hip || exit 1
   done
   for v in $VARIANTS; do

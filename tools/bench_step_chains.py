@@ -22,7 +22,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "splendor-gym_amd"))
 
 
-def run(T, C, G, replays, warm, seed=0):
+def run(T, C, G, replays, warm, seed=0, eager=False):
     import torch
     from splendor_gym import _native
     from splendor_gym.device import Engine
@@ -61,6 +61,40 @@ def run(T, C, G, replays, warm, seed=0):
     # eager warm-up on the capture streams' pattern, then capture
     issue([main] * C, G)
     torch.cuda.synchronize(dev)
+    if eager:  # eager launches, chain c on stream c, issued step by step across the chains
+        strms = [main] + side
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ends = [torch.cuda.Event() for _ in strms]
+        per = []
+        for rep in range(warm + replays):
+            ev0.record(main)
+            for s_ in side:
+                s_.wait_event(ev0)
+            for k in range(G):
+                for c, ch in enumerate(chains):
+                    e = ch["eng"]
+                    sa = ch["args"][k & 1]
+                    sa.ply = k + 1
+                    _native.check(e.lib, e.lib.spl_step(e.ctx, ctypes.byref(e.desc), ctypes.byref(sa),
+                                                        ctypes.c_void_p(strms[c].cuda_stream)))
+            for c, ch in enumerate(chains):
+                with torch.cuda.stream(strms[c]):
+                    ch["ply_base"].add_(G)
+            for s_, en in zip(side, ends[1:]):
+                en.record(s_)
+                main.wait_event(en)
+            ev1.record(main)
+            torch.cuda.synchronize(dev)
+            if rep >= warm:
+                per.append(ev0.elapsed_time(ev1) * 1e3 / G)
+        per.sort()
+        errs = _native.F_OOB | _native.F_AFTER_TERMINAL | _native.F_RNG_LIMIT | _native.F_FAULT
+        bad = sum(int(((ch["eng"].flags & errs) != 0).sum().item()) for ch in chains)
+        for ch in chains:
+            ch["eng"].close()
+        return {"tables": T, "chains": C, "mode": "eager", "tables_per_chain": n, "steps": G, "reps": replays,
+                "us_per_env_step": {"min": round(per[0], 3), "median": round(per[len(per) // 2], 3), "max": round(per[-1], 3)},
+                "env_steps_per_s": round(T / (per[len(per) // 2] * 1e-6), 1), "error_flags": bad}
     g = torch.cuda.CUDAGraph()
     cap = torch.cuda.Stream(device=dev)
     cap.wait_stream(main)
@@ -104,10 +138,11 @@ def main():
     ap.add_argument("--replays", type=int, default=8)
     ap.add_argument("--warm", type=int, default=2)
     ap.add_argument("--rounds", type=int, default=2, help="alternate the chain counts this many times")
+    ap.add_argument("--eager", action="store_true", help="eager launches on C streams instead of one hipGraph")
     a = ap.parse_args()
     for r in range(a.rounds):
         for C in [int(x) for x in a.chains.split(",")]:
-            print(json.dumps(dict(run(a.tables, C, a.graph_steps, a.replays, a.warm), round=r)), flush=True)
+            print(json.dumps(dict(run(a.tables, C, a.graph_steps, a.replays, a.warm, eager=a.eager), round=r)), flush=True)
 
 
 if __name__ == "__main__":

@@ -149,6 +149,7 @@ for step in "$@"; do
       done; done ;;
     abl32) bash tools/ablate_policy32.sh || exit 1 ;;  # k_act32 timing ablations (BUILD=1 here first)
     chains) run step_chains 300 python3 tools/bench_step_chains.py ;;
+    chainse) run step_chains_eager 300 python3 tools/bench_step_chains.py --eager ;;
     polab)  # the fp32 actor: staged epilogue (product) vs after each tile (ablate/lib_nopipe.so), alternating
       for i in 1 2; do
         run pol_pipe_$i 200 python tools/bench_policy.py --fused-only --iters 30
