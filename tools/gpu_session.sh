@@ -150,6 +150,14 @@ for step in "$@"; do
     abl32) bash tools/ablate_policy32.sh || exit 1 ;;  # k_act32 timing ablations (BUILD=1 here first)
     chains) run step_chains 300 python3 tools/bench_step_chains.py ;;
     chainse) run step_chains_eager 300 python3 tools/bench_step_chains.py --eager ;;
+    polab2)  # the fp32 actor's weight ring: LDS-DMA (product) vs VGPR-staged (lib_ringv*), hidden A prefetch 2 vs 1
+      for i in 1 2; do
+        run pol_full_$i 200 python tools/bench_policy.py --fused-only --iters 30
+        for v in ringv ringv_d1 d1; do
+          SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_$v.so run pol_${v}_$i 200 python tools/bench_policy.py --fused-only --iters 30
+        done
+      done
+      for f in $O/pol_*_[12]_$TAG.out; do echo "$f $(cut -c1-120 $f)"; done ;;
     polab)  # the fp32 actor: staged epilogue (product) vs after each tile (ablate/lib_nopipe.so), alternating
       for i in 1 2; do
         run pol_pipe_$i 200 python tools/bench_policy.py --fused-only --iters 30
