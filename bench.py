@@ -540,7 +540,7 @@ def main():
     ap.add_argument("--refill", choices=("fused", "separate"), default="fused",
                     help="rollout mode: due pool refills run inside the spl_rollout launch (fused) or as a "
                          "spl_refill launch after it (step mode always launches spl_refill)")
-    ap.add_argument("--pipeline", choices=("auto", "always", "half", "off", "dealer", "dealer2"), default="auto",
+    ap.add_argument("--pipeline", choices=("auto", "always", "half", "off", "dealer", "dealer2", "quad"), default="auto",
                     help="rollout mode: two-wave pipelined kernel (auto: 32 or 64 tables per workgroup by grid "
                          "size; always: 64; half: 32) vs one wave per 64 tables (off)")
     ap.add_argument("--sp-tables", type=int, default=65536,
@@ -589,7 +589,7 @@ def main():
     RK = args.rollout_k
     table0 = rank * T
     pipe = {"auto": True, "always": "always", "half": "half", "off": False, "dealer": "dealer",
-            "dealer2": "dealer2"}[args.pipeline]
+            "dealer2": "dealer2", "quad": "quad"}[args.pipeline]
     eng = Engine(T, P, device=dev, refill_period=R, table0=table0, refill_fused=args.refill == "fused",
                  pipeline=pipe, delegation=args.delegation, partner_lead=args.partner_lead)
     eng.reset(seeds=range(table0, table0 + T))

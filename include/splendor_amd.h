@@ -145,7 +145,9 @@ int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused);
  * 32 768 tables), else the three-wave dealer variant (4: a third wave deals the pool refills beside the
  * other two) when it fits, else two-wave at 64 tables per workgroup; 2 = two-wave at 64; 3 = two-wave
  * at 32; 4 = the three-wave dealer variant; 5 = the six-wave dealer variant (two dealer teams per
- * 128-table workgroup, roles given to waves by the SIMD they run on).
+ * 128-table workgroup, roles given to waves by the SIMD they run on); 6 = the quad variant (four
+ * two-wave teams per 256-table workgroup, one workgroup per CU, roles by SIMD; the partner hand-off
+ * of spl_ctx_set_partner_lead runs in it).
  * Results are identical in every mode. */
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
 /* spl_rollout with per_step_outputs at 64 tables per workgroup only: rollout-store delegation.  On

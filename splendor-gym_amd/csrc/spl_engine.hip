@@ -1898,12 +1898,14 @@ struct RefillSlots {
     int seg, count, off;
     __device__ __forceinline__ bool due(int k) const { return count > 0 && k < seg * count && k % seg == off; }
 };
-__device__ __forceinline__ RefillSlots refill_slots(int K, int count) {
+// `key` staggers the refill step per workgroup (per team in the multi-team kernels); results do not
+// depend on the schedule
+__device__ __forceinline__ RefillSlots refill_slots(int K, int count, uint32_t key = blockIdx.x) {
     RefillSlots r{1, 0, 0};
     if (count > 0) {
         r.count = min(count, K);
         r.seg = K / r.count;
-        r.off = (int)(((blockIdx.x * 0x9E3779B1u) >> 16) % (uint32_t)r.seg);
+        r.off = (int)(((key * 0x9E3779B1u) >> 16) % (uint32_t)r.seg);
     }
     return r;
 }
@@ -2704,7 +2706,8 @@ __device__ __forceinline__ bool dealer_step(DealerLDS &D, Tab<P> &T, const KAren
 struct WaveRole {
     int role, block;
 };
-template <int P, int TPW, bool kStore, bool kDealer = false, class LdsT = WsLDS<P>>
+// kTeams: 64-table teams per workgroup (the six-wave dealer 2, the quad kernel 4; one workgroup per CU)
+template <int P, int TPW, bool kStore, bool kDealer = false, class LdsT = WsLDS<P>, int kTeams = 1>
 __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep S, int K, int refill,
                                            int deleg_every, WaveRole wr = WaveRole{-1, -1}) {
     static_assert(TPW == 64 || TPW == 32, "64 or 32 tables per workgroup");
@@ -2715,7 +2718,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
     const int role = wr.role >= 0 ? wr.role : (int)(threadIdx.x >> 6);
     const bool rules_wave = role == 0;
     // delegation pairs neighbouring workgroups (blockIdx b and b + 1 on adjacent XCCs): identity map
-    const bool deleg_shape = TPW == 64 && kStore && !kDealer && deleg_every >= 4;
+    const bool deleg_shape = TPW == 64 && kStore && !kDealer && kTeams == 1 && deleg_every >= 4;
     const int t0 = (wr.block >= 0 ? wr.block : (deleg_shape ? (int)blockIdx.x : wg_block())) * TPW;
     const int t = t0 + lane;
     const bool valid = lane < TPW && t < A.n;
@@ -2727,18 +2730,19 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             L.dl.dreq = L.dl.ddone = L.dl.rdone = L.dl.odone = L.dl.stop = L.dl.abort = 0u;
         }
     }
-    // partner hand-off (per-step outputs, 64 tables per team; see PartnerLink): the six-wave dealer
-    // only (one workgroup per CU; round 5: not in the two-wave kernels), which passes the lead in steps
-    // as deleg_every (0 = off, -1 = forced).  Team j of workgroups b and b ^ 1, both full, K < 2^14
-    // (the step fits a flag).
+    // partner hand-off (per-step outputs, 64 tables per team; see PartnerLink): the multi-team kernels
+    // only — one workgroup per CU, the guide's first measured row (the six-wave dealer and, round 5, the
+    // quad kernel; not the two-wave kernel at four workgroups per CU), which pass the lead in steps as
+    // deleg_every (0 = off, -1 = forced).  Team j of workgroups b and b ^ 1, both full, K < 2^14 (the
+    // step fits a flag).
     PartnerLink pl{false, 0, 0, 0u, nullptr, nullptr, 0};
-    if constexpr (kStore && kDealer) {
+    if constexpr (kStore && kTeams > 1) {
         const int lead = wr.block >= 0 ? deleg_every : 0;
         if (lead != 0 && K < (1 << 14)) {
             const uint32_t b = blockIdx.x, pb = b ^ 1u;
-            const int team = wr.block - 2 * wg_block();
-            const int t0p = (2 * wg_block_of(pb) + team) * 64;
-            const int pair = (int)(b >> 1) * 2 + team;
+            const int team = wr.block - kTeams * wg_block();
+            const int t0p = (kTeams * wg_block_of(pb) + team) * 64;
+            const int pair = (int)(b >> 1) * kTeams + team;
             if (pb < gridDim.x && t0 + 64 <= A.n && t0p + 64 <= A.n && pair < A.n / 128) {
                 pl.on = true;
                 pl.lead = lead;
@@ -2782,7 +2786,8 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         }
     }
     if (rules_wave) {
-        const RefillSlots rs = refill_slots(K, (S.autoreset && !kDealer) ? refill : 0);
+        const RefillSlots rs = refill_slots(K, (S.autoreset && !kDealer) ? refill : 0,
+                                            wr.block >= 0 ? (uint32_t)wr.block : blockIdx.x);
         // dealer bookkeeping (per lane): slots whose deal is in flight (valid while a batch is
         // outstanding) and whether `pool` still lacks the next record's words
         uint32_t my_req = 0, infl = 0;
@@ -2802,6 +2807,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         bool pool_dirty = false;
         const uint64_t ply0 = S.ply + (S.ply_base ? *S.ply_base : 0ull);
         uint64_t cur_mask = 0ull;
+        uint32_t pv[3] = {0u, 0u, 0u}, pps = 0u, pcs = 0u;  // quad kernel's partner poller (loaded a step ahead)
         const uint64_t below = (1ull << lane) - 1ull;
 #ifdef SPL_STAMPS
         int rst_lo[kWsStamps] = {0}, rst_hi[kWsStamps] = {0};
@@ -2869,6 +2875,18 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             if constexpr (kDealer) {
                 lds_publish(&L.dl.rdone, (uint32_t)(k + 1));  // hand-off of step k
             } else {
+                if (pl.on) {  // the quad kernel's partner poller (the rules wave issues no row stores): the
+                              // words loaded last step go to the output wave's snapshots, then new loads
+                    if (k > 0)
+                        pt_publish(L.pt, (uint32_t)__builtin_amdgcn_readfirstlane(pv[0]),
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(pv[1]), pps,
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(pv[2]), pcs);
+                    pps = lds_poll(&L.pt.seq[0]);
+                    pcs = lds_poll(&L.pt.seq[1]);
+                    pv[0] = flag_load(pl.line(pt_progress_line(pl.side ^ 1)));
+                    pv[1] = flag_load(pl.line(pt_ready_line(pl.side * kPartnerSlots + (int)(pps % kPartnerSlots))));
+                    pv[2] = flag_load(pl.line(pt_ready_line((pl.side ^ 1) * kPartnerSlots + (int)(pcs % kPartnerSlots))));
+                }
                 ws_sync();  // hand-off of step k
             }
             WSSTAMP(3, k);
@@ -3241,7 +3259,8 @@ __device__ __forceinline__ void rollout_dealer2(WsDeal2LDS<P> &L, KArena A, KTab
     for (int i = 0; i < 6; ++i) simd[i] = __builtin_amdgcn_readfirstlane(L.simd[i]);
     const int code = __builtin_amdgcn_readfirstlane(dealer2_assign(simd, w));
     const int team = code / 3;
-    rollout_ws<P, 64, kStore, true>(L.team[team], A, Tb, S, K, refill, lead, WaveRole{code % 3, 2 * wg_block() + team});
+    rollout_ws<P, 64, kStore, true, WsDealLDS<P>, 2>(L.team[team], A, Tb, S, K, refill, lead,
+                                                      WaveRole{code % 3, 2 * wg_block() + team});
 }
 template <int P, bool kStore>
 struct RolloutDealer2Kernel;
@@ -3261,6 +3280,99 @@ SPL_DEALER2_KERNEL(k_rollout_inplace_dealer2_2p, 2, false)
 SPL_DEALER2_KERNEL(k_rollout_inplace_dealer2_3p, 3, false)
 SPL_DEALER2_KERNEL(k_rollout_inplace_dealer2_4p, 4, false)
 #undef SPL_DEALER2_KERNEL
+
+// The quad variant (round 5; k_rollout_*_quad_<P>p, 256 tables per workgroup, one workgroup per CU):
+// four two-wave teams (rules + output wave, 64 tables each) in ONE 512-thread workgroup — the
+// headline's 65 536 tables in 256 workgroups, all resident.  At one workgroup per CU the partner
+// hand-off (PartnerLink; the rules wave polls the pair's flag words, as it did in round 4's two-wave
+// kernel) is a hand-off of the guide's first measured row ("hipMalloc; one per CU", 4-byte sc1 stores
+// and loads, one signalling lane per storing wave after its vmcnt(0)), which the two-wave kernel at
+// four workgroups per CU was not.  Roles by SIMD as in the six-wave dealer: every
+// wave reads its SIMD, and the rules waves go to distinct SIMDs (each SIMD: one rules + one output
+// wave).  Each team is rollout_ws on its own LDS quarter; results are those of every other shape.
+template <int P>
+struct __align__(16) WsQuadLDS {
+    WsLDS<P> team[4];
+    uint32_t simd[8];
+};
+static_assert(sizeof(WsQuadLDS<2>) <= 163840 && sizeof(WsQuadLDS<3>) <= 163840 && sizeof(WsQuadLDS<4>) <= 163840,
+              "the quad rollout needs one workgroup per CU");
+
+// wave-uniform: (team * 2 + role) of wave w given the eight waves' SIMDs (dealer2_assign's rule for two
+// roles of four waves each: waves in the order (occupancy of their SIMD, index), rules first on distinct
+// SIMDs, then output).  Static indexing only.
+__device__ __forceinline__ int quad_assign(const uint32_t (&simd)[8], int w) {
+    int key[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        int occ = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) occ += simd[j] == simd[i] ? 1 : 0;
+        key[i] = occ * 8 + i;
+    }
+    int rank[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r += key[j] < key[i] ? 1 : 0;
+        rank[i] = r;
+    }
+    int code[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+#pragma unroll
+    for (int role = 0; role < 2; ++role) {
+        uint32_t used = 0u;
+        int got = 0;
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass)
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const bool take = rank[i] == r && got < 4 && code[i] < 0 &&
+                                      (pass == 1 || ((used >> (simd[i] & 3u)) & 1u) == 0u);
+                    code[i] = take ? got * 2 + role : code[i];
+                    used |= take ? 1u << (simd[i] & 3u) : 0u;
+                    got += take ? 1 : 0;
+                }
+    }
+    int mine = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mine = i == w ? code[i] : mine;
+    return mine;
+}
+
+template <int P, bool kStore>
+__device__ __forceinline__ void rollout_quad(WsQuadLDS<P> &L, KArena A, KTables Tb, KStep S, int K, int refill, int lead) {
+    const int w = (int)(threadIdx.x >> 6);
+    if (lane_id() == 0) L.simd[w] = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;
+    __syncthreads();
+    uint32_t simd[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) simd[i] = __builtin_amdgcn_readfirstlane(L.simd[i]);
+    const int code = __builtin_amdgcn_readfirstlane(quad_assign(simd, w));
+    const int team = code >> 1;
+    rollout_ws<P, 64, kStore, false, WsLDS<P>, 4>(L.team[team], A, Tb, S, K, refill, lead,
+                                                  WaveRole{code & 1, 4 * wg_block() + team});
+}
+template <int P, bool kStore>
+struct RolloutQuadKernel;
+#define SPL_QUAD_KERNEL(NAME, P_, ST_)                                                                         \
+    __global__ __launch_bounds__(512) void NAME(KArena A, KTables Tb, KStep S, int K, int refill, int deleg) { \
+        __shared__ WsQuadLDS<P_> L;                                                                            \
+        rollout_quad<P_, ST_>(L, A, Tb, S, K, refill, deleg);                                                  \
+    }                                                                                                          \
+    template <>                                                                                                \
+    struct RolloutQuadKernel<P_, ST_> {                                                                        \
+        static constexpr void (*fn)(KArena, KTables, KStep, int, int, int) = NAME;                             \
+    };
+SPL_QUAD_KERNEL(k_rollout_store_quad_2p, 2, true)
+SPL_QUAD_KERNEL(k_rollout_store_quad_3p, 3, true)
+SPL_QUAD_KERNEL(k_rollout_store_quad_4p, 4, true)
+SPL_QUAD_KERNEL(k_rollout_inplace_quad_2p, 2, false)
+SPL_QUAD_KERNEL(k_rollout_inplace_quad_3p, 3, false)
+SPL_QUAD_KERNEL(k_rollout_inplace_quad_4p, 4, false)
+#undef SPL_QUAD_KERNEL
 
 // Explicit reset (SplendorEnv.reset / VectorEnv.reset), then observation + mask of all tables.
 template <int P>
@@ -3560,6 +3672,7 @@ struct spl_ctx_s {
     int ws_resident[5];  // k_rollout_store_<P>p: workgroups resident per device (occupancy x CUs), index P
     int dealer_resident[5];  // k_rollout_store_dealer_<P>p: the same for the three-wave dealer variant
     int dealer2_resident[5]; // k_rollout_store_dealer2_<P>p: the same for the six-wave dealer variant
+    int quad_resident[5];    // k_rollout_store_quad_<P>p: the same for the quad variant
     int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
     int partner_lead;    // six-wave dealer per-step store: partner hand-off lead in steps (0 off, < 0 forced)
     uint64_t *fault_host;  // host-mapped, fine-grained: the serial of a launch that faulted (0 = none), spl_ctx_faults
@@ -3721,7 +3834,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         memcpy(&nrec[i], b, 8);
     }
     HIP_TRY(hipSetDevice(device));
-    int ws_resident[5], dealer_resident[5], dealer2_resident[5];
+    int ws_resident[5], dealer_resident[5], dealer2_resident[5], quad_resident[5];
     {
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -3740,6 +3853,11 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&d2occ[3], RolloutDealer2Kernel<3, true>::fn, 384, 0));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&d2occ[4], RolloutDealer2Kernel<4, true>::fn, 384, 0));
         for (int q = 0; q < 5; ++q) dealer2_resident[q] = d2occ[q] * cus;
+        int qocc[5] = {0, 0, 0, 0, 0};
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&qocc[2], RolloutQuadKernel<2, true>::fn, 512, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&qocc[3], RolloutQuadKernel<3, true>::fn, 512, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&qocc[4], RolloutQuadKernel<4, true>::fn, 512, 0));
+        for (int q = 0; q < 5; ++q) quad_resident[q] = qocc[q] * cus;
     }
     spl_ctx_t *c = new spl_ctx_t();
     c->device = device;
@@ -3751,6 +3869,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     memcpy(c->ws_resident, ws_resident, sizeof(ws_resident));
     memcpy(c->dealer_resident, dealer_resident, sizeof(dealer_resident));
     memcpy(c->dealer2_resident, dealer2_resident, sizeof(dealer2_resident));
+    memcpy(c->quad_resident, quad_resident, sizeof(quad_resident));
     if (hipMalloc(&c->cards, sizeof(uint4) * 90) != hipSuccess || hipMalloc(&c->nobles, sizeof(uint2) * 10) != hipSuccess ||
         hipMalloc(&c->lut, sizeof(uint4) * kLutEntries) != hipSuccess) {
         spl_ctx_destroy(c);
@@ -3814,7 +3933,7 @@ int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period) {
 
 int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on) {
     if (!ctx) return fail(SPL_E_ARG, "null ctx");
-    if (on < 0 || on > 5) return fail(SPL_E_ARG, "rollout pipeline must be 0..5");
+    if (on < 0 || on > 6) return fail(SPL_E_ARG, "rollout pipeline must be 0..6");
     ctx->pipeline = on;
     return SPL_OK;
 }
@@ -3991,12 +4110,13 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
 // per CU, e.g. C4's 32 768 tables per GPU: 1 120-1 137 against 1 166-1 172 us per 128-step launch
 // for the three-wave one, alternating on one box, profiles/r04/c4ab_r04b.txt), else the three-wave
 // one when it fits, else two waves at 64 tables per workgroup.
-constexpr int kDealerShape = -1, kDealer2Shape = -2;
+constexpr int kDealerShape = -1, kDealer2Shape = -2, kQuadShape = -3;
 static int rollout_tpw(const spl_ctx_t *ctx, int32_t n, int32_t players) {
     if (ctx->pipeline == 2) return 64;
     if (ctx->pipeline == 3) return 32;
     if (ctx->pipeline == 4) return kDealerShape;
     if (ctx->pipeline == 5) return kDealer2Shape;
+    if (ctx->pipeline == 6) return kQuadShape;
     if (ctx->pipeline == 1) {  // auto: the six-wave dealer (SIMD-aware roles, -3.5 % on C4's share), else three-wave
         if ((int64_t)((n + 127) / 128) <= ctx->dealer2_resident[players]) return kDealer2Shape;
         return (int64_t)blocks_for(n) <= ctx->dealer_resident[players] ? kDealerShape : 64;
@@ -4017,6 +4137,9 @@ const char *spl_rollout_kernel_name(spl_ctx_t *ctx, int32_t n, int32_t players, 
     static const char *const dealer2[2][3] = {
         {"k_rollout_inplace_dealer2_2p", "k_rollout_inplace_dealer2_3p", "k_rollout_inplace_dealer2_4p"},
         {"k_rollout_store_dealer2_2p", "k_rollout_store_dealer2_3p", "k_rollout_store_dealer2_4p"}};
+    static const char *const quad[2][3] = {
+        {"k_rollout_inplace_quad_2p", "k_rollout_inplace_quad_3p", "k_rollout_inplace_quad_4p"},
+        {"k_rollout_store_quad_2p", "k_rollout_store_quad_3p", "k_rollout_store_quad_4p"}};
     if (!ctx || n <= 0 || players < 2 || players > 4) {
         fail(SPL_E_ARG, "spl_rollout_kernel_name: bad arguments");
         return nullptr;
@@ -4025,6 +4148,7 @@ const char *spl_rollout_kernel_name(spl_ctx_t *ctx, int32_t n, int32_t players, 
     if (tpw == 0) return one_wave[players - 2];
     if (tpw == kDealerShape) return dealer[per_step_outputs ? 1 : 0][players - 2];
     if (tpw == kDealer2Shape) return dealer2[per_step_outputs ? 1 : 0][players - 2];
+    if (tpw == kQuadShape) return quad[per_step_outputs ? 1 : 0][players - 2];
     return names[per_step_outputs ? 1 : 0][tpw == 32 ? 1 : 0][players - 2];
 }
 
@@ -4059,6 +4183,7 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     // the six-wave dealer's partner lead, likewise 0 unless every workgroup is resident (ADVICE r04:
     // pipeline "dealer2" forced on a larger grid)
     const int lead2 = (int64_t)((arena->n + 127) / 128) <= ctx->dealer2_resident[arena->players] ? ctx->partner_lead : 0;
+    const int lead4 = (int64_t)((arena->n + 255) / 256) <= ctx->quad_resident[arena->players] ? ctx->partner_lead : 0;
 #define SPL_LAUNCH_WS(TPW, BLOCKS)                                                                           \
     DISPATCH_P(arena->players, if (p_out) {                                                                  \
         hipLaunchKernelGGL((RolloutKernel<PP, TPW, true>::fn), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
@@ -4067,7 +4192,16 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
         hipLaunchKernelGGL((RolloutKernel<PP, TPW, false>::fn), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
                            (int)steps, fused, 0);                                                            \
     })
-    if (tpw == kDealer2Shape) {
+    if (tpw == kQuadShape) {
+        const unsigned blocks = (unsigned)((arena->n + 255) / 256);
+        DISPATCH_P(arena->players, if (p_out) {
+            hipLaunchKernelGGL((RolloutQuadKernel<PP, true>::fn), dim3(blocks), dim3(512), 0, s, A, ktables(ctx), S,
+                               (int)steps, fused, lead4);
+        } else {
+            hipLaunchKernelGGL((RolloutQuadKernel<PP, false>::fn), dim3(blocks), dim3(512), 0, s, A, ktables(ctx), S,
+                               (int)steps, fused, 0);
+        })
+    } else if (tpw == kDealer2Shape) {
         const unsigned blocks = (unsigned)((arena->n + 127) / 128);
         DISPATCH_P(arena->players, if (p_out) {
             hipLaunchKernelGGL((RolloutDealer2Kernel<PP, true>::fn), dim3(blocks), dim3(384), 0, s, A, ktables(ctx), S,

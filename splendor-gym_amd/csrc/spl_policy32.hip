@@ -49,8 +49,15 @@
 #ifndef SPL_P32_RINGV
 #define SPL_P32_RINGV 0
 #endif
+// SPL_P32_GROUP 2 (default): one ring barrier per two chunks (four slots: two in use, two loading);
+// exact k_act32<true, true> 215.8 -> 206 us, alternating on one box (profiles/r05/pol_ring_ab_r05g.txt;
+// without any barrier, a racing timing build, 195 us: the barriers cost ~20 us, half of it recovered)
+#ifndef SPL_P32_GROUP
+#define SPL_P32_GROUP 2
+#endif
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
-// streaming, no per-tile barrier), 4 A fragments loaded once per tile (no per-group LDS reads)
+// streaming, no per-tile barrier), 4 A fragments loaded once per tile (no per-group LDS reads),
+// 16 the ring without its per-chunk barrier (waves race the slots)
 #ifndef SPL_POL_ABL
 #define SPL_POL_ABL 0
 #endif
@@ -89,7 +96,7 @@ struct FmtF16x2 {   // SPL_PREC_FP32_F16X2: 22 significant bits in two fp16 plan
     static constexpr int kPlanes = 2;
     static constexpr int kActScaleExp = 10;  // hidden activations enter the next layer as tanh * 2^10
     static constexpr int kRowMaxExp = 10;    // a weight row's largest |w| is scaled into [2^9, 2^10)
-    static constexpr int kSlots = 5;         // ring slots of 21 KB (4 chunks in flight)
+    static constexpr int kSlots = SPL_P32_GROUP == 2 ? 4 : 5;  // ring slots of 21 KB (4 chunks in flight)
     static constexpr bool kExact = false;
 };
 
@@ -719,7 +726,11 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     uint8_t *ms = lds + G::kLdsMask + wave * kMaskWave;
     const __amdgpu_buffer_rsrc_t wrs = image_rsrc(W);
 
-#if SPL_P32_RINGV
+#if SPL_P32_GROUP == 2
+    static_assert(kSlots == 4, "two chunks per barrier: four slots");
+    issue_chunk<F>(wrs, 0, ring, wave, lane);
+    issue_chunk<F>(wrs, 1, ring + kChunk, wave, lane);
+#elif SPL_P32_RINGV
     // VGPR-staged ring (SPL_P32_RINGV): chunks 0 .. S-3 by LDS-DMA, chunk S-2 into this wave's staging
     // registers; enter(c) writes the staged chunk c+S-2 into its slot and loads chunk c+S-1
     u32x4 stg[G::kBlocksPerWave];
@@ -774,7 +785,19 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
         }
         return ring;
 #endif
-#if SPL_P32_RINGV
+#if SPL_P32_GROUP == 2
+        // two chunks per barrier: on even c, wait for this wave's pieces of chunks c, c+1 (issued two tiles
+        // ago), barrier (everyone's landed; everyone is done with c-2, c-1), then issue c+2, c+3 into their
+        // slots; odd c just moves on to the next slot
+        if ((c & 1) == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int j = 2; j < 4; ++j)
+                if (c + j < kTotal) issue_chunk<F>(wrs, c + j, ring + ((c + j) % kSlots) * kChunk, wave, lane);
+        }
+#elif SPL_P32_RINGV
         // the staged chunk c+S-2 (loaded one tile ago) -> its slot, which held chunk c-2 (every wave was
         // done with it at the previous barrier); then, behind this barrier, chunk c is complete (written
         // S-2 tiles ago, or by the prologue's LDS-DMA) and every wave is done with chunk c-1
@@ -788,7 +811,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
         // this wave's part of chunk c landed (later chunks' loads may stay outstanding)
         if (wave < G::kChunkBlocks - (G::kBlocksPerWave - 1) * kWaves) __builtin_amdgcn_s_waitcnt(vmcnt_imm(G::kWaitMost));
         else __builtin_amdgcn_s_waitcnt(vmcnt_imm(G::kWaitLast));
-        __builtin_amdgcn_s_barrier();  // everyone's part landed; slot c-1 is free
+        if (!(SPL_POL_ABL & 16)) __builtin_amdgcn_s_barrier();  // everyone's part landed; slot c-1 is free
         asm volatile("" ::: "memory");
         const int nxt = c + kSlots - 1 < kTotal ? c + kSlots - 1 : kTotal - 1;  // past the end: harmless reload
         issue_chunk<F>(wrs, nxt, ring + ((c + kSlots - 1) % kSlots) * kChunk, wave, lane);

@@ -24,8 +24,9 @@ class Engine:
     pipeline: rollout() kernel choice, same results in every mode: True = auto (the three-wave dealer
               variant for grids of at most two workgroups per CU, else two-wave at 64 tables per
               workgroup); "always" / "half" = two-wave at 64 / 32 tables per workgroup; "dealer" = the
-              dealer variant; "dealer2" = the six-wave dealer variant (SIMD-aware roles); False = one
-              wave per 64 tables.
+              dealer variant; "dealer2" = the six-wave dealer variant (SIMD-aware roles); "quad" = four
+              two-wave teams per workgroup, one workgroup per CU (SIMD-aware roles, partner hand-off);
+              False = one wave per 64 tables.
     """
 
     # pool refill period by player count (three pool deals per table cover the resets in between;
@@ -98,7 +99,7 @@ class Engine:
         # rollout(): a due refill runs inside the rollout launch (True) or as a refill launch after it
         check(self.lib, self.lib.spl_ctx_set_refill_fused(self.ctx, 1 if refill_fused else 0))
         # rollout(): two-wave pipelined kernel or one wave per 64 tables; same results
-        pipe = {"always": 2, "half": 3, "dealer": 4, "dealer2": 5}.get(pipeline, 1 if pipeline else 0)
+        pipe = {"always": 2, "half": 3, "dealer": 4, "dealer2": 5, "quad": 6}.get(pipeline, 1 if pipeline else 0)
         check(self.lib, self.lib.spl_ctx_set_rollout_pipeline(self.ctx, pipe))
         # rollout() into a per-step store: every n-th step the odd-XCC workgroups' rows are stored by
         # their even-XCC partners (None = the library default, 0 = off); same results

@@ -39,7 +39,8 @@ def store(K, n, dev):
             "final_obs": torch.zeros((K, n, 297), dtype=torch.int32, device=dev)}
 
 
-@pytest.mark.parametrize("P,n,R,lead,pipeline", [(2, 65536, 64, None, True), (2, 65536, 64, -1, True),
+@pytest.mark.parametrize("P,n,R,lead,pipeline", [(2, 65536, 64, None, True), (2, 65536, 64, -1, "always"),
+                                                 (2, 65536, 64, None, "quad"), (2, 65536, 64, -1, "quad"),
                                                  (4, 32768, 16, None, True), (4, 32768, 16, -1, True),
                                                  (2, 32768, 64, -1, "dealer2")])
 def test_headline_rollout_65536_equals_step_chain_and_oracle(P, n, R, lead, pipeline):
@@ -47,17 +48,21 @@ def test_headline_rollout_65536_equals_step_chain_and_oracle(P, n, R, lead, pipe
     CU, fused refills) and C4's per-GPU share (4p x 32 768 of 262 144 on 8 GPUs: the six-wave dealer,
     one workgroup per CU) at full size: two 128-step rollout launches equal the spl_step chain bit for
     bit; every 256th table is replayed through the CPU oracle.  lead -1 forces the partner hand-off
-    whenever a task slot is free: the six-wave dealer then hands rows between
-    every pair of workgroups with the most slot reuse its ring allows (also 2p x 32 768 on it), and the
-    two-wave headline kernel, which has no partner hand-off since round 5, must hand off nothing."""
+    whenever a task slot is free: the six-wave dealer and the quad kernel (one
+    workgroup per CU, 4 teams: the headline's 65 536 tables in 256 workgroups) then hand rows between
+    every pair of workgroups with the most slot reuse their rings allow (dealer2 also at 2p x 32 768),
+    and the two-wave kernel ("always", four workgroups per CU), which has no partner hand-off since
+    round 5, must hand off nothing."""
     import ctypes
     import torch
     from splendor_gym import _native
     K, seed, launches = 128, 0, 2
     chain = engine(n, P, refill_period=R)
     roll = engine(n, P, refill_period=R, refill_fused=True, pipeline=pipeline, partner_lead=lead)  # bench.py defaults
-    want = "k_rollout_store_2p" if (P == 2 and pipeline is True) else f"k_rollout_store_dealer2_{P}p"
+    want = {"always": "k_rollout_store_2p", "quad": f"k_rollout_store_quad_{P}p",
+            "dealer2": f"k_rollout_store_dealer2_{P}p"}.get(pipeline, roll.rollout_kernel_name())
     assert roll.rollout_kernel_name() == want
+    multi = want.startswith(("k_rollout_store_dealer2", "k_rollout_store_quad"))  # the partner hand-off runs
     pst = (ctypes.c_uint64 * 2)()
     _native.check(roll.lib, roll.lib.spl_debug_partner_stats(pst, 1))
     chain.reset(seeds=range(n))
@@ -97,9 +102,9 @@ def test_headline_rollout_65536_equals_step_chain_and_oracle(P, n, R, lead, pipe
     assert int(st["c"][1].sum()) > (100_000 if n == 65536 else 50_000 if P == 2 else 200_000)  # one episode per ~77 (2p) / ~29 (4p) plies
     assert chain.download().tobytes() == roll.download().tobytes()
     _native.check(roll.lib, roll.lib.spl_debug_partner_stats(pst, 0))
-    if want.startswith("k_rollout_store_dealer2") and lead == -1:
+    if multi and lead == -1:
         assert pst[0] > 1000, (pst[0], pst[1])  # many row blocks were stored by the partner
-    elif not want.startswith("k_rollout_store_dealer2"):
+    elif not multi:
         assert pst[0] == 0 and pst[1] == 0, (pst[0], pst[1])
 
 

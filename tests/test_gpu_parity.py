@@ -273,7 +273,9 @@ def test_unseeded_tables_deal_engine_seed_zero(orc):
                                                           (4, 128, True, "dealer", 16), (2, 16, True, "dealer", 0),
                                                           (3, 64, False, "dealer", 32), (4, 64, True, "dealer", 1),
                                                           (4, 128, True, "dealer2", 16), (2, 16, True, "dealer2", 0),
-                                                          (3, 64, False, "dealer2", 32)])
+                                                          (3, 64, False, "dealer2", 32), (2, 64, True, "quad", 64),
+                                                          (4, 128, True, "quad", 16), (3, 16, True, "quad", 0),
+                                                          (2, 16, False, "quad", 16)])
 def test_rollout_equals_step_chain(P, K, refill_fused, pipeline, R):
     """spl_rollout(K) is K chained spl_step calls (next_actions fed back, plies ply..ply+K-1):
     every per-step output, the terminal rows of final_obs, episode statistics, the next action
@@ -346,7 +348,8 @@ def _check_rollout_vs_chain(P, K, refill_fused, pipeline, R, partner_lead=None, 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("P,lead,pipeline", [(4, -1, "dealer2"), (2, -1, "dealer2"), (4, 2, "dealer2"), (3, 1, "dealer2"),
-                                             (3, -1, "dealer2"), (2, -1, "always"), (4, -1, "always")])
+                                             (3, -1, "dealer2"), (2, -1, "always"), (4, -1, "always"),
+                                             (2, -1, "quad"), (4, -1, "quad"), (3, -1, "quad"), (2, 2, "quad")])
 def test_partner_handoff_equals_step_chain(P, lead, pipeline):
     """The partner hand-off of the six-wave dealer's rollout store (spl_ctx_set_partner_lead; its dealer
     wave polls the flags): with lead -1 every team hands its steps' rows to the same team of the
@@ -355,29 +358,33 @@ def test_partner_handoff_equals_step_chain(P, lead, pipeline):
     every per-step output still equals the chained spl_step bit for bit, and the diagnostic counters
     show the hand-offs happened.  Lead 1-2: hand-offs only when a partner runs ahead (timing-dependent;
     same results either way).  The two-wave kernel ("always") has no partner hand-off since round 5
-    (VERDICT r04 item 1): a forced lead is ignored there, no task is handed off."""
+    (VERDICT r04 item 1): a forced lead is ignored there, no task is handed off; the quad kernel (four
+    two-wave teams in one workgroup per CU, its rules waves polling) has it."""
     import ctypes
     from splendor_gym import _native
     st = (ctypes.c_uint64 * 2)()
     probe = engine(128, 2)
     _native.check(probe.lib, probe.lib.spl_debug_partner_stats(st, 1))
     fused = _check_rollout_vs_chain(P, 64, True, pipeline, 16, partner_lead=lead, launches=3)
-    assert fused.rollout_kernel_name() == (f"k_rollout_store_dealer2_{P}p" if pipeline == "dealer2" else f"k_rollout_store_{P}p")
+    name = {"dealer2": f"k_rollout_store_dealer2_{P}p", "quad": f"k_rollout_store_quad_{P}p"}.get(pipeline, f"k_rollout_store_{P}p")
+    assert fused.rollout_kernel_name() == name
     _native.check(fused.lib, fused.lib.spl_debug_partner_stats(st, 1))
-    if pipeline != "dealer2":
+    if pipeline not in ("dealer2", "quad"):
         assert st[0] == 0 and st[1] == 0, (st[0], st[1])
     elif lead < 0:
         assert st[0] > 0, (st[0], st[1])  # the partners stored handed-off blocks
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1000, 1156])
-def test_partner_handoff_ragged_grids_equal_step_chain(n):
-    """Forced partner hand-off of the six-wave dealer on grids whose last workgroup is partial or has
-    no neighbour (n = 1000: 8 workgroups of two 64-table teams, the last team ragged; 1 156: an odd
-    count of 64-table teams): those teams keep their rows (pair and neighbour checks), every other
-    team hands off, and the outputs equal the chained spl_step."""
-    _check_rollout_vs_chain(2, 32, True, "dealer2", 16, partner_lead=-1, launches=2, n=n)
+@pytest.mark.parametrize("pipeline,n", [("dealer2", 1000), ("dealer2", 1156), ("quad", 1000), ("quad", 1156),
+                                        ("quad", 1792)])
+def test_partner_handoff_ragged_grids_equal_step_chain(pipeline, n):
+    """Forced partner hand-off of the multi-team kernels on grids whose last workgroup is partial or
+    has no neighbour (dealer2, n = 1000: 8 workgroups of two 64-table teams, the last team ragged;
+    1 156: an odd count of 64-table teams; quad, n = 1792: 7 workgroups of four teams, the last without
+    a neighbour): those teams keep their rows (pair and neighbour checks), every other team hands off,
+    and the outputs equal the chained spl_step."""
+    _check_rollout_vs_chain(2, 32, True, pipeline, 16, partner_lead=-1, launches=2, n=n)
 
 
 @pytest.mark.parametrize("pipeline", [True, "always", False])

@@ -153,7 +153,7 @@ for step in "$@"; do
     polab2)  # the fp32 actor's weight ring: LDS-DMA (product) vs VGPR-staged (lib_ringv*), hidden A prefetch 2 vs 1
       for i in 1 2; do
         run pol_full_$i 200 python tools/bench_policy.py --fused-only --iters 30
-        for v in ringv ringv_d1 d1; do
+        for v in ${POLAB_LIBS:-ringv ringv_d1 d1}; do
           SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_$v.so run pol_${v}_$i 200 python tools/bench_policy.py --fused-only --iters 30
         done
       done
