@@ -4109,7 +4109,8 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
 // (pipeline 1): the six-wave dealer variant when every 128-table workgroup is resident at once (one
 // per CU, e.g. C4's 32 768 tables per GPU: 1 120-1 137 against 1 166-1 172 us per 128-step launch
 // for the three-wave one, alternating on one box, profiles/r04/c4ab_r04b.txt), else the three-wave
-// one when it fits, else two waves at 64 tables per workgroup.
+// one when it fits, else (2 players) the quad kernel when every 256-table workgroup is resident, else
+// two waves at 64 tables per workgroup.
 constexpr int kDealerShape = -1, kDealer2Shape = -2, kQuadShape = -3;
 static int rollout_tpw(const spl_ctx_t *ctx, int32_t n, int32_t players) {
     if (ctx->pipeline == 2) return 64;
@@ -4119,7 +4120,12 @@ static int rollout_tpw(const spl_ctx_t *ctx, int32_t n, int32_t players) {
     if (ctx->pipeline == 6) return kQuadShape;
     if (ctx->pipeline == 1) {  // auto: the six-wave dealer (SIMD-aware roles, -3.5 % on C4's share), else three-wave
         if ((int64_t)((n + 127) / 128) <= ctx->dealer2_resident[players]) return kDealer2Shape;
-        return (int64_t)blocks_for(n) <= ctx->dealer_resident[players] ? kDealerShape : 64;
+        if ((int64_t)blocks_for(n) <= ctx->dealer_resident[players]) return kDealerShape;
+        // 2 players up to one quad workgroup per CU (the headline's 65 536 tables): the quad kernel with its
+        // partner hand-off, 1 959-1 983 against 2 008-2 031 us per 128-step launch for the two-wave kernel,
+        // alternating on one box (profiles/r05/headline_quad_ab_r05h.txt); 3-4 players keep the two-wave
+        if (players == 2 && (int64_t)((n + 255) / 256) <= ctx->quad_resident[players]) return kQuadShape;
+        return 64;
     }
     return 0;
 }

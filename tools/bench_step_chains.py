@@ -22,7 +22,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "splendor-gym_amd"))
 
 
-def run(T, C, G, replays, warm, seed=0, eager=False):
+def run(T, C, G, replays, warm, seed=0, eager=False, offset_cycles=0):
     import torch
     from splendor_gym import _native
     from splendor_gym.device import Engine
@@ -68,8 +68,11 @@ def run(T, C, G, replays, warm, seed=0, eager=False):
         per = []
         for rep in range(warm + replays):
             ev0.record(main)
-            for s_ in side:
+            for c, s_ in enumerate(side, start=1):
                 s_.wait_event(ev0)
+                if offset_cycles:  # chain c starts c x offset later: its rules phases fall into chain 0's stores
+                    with torch.cuda.stream(s_):
+                        torch.cuda._sleep(int(c * offset_cycles))
             for k in range(G):
                 for c, ch in enumerate(chains):
                     e = ch["eng"]
@@ -92,7 +95,8 @@ def run(T, C, G, replays, warm, seed=0, eager=False):
         bad = sum(int(((ch["eng"].flags & errs) != 0).sum().item()) for ch in chains)
         for ch in chains:
             ch["eng"].close()
-        return {"tables": T, "chains": C, "mode": "eager", "tables_per_chain": n, "steps": G, "reps": replays,
+        return {"tables": T, "chains": C, "mode": "eager", "offset_cycles": offset_cycles, "tables_per_chain": n,
+                "steps": G, "reps": replays,
                 "us_per_env_step": {"min": round(per[0], 3), "median": round(per[len(per) // 2], 3), "max": round(per[-1], 3)},
                 "env_steps_per_s": round(T / (per[len(per) // 2] * 1e-6), 1), "error_flags": bad}
     g = torch.cuda.CUDAGraph()
@@ -139,10 +143,13 @@ def main():
     ap.add_argument("--warm", type=int, default=2)
     ap.add_argument("--rounds", type=int, default=2, help="alternate the chain counts this many times")
     ap.add_argument("--eager", action="store_true", help="eager launches on C streams instead of one hipGraph")
+    ap.add_argument("--offsets", default="0", help="eager: start offsets of chain c (c x this many GPU cycles), comma list")
     a = ap.parse_args()
     for r in range(a.rounds):
         for C in [int(x) for x in a.chains.split(",")]:
-            print(json.dumps(dict(run(a.tables, C, a.graph_steps, a.replays, a.warm, eager=a.eager), round=r)), flush=True)
+            for off in ([int(x) for x in a.offsets.split(",")] if a.eager and C > 1 else [0]):
+                print(json.dumps(dict(run(a.tables, C, a.graph_steps, a.replays, a.warm, eager=a.eager,
+                                          offset_cycles=off), round=r)), flush=True)
 
 
 if __name__ == "__main__":

@@ -148,8 +148,17 @@ for step in "$@"; do
         run c4ab_${pl}_$i 300 python3 bench.py --no-cpu-baseline --players 4 --tables 32768 --only --pipeline $pl
       done; done ;;
     abl32) bash tools/ablate_policy32.sh || exit 1 ;;  # k_act32 timing ablations (BUILD=1 here first)
+    quadtests) run pytest_quad 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_headline.py -k "quad" -x -v \
+                   --timeout 300 --timeout-method thread ;;
+    quadab)  # the headline shape: two-wave (4 workgroups per CU) vs quad (one per CU, partner hand-off at lead 4 / off), alternating
+      for i in 1 2; do
+        run head_ws_$i 300 python3 bench.py --no-cpu-baseline --only --pipeline always
+        run head_quad_$i 300 python3 bench.py --no-cpu-baseline --only --pipeline quad
+        run head_quad0_$i 300 python3 bench.py --no-cpu-baseline --only --pipeline quad --partner-lead 0
+      done
+      for f in $O/head_*_[12]_$TAG.out; do python3 -c "import json,sys; d=json.loads(open('$f').read().strip().splitlines()[-1]); r=d['roofline']; print('$f', d['value'], r['kernel'], r['kernel_us'], d.get('partner_handoffs'))"; done ;;
     chains) run step_chains 300 python3 tools/bench_step_chains.py ;;
-    chainse) run step_chains_eager 300 python3 tools/bench_step_chains.py --eager ;;
+    chainse) run step_chains_eager 300 python3 tools/bench_step_chains.py --eager --chains 1,2 --offsets 0,8000,16000,24000 ;;
     polab2)  # the fp32 actor's weight ring: LDS-DMA (product) vs VGPR-staged (lib_ringv*), hidden A prefetch 2 vs 1
       for i in 1 2; do
         run pol_full_$i 200 python tools/bench_policy.py --fused-only --iters 30
