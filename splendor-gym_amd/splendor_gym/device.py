@@ -34,7 +34,7 @@ class Engine:
     DEFAULT_REFILL = {2: 64, 3: 32, 4: 16}
 
     def __init__(self, num_tables, num_players=2, device=None, refill_period=None, table0=0, refill_fused=True,
-                 pipeline=True, delegation=None, cards=None, partner_lead=None):
+                 pipeline=True, delegation=None, cards=None, partner_lead=None, host_io=False):
         torch = _native.require_gpu()
         self.torch = torch
         self.lib = _native.load_library()
@@ -68,7 +68,12 @@ class Engine:
             nb = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
             offs.append((name, dt, shape, off, nb))
             off = (off + nb + 255) // 256 * 256
-        self.io = torch.zeros(off, dtype=torch.uint8, device=dev)
+        # host_io (the single-table SplendorEnv): the I/O block lives in pinned host memory, which the
+        # kernels read (actions) and write (outputs) through its device mapping — a step is then one
+        # launch and a stream synchronisation, no fill kernel for the action and no copy of the outputs
+        self.host_io = bool(host_io)
+        self.io = (torch.zeros(off, dtype=torch.uint8, pin_memory=True) if self.host_io
+                   else torch.zeros(off, dtype=torch.uint8, device=dev))
         for name, dt, shape, o, nb in offs:
             setattr(self, name, self.io[o:o + nb].view(dt).view(shape))
         self.io_step_bytes = offs[6][3]  # obs .. winner
@@ -231,8 +236,8 @@ class Engine:
             raise RuntimeError("splendor engine: used after close()")
         if actions is None:
             actions = self.actions
-        if not (isinstance(actions, torch.Tensor) and actions.device == self.device and actions.dtype == torch.int32
-                and actions.is_contiguous()):
+        if not (isinstance(actions, torch.Tensor) and actions.dtype == torch.int32 and actions.is_contiguous()
+                and (actions.device == self.device or (self.host_io and actions is self.actions))):
             actions = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
         if actions.numel() != self.n:
             raise ValueError(f"expected {self.n} actions")

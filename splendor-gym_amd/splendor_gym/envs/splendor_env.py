@@ -2,7 +2,8 @@
 
 Drop-in for reference splendor_gym/envs/splendor_env.py:23-130 — same constructor, spaces, info
 keys, reward values and exceptions.  The table lives on the GPU (an Engine of one table,
-autoreset off); each call launches the step kernel and copies the ~1.3 KB result back.
+autoreset off); each call launches the step kernel, which reads the action from and writes its ~1.3 KB
+of outputs to pinned host memory (Engine(host_io=True)), and waits for it.
 For throughput use SplendorVectorEnv (thousands of tables per launch).
 """
 from typing import Any, Dict, Optional, Tuple
@@ -42,17 +43,17 @@ class SplendorEnv(Env):
     def _engine(self):
         if self._eng is None:
             from ..device import Engine
-            e = Engine(1, self.num_players, device=self._device, refill_period=0)
-            import torch
-            self._host = torch.empty(e.io_step_bytes, dtype=torch.uint8).pin_memory()
+            e = Engine(1, self.num_players, device=self._device, refill_period=0, host_io=True)
+            self._host = e.io.numpy()  # the pinned I/O block the kernels write
             self._eng = e
         return self._eng
 
     def _fetch(self):
-        """One device->host copy of this table's step outputs (obs, mask, reward, flags, ...)."""
+        """This table's step outputs (obs, mask, reward, flags, ...), written by the kernel straight
+        into the pinned I/O block: wait for the launch, then read them."""
         e = self._eng
-        self._host.copy_(e.io[:e.io_step_bytes])  # synchronising copy
-        h = self._host.numpy()
+        e.torch.cuda.current_stream(e.device).synchronize()
+        h = self._host
         base = e.io.data_ptr()
 
         def view(t, dt, count):
@@ -180,7 +181,8 @@ class SplendorEnv(Env):
         e = self._engine()
         self._flush_view()
         e.legal()
-        return e.mask[0].cpu().numpy()
+        e.torch.cuda.current_stream(e.device).synchronize()  # the mask lands in the pinned I/O block
+        return e.mask[0].numpy().copy()
 
     def render(self):
         """Print the reference logger's compact text of the table (envs/splendor_env.py:119-126)."""
