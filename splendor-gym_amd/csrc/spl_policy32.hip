@@ -55,6 +55,14 @@
 #ifndef SPL_P32_GROUP
 #define SPL_P32_GROUP 2
 #endif
+// SPL_P32_SPREAD k (group-2 ring, pipelined epilogue): tile c issues chunk c+2's LDS-DMA pieces inside
+// its own k-steps, piece i after k-step k*i, instead of chunks c+2 and c+3 back to back right behind the
+// even barrier (a piece issued among MFMAs costs the wave ~60 cycles of issue, 100-185 in a burst of
+// eight, MI355X_MICROARCH.md).  0: the burst.  Default 2: exact k_act32<true, true> 208.3 -> 201.5 us,
+// f16x2 121.6 -> 118.7 us, alternating on one box (profiles/r05/pol_spread_ab_r05j.txt; 1: 203.4 us)
+#ifndef SPL_P32_SPREAD
+#define SPL_P32_SPREAD 2
+#endif
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
 // streaming, no per-tile barrier), 4 A fragments loaded once per tile (no per-group LDS reads),
 // 16 the ring without its per-chunk barrier (waves race the slots)
@@ -777,6 +785,22 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     }
 
     int c = 0;
+#if SPL_P32_SPREAD
+    static_assert(SPL_P32_GROUP == 2 && SPL_P32_PIPE, "spread pieces ride the pipelined k-steps of the group-2 ring");
+    // tile c loads chunk c+2 (its slot held chunk c-2, free since the barrier of c or c-1): piece i of
+    // this wave (block wave + 8 i) after k-step SPREAD * i
+    int dnext = 0;
+    auto tick = [&](int s) {
+        if (s % SPL_P32_SPREAD == 0 && s / SPL_P32_SPREAD < G::kBlocksPerWave) {
+            const int blk = wave + kWaves * (s / SPL_P32_SPREAD);
+            if (dnext < kTotal && blk < G::kChunkBlocks)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void *)(ring + (dnext % kSlots) * kChunk + blk * 1024), 16,
+                                                         lane * 16, dnext * kChunk + blk * 1024, 0, 0);
+        }
+    };
+#else
+    auto tick = [&](int) {};
+#endif
     auto enter = [&]() -> const uint8_t * {
 #if SPL_POL_ABL & 2
         if (c++ == 0) {
@@ -793,9 +817,11 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
+#if !SPL_P32_SPREAD
 #pragma unroll
             for (int j = 2; j < 4; ++j)
                 if (c + j < kTotal) issue_chunk<F>(wrs, c + j, ring + ((c + j) % kSlots) * kChunk, wave, lane);
+#endif
         }
 #elif SPL_P32_RINGV
         // the staged chunk c+S-2 (loaded one tile ago) -> its slot, which held chunk c-2 (every wave was
@@ -817,6 +843,9 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
         issue_chunk<F>(wrs, nxt, ring + ((c + kSlots - 1) % kSlots) * kChunk, wave, lane);
 #endif
         const uint8_t *slot = ring + (c % kSlots) * kChunk;
+#if SPL_P32_SPREAD
+        dnext = c + 2;
+#endif
         ++c;
         return slot;
     };
@@ -837,6 +866,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
         for (int t = 0; t < kTiles; ++t) {  // critic layer 1 -> H1
             f32x4 cf;
             const f32x4 acc = tile_mma<F, kKs1, 1, kAheadL1, kFoldP>(enter(), X, lane, &cf, &hi, [&](int s) {
+                tick(s);
                 if (t > 0) split_stage<F>(H1, t - 1, q, s);
             });
             q.acc = acc;
@@ -845,6 +875,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
         {  // critic layer 2 -> its tiles' shares of the output unit; tile 0 finishes layer 1's last tile
             f32x4 cf;
             const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid, kFoldP>(enter(), H1, lane, &cf, nullptr, [&](int s) {
+                tick(s);
                 split_stage<F>(H1, kTiles - 1, q, s);
             });
             q.acc = acc;
@@ -854,6 +885,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
         for (int t = 1; t < kTiles; ++t) {  // one loop body (as round 4's critic layer 2): no register
             f32x4 cf;                       // array is indexed by t here
             const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid, kFoldP>(enter(), H1, lane, &cf, nullptr, [&](int s) {
+                tick(s);
                 value_stage<F>(q, crit + 16 * (t - 1) + 4 * g, value, s);
             });
             q.acc = acc;
@@ -874,6 +906,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     for (int t = 0; t < kTiles; ++t) {  // actor layer 1 -> H1 (the critic's layer 2 has read H1 by now)
         f32x4 cf;
         const f32x4 acc = tile_mma<F, kKs1, 1, kAheadL1, kFoldP>(enter(), X, lane, &cf, &hi, [&](int s) {
+            tick(s);
             if (t > 0) split_stage<F>(H1, t - 1, q, s);
             else if (kCritic) value_stage<F>(q, crit + 16 * (kTiles - 1) + 4 * g, value, s);
         });
@@ -890,6 +923,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     for (int t = 0; t < kTiles; ++t) {  // actor layer 2 -> H2
         f32x4 cf;
         const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid, kFoldP>(enter(), H1, lane, &cf, nullptr, [&](int s) {
+            tick(s);
             if (t == 0) split_stage<F>(H1, kTiles - 1, q, s);
             else split_stage<F>(H2, t - 1, q, s);
         });
@@ -900,6 +934,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
 #pragma unroll
     for (int t = 0; t < kActTiles; ++t)  // the logits (true scale)
         L[t] = tile_mma<F, kKs2, F::kPlanes, kAheadHid>(enter(), H2, lane, nullptr, nullptr, [&](int s) {
+            tick(s);
             if (t == 0) split_stage<F>(H2, kTiles - 1, q, s);
         });
 #else

@@ -167,6 +167,16 @@ for step in "$@"; do
         done
       done
       for f in $O/pol_*_[12]_$TAG.out; do echo "$f $(cut -c1-120 $f)"; done ;;
+    spreadab)  # the fp32 actor's ring refill: pieces in a burst behind the barrier (product) vs spread over k-steps
+      SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_spread${SPREAD_K:-2}.so run pytest_spread 400 python -u -m pytest \
+          tests/test_gpu_policy.py -x -q --timeout 200 --timeout-method thread
+      for i in 1 2; do
+        run pol_burst_$i 200 python tools/bench_policy.py --fused-only --iters 30
+        for k in ${SPREAD_KS:-1 2}; do
+          SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_spread$k.so run pol_spread${k}_$i 200 python tools/bench_policy.py --fused-only --iters 30
+        done
+      done
+      for f in $O/pol_*_[12]_$TAG.out; do echo "$f $(cut -c1-160 $f)"; done ;;
     polab)  # the fp32 actor: staged epilogue (product) vs after each tile (ablate/lib_nopipe.so), alternating
       for i in 1 2; do
         run pol_pipe_$i 200 python tools/bench_policy.py --fused-only --iters 30
