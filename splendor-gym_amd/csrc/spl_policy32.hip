@@ -55,13 +55,16 @@
 #ifndef SPL_P32_GROUP
 #define SPL_P32_GROUP 2
 #endif
-// SPL_P32_SPREAD k (group-2 ring, pipelined epilogue): tile c issues chunk c+2's LDS-DMA pieces inside
-// its own k-steps, piece i after k-step k*i, instead of chunks c+2 and c+3 back to back right behind the
-// even barrier (a piece issued among MFMAs costs the wave ~60 cycles of issue, 100-185 in a burst of
-// eight, MI355X_MICROARCH.md).  0: the burst.  Default 2: exact k_act32<true, true> 208.3 -> 201.5 us,
-// f16x2 121.6 -> 118.7 us, alternating on one box (profiles/r05/pol_spread_ab_r05j.txt; 1: 203.4 us)
+// SPL_P32_SPREAD (group-2 ring, pipelined epilogue): the ring's LDS-DMA pieces are issued one per
+// k-step inside the tiles (see tick in act32_body) instead of eight back to back right behind the even
+// barrier (a piece issued among MFMAs costs the wave ~60 cycles of issue, 100-185 in a burst of eight,
+// MI355X_MICROARCH.md).  0: the burst.  Alternating on one box, exact k_act32<true, true>: burst
+// 208.3 us -> one piece per two k-steps of every tile 201.5 (profiles/r05/pol_spread_ab_r05j.txt) ->
+// branch-free pieces 197.1 (pol_nobr_ab_r05k.txt) -> + the paired plane split 198.1 vs 201.4
+// (pol_pair_ab_r05l.txt) -> even tiles load the next pair, hidden chunks without their padding blocks
+// 191.9 vs 198.3 (pol_ahead_ab_r05m.txt)
 #ifndef SPL_P32_SPREAD
-#define SPL_P32_SPREAD 2
+#define SPL_P32_SPREAD 1
 #endif
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
 // streaming, no per-tile barrier), 4 A fragments loaded once per tile (no per-group LDS reads),
@@ -125,8 +128,13 @@ constexpr int kLogitRow = 49;                   // floats per staged logit row (
 // sizes that follow from the format
 template <class F>
 struct Geo {
-    static constexpr int kBiasOff = kKs1 * F::kPlanes * kFrag;  // after the largest weight block
-    static constexpr int kChunk = kBiasOff + 1024;              // + 16 biases, 16 row factors, 16 tanh factors
+    // a layer's chunk: its KS k-steps of weight blocks, then one block of 16 biases, 16 row factors and
+    // 16 tanh factors (bias_off); chunks are kChunk apart in the image (the largest, layer 1's) and a
+    // hidden layer's 6 (exact) / 4 (f16x2) trailing blocks are zero padding the ring does not load
+    static constexpr int kBiasOff = kKs1 * F::kPlanes * kFrag;
+    static constexpr int kChunk = kBiasOff + 1024;
+    static constexpr int bias_off(int ks) { return ks * F::kPlanes * kFrag; }
+    static constexpr int blocks(int ks) { return ks * F::kPlanes + 1; }
     static constexpr int kLdsMask = F::kSlots * kChunk;
     static constexpr int kLdsCritic = kLdsMask + kWaves * kMaskWave;  // the critic's fp32 output layer (1 KB)
     static constexpr int kLds = kLdsCritic + kCriticTail;
@@ -171,7 +179,7 @@ __device__ __forceinline__ void split_planes(float x, typename F::pel (&q)[F::kP
 template <class F>
 __device__ __forceinline__ void pack_chunk(PackNet actor, PackNet critic, int with_critic, uint8_t *dst) {
     typedef typename F::pel pel;
-    constexpr int kChunk = Geo<F>::kChunk, kBiasOff = Geo<F>::kBiasOff;
+    constexpr int kChunk = Geo<F>::kChunk;
     const int ch = blockIdx.x;
     const int net = with_critic && ch < kCriticChunks ? 1 : 0;  // 0 actor, 1 critic
     const int local = ch - (with_critic && !net ? kCriticChunks : 0);
@@ -181,7 +189,7 @@ __device__ __forceinline__ void pack_chunk(PackNet actor, PackNet critic, int wi
     const float *W = layer == 1 ? P.w1 : layer == 2 ? P.w2 : P.w3;
     const float *B = layer == 1 ? P.b1 : layer == 2 ? P.b2 : P.b3;
     const int in = layer == 1 ? kObs : kHid, rows = layer == 3 ? P.out : kHid;
-    const int ks = layer == 1 ? kKs1 : kKs2;
+    const int ks = layer == 1 ? kKs1 : kKs2, bias_at = Geo<F>::bias_off(ks);
     uint8_t *out = dst + (size_t)ch * kChunk;
     pel *o = reinterpret_cast<pel *>(out);
     // each row's scale exponent: its largest |w| into [2^(kRowMaxExp-1), 2^kRowMaxExp) (fp16 planes)
@@ -213,9 +221,7 @@ __device__ __forceinline__ void pack_chunk(PackNet actor, PackNet critic, int wi
 #pragma unroll
         for (int p = 0; p < F::kPlanes; ++p) o[base + (size_t)p * 64 * 8] = q[p];
     }
-    for (int v = ks * F::kPlanes * kFrag + 4 * threadIdx.x; v < kBiasOff; v += 4 * blockDim.x)
-        *reinterpret_cast<uint32_t *>(out + v) = 0u;
-    float *bias = reinterpret_cast<float *>(out + kBiasOff);
+    float *bias = reinterpret_cast<float *>(out + bias_at);
     const int act_exp = layer == 1 ? 0 : F::kActScaleExp;  // layer 1 reads the observation unscaled
     if (threadIdx.x < 16) {  // scaled biases in row order, the row factors, the tanh factors, zero padding
         const int row = 16 * tile + threadIdx.x, ex = rexp[threadIdx.x] + act_exp;
@@ -225,7 +231,7 @@ __device__ __forceinline__ void pack_chunk(PackNet actor, PackNet critic, int wi
         // unscaled sum (tanh_fold)
         bias[32 + threadIdx.x] = ldexpf(kTwoLog2e, -ex);
     }
-    for (int v = kBiasOff + 192 + 4 * threadIdx.x; v < kChunk; v += 4 * blockDim.x)
+    for (int v = bias_at + 192 + 4 * threadIdx.x; v < kChunk; v += 4 * blockDim.x)
         *reinterpret_cast<uint32_t *>(out + v) = 0u;
     if (net == 1 && layer == 2 && tile == 0) {  // the critic's output layer as fp32 (evaluated on VALU)
         float *tail = reinterpret_cast<float *>(dst + (size_t)kAllChunks * kChunk);
@@ -406,7 +412,7 @@ __device__ __forceinline__ f32x4 tile_mma(const uint8_t *src, const typename F::
     typedef typename F::pelx8 pelx8;
     constexpr int kPlanes = F::kPlanes;
     static_assert(NB == 1 || NB == kPlanes, "planes");
-    const float *bias = reinterpret_cast<const float *>(src + Geo<F>::kBiasOff) + 4 * (lane >> 4);
+    const float *bias = reinterpret_cast<const float *>(src + Geo<F>::bias_off(KS)) + 4 * (lane >> 4);
     f32x4 acc = {bias[0], bias[1], bias[2], bias[3]};
     const f32x4 unscale = {bias[16], bias[17], bias[18], bias[19]};
     if constexpr (kFold) *fold = f32x4{bias[32], bias[33], bias[34], bias[35]};
@@ -501,18 +507,32 @@ __device__ __forceinline__ float pend_tanh(const PendTile<F> &q, int i) {
     if constexpr (F::kExact) return tanh_acc(q.acc[i]);
     else return tanh_fold<F::kActScaleExp>(q.acc[i], q.c[i]);
 }
+// split_planes of two values at once, each plane as the packed dword of the pair: one paired
+// conversion per plane (v_cvt_pk_bf16_f32 rounds both to nearest even) and the residuals from the
+// packed halves (the bf16 -> fp32 widening is a shift or a mask), 11 VALU ops per pair in the exact
+// format instead of 15 for two single splits plus their packing
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <class F>
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t (&d)[F::kPlanes]) {
+    typedef typename F::pelx2 pelx2;
+    f32x2 v = {a, b};
+#pragma unroll
+    for (int p = 0; p < F::kPlanes; ++p) {
+        const pelx2 q = __builtin_convertvector(v, pelx2);
+        d[p] = __builtin_bit_cast(uint32_t, q);
+        if (p + 1 < F::kPlanes) v -= __builtin_convertvector(q, f32x2);  // exact in fp32
+    }
+}
 // values (2 pair, 2 pair + 1) of tile t -> dword 2 (t & 1) + pair of k-step t / 2 of every plane
 template <class F>
 __device__ __forceinline__ void put_pair(typename F::pelx8 (&H)[F::kPlanes][kKs2], int t, int pair, float ha, float hb) {
-    typedef typename F::pel pel;
     typedef typename F::pelx8 pelx8;
-    pel xa[F::kPlanes], xb[F::kPlanes];
-    split_planes<F>(ha, xa);  // h carries 2^kActScaleExp already (tanh_fold) or needs none (exact)
-    split_planes<F>(hb, xb);
+    uint32_t d[F::kPlanes];
+    split_pair<F>(ha, hb, d);  // h carries 2^kActScaleExp already (tanh_fold) or needs none (exact)
 #pragma unroll
     for (int p = 0; p < F::kPlanes; ++p) {
         u32x4 w = __builtin_bit_cast(u32x4, H[p][t >> 1]);
-        w[2 * (t & 1) + pair] = pk2<F>(xa[p], xb[p]);
+        w[2 * (t & 1) + pair] = d[p];
         H[p][t >> 1] = __builtin_bit_cast(pelx8, w);
     }
 }
@@ -787,19 +807,37 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     int c = 0;
 #if SPL_P32_SPREAD
     static_assert(SPL_P32_GROUP == 2 && SPL_P32_PIPE, "spread pieces ride the pipelined k-steps of the group-2 ring");
-    // tile c loads chunk c+2 (its slot held chunk c-2, free since the barrier of c or c-1): piece i of
-    // this wave (block wave + 8 i) after k-step SPREAD * i
+    // even tile c loads the next pair, chunks c+2 and c+3 (their slots held c-2 and c-1, free since the
+    // barrier of c), which the barrier of c+2 waits for: a tile or more after the last piece is issued.
+    // Pieces 0 .. kLast-1 of each chunk (blocks wave + 8 i, which every wave and layer has) one per
+    // k-step from k-step 0, branch-free (a branch would end the scheduling region between a k-step's
+    // MFMAs and the epilogue stage that should interleave with them; a chunk past the image's last
+    // re-loads that last chunk into its free slot); the last piece after the tile's last k-step, where
+    // a branch splits nothing, by the waves whose block the chunk's layer has (layer 1: all but the
+    // last; a hidden layer: its bias block, wave 0).  Odd tiles load nothing.
     int dnext = 0;
-    auto tick = [&](int s) {
-        if (s % SPL_P32_SPREAD == 0 && s / SPL_P32_SPREAD < G::kBlocksPerWave) {
-            const int blk = wave + kWaves * (s / SPL_P32_SPREAD);
-            if (dnext < kTotal && blk < G::kChunkBlocks)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void *)(ring + (dnext % kSlots) * kChunk + blk * 1024), 16,
-                                                         lane * 16, dnext * kChunk + blk * 1024, 0, 0);
+    auto tick = [&](int s, int ks, int odd) {  // after k-step s of a tile of ks k-steps (s, ks, odd known at compile time)
+        constexpr int kLast = G::kBlocksPerWave - 1;
+        if (odd) return;
+        if (s < 2 * kLast) {
+            const int j = s / kLast, blk = wave + kWaves * (s % kLast), ch = min(dnext + j, kTotal - 1);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void *)(ring + ((dnext + j) % kSlots) * kChunk + blk * 1024),
+                                                     16, lane * 16, ch * kChunk + blk * 1024, 0, 0);
+        }
+        if (s == ks - 1) {
+            const int blk = wave + kWaves * kLast;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int ch = dnext + j;
+                const bool l1 = (kCritic && ch >= kCriticChunks ? ch - kCriticChunks : ch) < kTiles;
+                if (ch < kTotal && blk < (l1 ? G::blocks(kKs1) : G::blocks(kKs2)))
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void *)(ring + (ch % kSlots) * kChunk + blk * 1024), 16,
+                                                             lane * 16, ch * kChunk + blk * 1024, 0, 0);
+            }
         }
     };
 #else
-    auto tick = [&](int) {};
+    auto tick = [&](int, int, int) {};
 #endif
     auto enter = [&]() -> const uint8_t * {
 #if SPL_POL_ABL & 2
@@ -866,7 +904,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
         for (int t = 0; t < kTiles; ++t) {  // critic layer 1 -> H1
             f32x4 cf;
             const f32x4 acc = tile_mma<F, kKs1, 1, kAheadL1, kFoldP>(enter(), X, lane, &cf, &hi, [&](int s) {
-                tick(s);
+                tick(s, kKs1, t & 1);
                 if (t > 0) split_stage<F>(H1, t - 1, q, s);
             });
             q.acc = acc;
@@ -875,21 +913,26 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
         {  // critic layer 2 -> its tiles' shares of the output unit; tile 0 finishes layer 1's last tile
             f32x4 cf;
             const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid, kFoldP>(enter(), H1, lane, &cf, nullptr, [&](int s) {
-                tick(s);
+                tick(s, kKs2, 0);
                 split_stage<F>(H1, kTiles - 1, q, s);
             });
             q.acc = acc;
             q.c = cf;
         }
-#pragma unroll 1
-        for (int t = 1; t < kTiles; ++t) {  // one loop body (as round 4's critic layer 2): no register
-            f32x4 cf;                       // array is indexed by t here
+        auto crit_l2 = [&](int t, int odd) {
+            f32x4 cf;
             const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid, kFoldP>(enter(), H1, lane, &cf, nullptr, [&](int s) {
-                tick(s);
+                tick(s, kKs2, odd);
                 value_stage<F>(q, crit + 16 * (t - 1) + 4 * g, value, s);
             });
             q.acc = acc;
             q.c = cf;
+        };
+        crit_l2(1, 1);
+#pragma unroll 1
+        for (int t = 2; t < kTiles; t += 2) {  // one loop body of an even and an odd tile (as round 4's
+            crit_l2(t, 0);                     // critic layer 2: no register array is indexed by t here)
+            crit_l2(t + 1, 1);
         }
     }
     if constexpr (!kActor) {
@@ -906,7 +949,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     for (int t = 0; t < kTiles; ++t) {  // actor layer 1 -> H1 (the critic's layer 2 has read H1 by now)
         f32x4 cf;
         const f32x4 acc = tile_mma<F, kKs1, 1, kAheadL1, kFoldP>(enter(), X, lane, &cf, &hi, [&](int s) {
-            tick(s);
+            tick(s, kKs1, t & 1);
             if (t > 0) split_stage<F>(H1, t - 1, q, s);
             else if (kCritic) value_stage<F>(q, crit + 16 * (kTiles - 1) + 4 * g, value, s);
         });
@@ -923,7 +966,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     for (int t = 0; t < kTiles; ++t) {  // actor layer 2 -> H2
         f32x4 cf;
         const f32x4 acc = tile_mma<F, kKs2, F::kPlanes, kAheadHid, kFoldP>(enter(), H1, lane, &cf, nullptr, [&](int s) {
-            tick(s);
+            tick(s, kKs2, t & 1);
             if (t == 0) split_stage<F>(H1, kTiles - 1, q, s);
             else split_stage<F>(H2, t - 1, q, s);
         });
@@ -934,7 +977,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
 #pragma unroll
     for (int t = 0; t < kActTiles; ++t)  // the logits (true scale)
         L[t] = tile_mma<F, kKs2, F::kPlanes, kAheadHid>(enter(), H2, lane, nullptr, nullptr, [&](int s) {
-            tick(s);
+            tick(s, kKs2, t & 1);
             if (t == 0) split_stage<F>(H2, kTiles - 1, q, s);
         });
 #else

@@ -177,6 +177,18 @@ for step in "$@"; do
         done
       done
       for f in $O/pol_*_[12]_$TAG.out; do echo "$f $(cut -c1-160 $f)"; done ;;
+    libab)  # the in-tree product library vs ablate/lib_$v.so for v in $LIBAB (policy parity on each, then alternating timings)
+      for v in $LIBAB; do
+        SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_$v.so run pytest_lib_$v 400 python -u -m pytest \
+            tests/test_gpu_policy.py -x -q --timeout 200 --timeout-method thread
+      done
+      for i in 1 2; do
+        run pol_product_$i 200 python tools/bench_policy.py --fused-only --iters 30
+        for v in $LIBAB; do
+          SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_$v.so run pol_${v}_$i 200 python tools/bench_policy.py --fused-only --iters 30
+        done
+      done
+      for f in $O/pol_*_[12]_$TAG.out; do echo "$f $(cut -c1-160 $f)"; done ;;
     polab)  # the fp32 actor: staged epilogue (product) vs after each tile (ablate/lib_nopipe.so), alternating
       for i in 1 2; do
         run pol_pipe_$i 200 python tools/bench_policy.py --fused-only --iters 30
