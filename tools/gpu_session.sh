@@ -178,9 +178,9 @@ for step in "$@"; do
       done
       for f in $O/pol_*_[12]_$TAG.out; do echo "$f $(cut -c1-160 $f)"; done ;;
     libab)  # the in-tree product library vs ablate/lib_$v.so for v in $LIBAB (policy parity on each, then alternating timings)
-      for v in $LIBAB; do
-        SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_$v.so run pytest_lib_$v 400 python -u -m pytest \
-            tests/test_gpu_policy.py -x -q --timeout 200 --timeout-method thread
+      for v in $LIBAB; do  # LIBAB_NOTEST=1: timing ablations (wrong results by design), no parity run
+        [ "${LIBAB_NOTEST:-0}" = "1" ] || SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_$v.so run pytest_lib_$v 400 \
+            python -u -m pytest tests/test_gpu_policy.py -x -q --timeout 200 --timeout-method thread
       done
       for i in 1 2; do
         run pol_product_$i 200 python tools/bench_policy.py --fused-only --iters 30
