@@ -369,15 +369,15 @@ def caller_path_line(n_envs=16, iters=150, warmup=10):
     with its own seed), driven one env at a time in Python exactly as ppo_splendor.py:235-269 does —
     env.dual_step(action), env.reset() after done.  The agent's actions are uniform over each env's
     legal mask (numpy), so the line times the env path alone, not the torch agent.  Every
-    SplendorEnv.step here is a one-table spl_step launch + one synchronous device->host copy of its
-    ~1.3 KB of outputs; the line reports env-steps/s (every SplendorEnv.step call: agent, opponent and
+    SplendorEnv.step here is a one-table spl_step launch that reads its action from and writes its
+    ~1.3 KB of outputs to pinned host memory, then one stream synchronisation; the line reports env-steps/s (every SplendorEnv.step call: agent, opponent and
     the openings after resets) and the time per SplendorEnv.step."""
     import numpy as np
     from training_utils import make_env
     np.random.seed(0)
     envs = [make_env(1000 + i, use_dual_player=True)() for i in range(n_envs)]
     clock = {"n": 0, "s": 0.0}
-    for w in envs:  # time every SplendorEnv.step (launch + synchronous copy)
+    for w in envs:  # time every SplendorEnv.step (launch + stream synchronisation)
         inner = w.env
         raw = inner.step
 
@@ -413,7 +413,7 @@ def caller_path_line(n_envs=16, iters=150, warmup=10):
             "us_per_splendorenv_step": round(clock["s"] / max(1, steps) * 1e6, 2),
             "us_per_dual_step": round(el / (iters * n_envs) * 1e6, 2),
             "host_share": round(1.0 - clock["s"] / el, 4),
-            "note": "host-bound: one launch + one synchronous copy per SplendorEnv.step; the batched "
+            "note": "host-bound: one launch + one stream synchronisation per SplendorEnv.step; the batched "
                     "DualStepVectorEnv (config5_selfplay) steps every table in one launch; agent forward excluded",
             "config": {"workload": "ppo_splendor.py:151-159,235-269 rollout loop shape, random legal agent actions, "
                                    "random_opponent", "envs": n_envs}}

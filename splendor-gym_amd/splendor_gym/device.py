@@ -276,6 +276,30 @@ class Engine:
         self._keep_actions = actions
         return self.obs, self.mask, rw, tm, fl
 
+    def host_stepper(self):
+        """SplendorEnv's per-call path: a launcher of spl_step over this engine's own actions and
+        outputs, autoreset off, no policy (what step(self.actions, autoreset=False) launches), with the
+        argument block built once — the per-call Python of step() is most of a one-table step's time."""
+        torch, lib, dev, idx = self.torch, self.lib, self.device, self.device.index
+        a = StepArgs(actions=self.actions.data_ptr(), obs=self.obs.data_ptr(), mask=self.mask.data_ptr(),
+                     reward=self.reward.data_ptr(), terminated=self.terminated.data_ptr(), flags=self.flags.data_ptr(),
+                     winner=self.winner.data_ptr(), final_obs=None, autoreset=0, table0=self.table0)
+        ref = ctypes.byref(a)
+
+        def go():
+            if self.ctx is None:
+                raise RuntimeError("splendor engine: used after close()")
+            s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            if torch.cuda.current_device() == idx:
+                rc = lib.spl_step(self.ctx, ctypes.byref(self.desc), ref, s)
+            else:
+                with torch.cuda.device(dev):
+                    rc = lib.spl_step(self.ctx, ctypes.byref(self.desc), ref, s)
+            if rc:
+                check(lib, rc)
+        go.args = a  # the block the launches point at
+        return go
+
     def rollout(self, steps, actions=None, next_actions=None, policy_seed=0, ply=0, out=None, final_obs=True,
                 ep_return=None, ep_count=None, ply_base=None, policy=0):
         """`steps` env steps of every table under the device uniform-random policy in one launch

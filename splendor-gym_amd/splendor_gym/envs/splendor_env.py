@@ -44,24 +44,26 @@ class SplendorEnv(Env):
         if self._eng is None:
             from ..device import Engine
             e = Engine(1, self.num_players, device=self._device, refill_period=0, host_io=True)
-            self._host = e.io.numpy()  # the pinned I/O block the kernels write
+            h, base = e.io.numpy(), e.io.data_ptr()  # the pinned I/O block the kernels read and write
+
+            def view(t, dt, count):
+                return np.frombuffer(h, dtype=dt, count=count, offset=t.data_ptr() - base)
+            self._v = dict(actions=view(e.actions, np.int32, 1), obs=view(e.obs, np.int32, OBSERVATION_DIM),
+                           mask=view(e.mask, np.int8, TOTAL_ACTIONS), reward=view(e.reward, np.float32, 1),
+                           terminated=view(e.terminated, np.uint8, 1), flags=view(e.flags, np.uint8, 1),
+                           winner=view(e.winner, np.int8, 1))
+            self._launch = e.host_stepper()
             self._eng = e
         return self._eng
 
     def _fetch(self):
         """This table's step outputs (obs, mask, reward, flags, ...), written by the kernel straight
         into the pinned I/O block: wait for the launch, then read them."""
-        e = self._eng
+        e, v = self._eng, self._v
         e.torch.cuda.current_stream(e.device).synchronize()
-        h = self._host
-        base = e.io.data_ptr()
-
-        def view(t, dt, count):
-            o = t.data_ptr() - base
-            return np.frombuffer(h, dtype=dt, count=count, offset=o)
-        self._out = dict(reward=float(view(e.reward, np.float32, 1)[0]), terminated=int(view(e.terminated, np.uint8, 1)[0]),
-                         flags=int(view(e.flags, np.uint8, 1)[0]), winner=int(view(e.winner, np.int8, 1)[0]))
-        return view(e.obs, np.int32, 297).copy(), view(e.mask, np.int8, 45).copy()
+        self._out = dict(reward=float(v["reward"][0]), terminated=int(v["terminated"][0]), flags=int(v["flags"][0]),
+                         winner=int(v["winner"][0]))
+        return v["obs"].copy(), v["mask"].copy()
 
     def reset(self, *, seed: Optional[int] = None, options: Optional[Dict[str, Any]] = None):
         super().reset(seed=seed)
@@ -91,8 +93,8 @@ class SplendorEnv(Env):
             raise ValueError("Action out of bounds for action_space")
         a = max(min(a, 2**31 - 1), -(2**31))
         self._flush_view()
-        e.actions.fill_(a)
-        e.step(e.actions, autoreset=False)
+        self._v["actions"][0] = a  # read by the kernel from pinned memory (no kernel is in flight here)
+        self._launch()              # = e.step(e.actions, autoreset=False)
         self._view = None
         obs, mask = self._fetch()
         o = self._out
