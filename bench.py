@@ -255,6 +255,9 @@ def node_fields(census, metric):
             "devices": census["identities"], "shared_device": shared}
 
 
+SELFPLAY_GRAPH_STEPS = 4
+
+
 def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
     """BASELINE config 5 per GPU: the PPO rollout step of ppo_splendor.py:227-269 for N tables —
     the agent's fused fp32 ActorCritic (get_action_and_value: actor + critic + masked sample) and
@@ -281,14 +284,15 @@ def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
     pool = OpponentPool(agent, pool_size=12, p_current=0.25, seed=99, precision=precision)
     for _ in range(12):
         pool.add_snapshot(net())
-    env = DualStepVectorEnv(N, device=dev, opponent=pool, table0=rank * N, opponent_obs=False)
+    # the agent's sampling draws are keyed by (seed; table, ply_base): the dual step's last launch
+    # advances ply_base (spl_dual_io_t.step_counter), so every captured step draws fresh actions
+    ply_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    env = DualStepVectorEnv(N, device=dev, opponent=pool, table0=rank * N, opponent_obs=False, step_counter=ply_t)
     obs, info = env.reset(seed=rank * N)
     mask = info["action_mask"]
-    ply_t = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def iteration():
         with torch.no_grad():
-            ply_t.add_(1)
             a, _, _, _ = agent_k.act(obs, mask, seed=1234, table0=rank * N, ply_base=ply_t)
             return env.dual_step(a)
 
@@ -300,15 +304,19 @@ def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
     with torch.cuda.stream(side):
         iteration()
     torch.cuda.current_stream(dev).wait_stream(side)
+    # SELFPLAY_GRAPH_STEPS dual steps per hipGraph (the host's replay call sits between graphs, ~8 us
+    # of idle GPU per replay in the round-5 trace): every step's work is in the graph
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph):
-        iteration()
+        for _ in range(SELFPLAY_GRAPH_STEPS):
+            iteration()
     graph.replay()
     torch.cuda.synchronize(dev)
     barrier(dev)
+    iters = max(SELFPLAY_GRAPH_STEPS, iters - iters % SELFPLAY_GRAPH_STEPS)
     region_mark("config5_selfplay", "start")
     t0 = time.perf_counter()
-    for _ in range(iters):
+    for _ in range(iters // SELFPLAY_GRAPH_STEPS):
         graph.replay()
     torch.cuda.synchronize(dev)
     region_mark("config5_selfplay", "end")
@@ -359,7 +367,8 @@ def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
                          "traffic": None},
             "config": {"workload": f"BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused, precision "
                                    f"{precision}) + DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of "
-                                   "12 frozen snapshots per episode, greedy, same precision), reset after done; hipGraph replays",
+                                   "12 frozen snapshots per episode, greedy, same precision), reset after done; hipGraph replays "
+                                   f"of {SELFPLAY_GRAPH_STEPS} dual steps",
                        "tables_per_gpu": N, "weights": "reference checkpoint runs/ppo_splendor/ppo_splendor_latest.pt"}}
 
 

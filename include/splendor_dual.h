@@ -40,6 +40,10 @@ typedef struct {
     /* optional opponent_obs: done ? final_obs : obs, int32 [n][297] (NULL = skip) */
     const int32_t *obs, *final_obs;
     int32_t *opp_obs;
+    /* optional: incremented by one after the dual step (one device thread; NULL = skip).  A
+     * graph-captured rollout loop passes it as the next step's policy ply_base (spl_act_args_t),
+     * so every replay draws fresh actions without a separate counter launch. */
+    int64_t *step_counter;
 } spl_dual_io_t;
 
 #define SPL_DUAL_ILLEGAL 0x01

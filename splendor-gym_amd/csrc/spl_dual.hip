@@ -69,12 +69,14 @@ struct Io {
     uint8_t *done;
     int8_t *ended_on;
     uint8_t *info;
+    int64_t *step_counter;
 };
 
 template <bool kDraw>
 __global__ __launch_bounds__(256) void k_dual_finish(int n, Io io, Draw d) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (i == 0 && io.step_counter) *io.step_counter += 1;  // read by the next step's launches only
     const uint8_t ta = io.ta[i], fa = io.fa[i], fb = io.fb[i];
     const bool ended_a = ta != 0, ended_b = !ended_a && io.tb[i] != 0;
     const bool passed = !ended_a && (fa & (SPL_F_ILLEGAL | SPL_F_OOB)) == 0;
@@ -148,7 +150,8 @@ static int dual_finish(int32_t n, const spl_dual_io_t *io, const spl_dual_draw_t
         return spl_fail(SPL_E_ARG, "observation buffers must be 16-byte aligned");
     const hipStream_t s = (hipStream_t)stream;
     const Io k{io->reward_a, io->reward_b, io->terminated_a, io->terminated_b, io->flags_a, io->flags_b, io->winner_a,
-               io->winner_b, io->agent_reward, io->opp_reward, io->done, io->game_ended_on, io->info_flags};
+               io->winner_b, io->agent_reward, io->opp_reward, io->done, io->game_ended_on, io->info_flags,
+               io->step_counter};
     if (draw) {
         const Draw d{draw->episode, draw->group_of, draw->group_prev, draw->pool_slots, draw->pool_len, draw->p_current,
                      draw->seed, draw->table0};

@@ -1197,50 +1197,69 @@ __global__ __launch_bounds__(256) void k_group_count(int n, int G, const int32_t
     if (threadIdx.x < G && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
 }
 
-// per group g: gtab[g] its first full (128-table) workgroup of k_act32, gtab[G + 1 + g] its first
-// position in `order`, ntab[g] its first narrow (16-table tail) workgroup of k_act32_narrow
-__global__ __launch_bounds__(64) void k_group_scan(int G, int32_t *counts, int32_t *cursor, int32_t *gtab) {
-    if (threadIdx.x != 0) return;
-    int32_t *ntab = gtab + 2 * G + 2;
-    int wg = 0, nw = 0, pos = 0;
-    for (int g = 0; g < G; ++g) {
-        gtab[g] = wg;
-        ntab[g] = nw;
-        gtab[G + 1 + g] = pos;
-        cursor[g] = pos;
-        const int c = counts[g];
-        counts[g] = 0;  // ready for the next call's k_group_count (no memset launch)
-        wg += c / kRowsPerBlock;
-        nw += (c % kRowsPerBlock + kRowsPerWave - 1) / kRowsPerWave;
-        pos += c;
-    }
-    gtab[G] = wg;
-    ntab[G] = nw;
-    gtab[2 * G + 1] = pos;
-}
-
-// Tables into their group's range of `order` (order within a group is irrelevant).  Ranks are
-// taken in LDS and each workgroup reserves its span of every group with ONE global atomic: one
-// global atomic per table on a dozen hot addresses serialises in L2 (about 0.3 ms for 65 536
-// tables over 13 groups).
-__global__ __launch_bounds__(256) void k_group_scatter(int n, int G, const int32_t *group_of, int32_t *cursor,
-                                                       int32_t *order) {
-    __shared__ int32_t cnt[64], base[64];
+// Tables into their group's range of `order` (order within a group is irrelevant), the group scan
+// included: every workgroup derives the groups' starts from the final counts itself (G <= 64, one
+// pass by one thread) instead of a separate one-thread scan launch (a launch of its own cost ~4.6 us
+// in the config-5 dual step's trace).  Ranks are taken in LDS and each workgroup reserves its span of
+// every group with ONE global atomic on cursor[g] (relative to the group's start): one global atomic
+// per table on a dozen hot addresses serialises in L2 (about 0.3 ms for 65 536 tables over 13
+// groups).  Workgroup 0 writes the launch tables: gtab[g] the group's first full (128-table)
+// workgroup of k_act32, gtab[G + 1 + g] its first position in `order`, ntab[g] its first narrow
+// (16-table tail) workgroup of k_act32_narrow.  The last workgroup to finish (ticket) zeroes counts
+// and cursors for the next call's k_group_count (no memset launch).
+__global__ __launch_bounds__(256) void k_group_place(int n, int G, const int32_t *group_of, int32_t *counts,
+                                                     int32_t *cursor, int32_t *gtab, int32_t *ticket, int32_t *order) {
+    __shared__ int32_t cnt[64], base[64], start[64];
+    __shared__ int last;
     if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        int pos = 0;
+        for (int g = 0; g < G; ++g) {
+            start[g] = pos;
+            pos += counts[g];
+        }
+        if (blockIdx.x == 0) {
+            int32_t *ntab = gtab + 2 * G + 2;
+            int wg = 0, nw = 0;
+            for (int g = 0; g < G; ++g) {
+                const int c = counts[g];
+                gtab[g] = wg;
+                ntab[g] = nw;
+                gtab[G + 1 + g] = start[g];
+                wg += c / kRowsPerBlock;
+                nw += (c % kRowsPerBlock + kRowsPerWave - 1) / kRowsPerWave;
+            }
+            gtab[G] = wg;
+            ntab[G] = nw;
+            gtab[2 * G + 1] = pos;
+        }
+    }
     __syncthreads();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int g = i < n ? group_of[i] : -1;
     const bool in = g >= 0 && g < G;
     const int rank = in ? atomicAdd(&cnt[g], 1) : 0;
     __syncthreads();
-    if (threadIdx.x < G && cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
+    if (threadIdx.x < G && cnt[threadIdx.x]) base[threadIdx.x] = start[threadIdx.x] + atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
     __syncthreads();
     if (in) order[base[g] + rank] = i;
+    if (threadIdx.x == 0) {  // this workgroup's reads of counts and cursors are done
+        __threadfence();
+        last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last) {
+        if (threadIdx.x < G) {
+            counts[threadIdx.x] = 0;
+            cursor[threadIdx.x] = 0;
+        }
+        if (threadIdx.x == 0) *ticket = 0;
+    }
 }
 
 constexpr int kMaxGroups = 64;
 
-int64_t splp32_group_scratch(int32_t n, int32_t groups) { return 4 * ((int64_t)5 * groups + 3 + n); }
+int64_t splp32_group_scratch(int32_t n, int32_t groups) { return 4 * ((int64_t)5 * groups + 4 + n); }
 
 template <template <bool, bool> class K>
 struct ActKernels {  // the four instantiations of one format's kernel template
@@ -1275,14 +1294,13 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
     if (groups > 0) {  // sort the tables by network, then one workgroup per 128 tables of one group
         if (groups > kMaxGroups) return spl_fail(SPL_E_ARG, "at most 64 networks per grouped call");
         if (critic) return spl_fail(SPL_E_ARG, "grouped evaluation serves actor-only images");
-        // scratch: counts[G] | cursor[G] | gtab[2G + 2] | ntab[G + 1] | order[n]
+        // scratch: counts[G] | cursor[G] | gtab[2G + 2] | ntab[G + 1] | ticket | order[n]
         int32_t *counts = static_cast<int32_t *>(scratch), *cursor = counts + groups, *gtab = cursor + groups;
-        int32_t *order = gtab + 2 * groups + 2 + groups + 1;
+        int32_t *ticket = gtab + 2 * groups + 2 + groups + 1, *order = ticket + 1;
         const hipStream_t s = (hipStream_t)stream;
         const dim3 g256((unsigned)((n + 255) / 256));
         hipLaunchKernelGGL(k_group_count, g256, dim3(256), 0, s, n, groups, group_of, counts);
-        hipLaunchKernelGGL(k_group_scan, dim3(1), dim3(64), 0, s, groups, counts, cursor, gtab);
-        hipLaunchKernelGGL(k_group_scatter, g256, dim3(256), 0, s, n, groups, group_of, cursor, order);
+        hipLaunchKernelGGL(k_group_place, g256, dim3(256), 0, s, n, groups, group_of, counts, cursor, gtab, ticket, order);
         a.order = order;
         a.gtab = gtab;
         a.groups = groups;

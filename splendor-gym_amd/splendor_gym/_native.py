@@ -64,7 +64,8 @@ class DualIo(ctypes.Structure):
     """spl_dual_io_t (include/splendor_dual.h)"""
     _fields_ = [(k, c_void_p) for k in ("reward_a", "reward_b", "terminated_a", "terminated_b", "flags_a", "flags_b",
                                         "winner_a", "winner_b", "agent_reward", "opp_reward", "done",
-                                        "game_ended_on", "info_flags", "obs", "final_obs", "opp_obs")]
+                                        "game_ended_on", "info_flags", "obs", "final_obs", "opp_obs",
+                                        "step_counter")]
 
 
 class DualDraw(ctypes.Structure):

@@ -69,7 +69,10 @@ class DualInfo(Mapping):
 
 class DualStepVectorEnv:
     def __init__(self, num_envs, device=None, opponent="random", policy_seed=0, refill_period=None, table0=0,
-                 opponent_obs=True, random_starts=False):
+                 opponent_obs=True, random_starts=False, step_counter=None):
+        """step_counter: optional int64 [1] device tensor that every dual_step increments by one in its
+        last launch (spl_dual_io_t.step_counter) — a graph-captured rollout loop passes it to the
+        agent's act as ply_base, so each replay draws fresh actions without a counter launch."""
         if isinstance(opponent, str) and opponent not in _DEVICE_POLICIES:
             raise ValueError(f"unknown device opponent {opponent!r}; choose {sorted(_DEVICE_POLICIES)} or a callable")
         self.eng = Engine(num_envs, 2, device=device, refill_period=refill_period, table0=table0)
@@ -108,7 +111,12 @@ class DualStepVectorEnv:
                                   winner_b=p(e.winner), agent_reward=p(self.agent_reward),
                                   opp_reward=p(self.opp_reward), done=p(self.done),
                                   game_ended_on=p(self.game_ended_on), info_flags=p(self.info_flags),
-                                  obs=p(e.obs), final_obs=p(e.final_obs), opp_obs=p(self.opp_obs))
+                                  obs=p(e.obs), final_obs=p(e.final_obs), opp_obs=p(self.opp_obs),
+                                  step_counter=p(step_counter))
+        if step_counter is not None and not (step_counter.dtype == torch.int64 and step_counter.numel() == 1
+                                             and step_counter.device == self.device):
+            raise ValueError("step_counter must be an int64 [1] tensor on the env's device")
+        self._step_counter = step_counter
         self._ply = 0
 
     # ------------------------------------------------------------------------------------

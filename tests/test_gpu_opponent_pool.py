@@ -228,3 +228,27 @@ def test_snapshot_in_play_is_not_overwritten():
     playing.zero_()
     pool.add_snapshot(ms[2])  # nothing busy: the ring position moves on, reusing freed slots
     assert pool.pool[-1] != n0
+
+
+def test_grouped_calls_reuse_their_scratch():
+    """Back-to-back grouped calls on ONE scratch block with different groupings (and group counts of
+    zero): the placing kernel derives each call's group starts itself and its last workgroup zeroes
+    the counts, cursors and ticket for the next call — every call must still give each table its own
+    network's action."""
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic, OpponentPool
+    ms = models(4, seed=21)
+    pool = OpponentPool(ms[0], pool_size=3)
+    for m in ms[1:]:
+        pool.add_snapshot(m)
+    n = 3000
+    obs, mask = states(n, seed=5)
+    want = [FusedActorCritic(m, with_critic=False).greedy(obs, mask) for m in ms]
+    gen = torch.Generator(device="cpu").manual_seed(3)
+    for call in range(4):
+        hi = 4 if call != 2 else 2  # call 2 leaves groups 2 and 3 empty
+        g = torch.randint(0, hi, (n,), generator=gen, dtype=torch.int32).to(obs.device)
+        out = pool.act(obs, mask, g)
+        for i in range(4):
+            sel = g == i
+            assert torch.equal(out[sel], want[i][sel]), (call, i)

@@ -79,17 +79,16 @@ def main():
             opponent = FusedActorCritic(opp_model, with_critic=False, precision=prec).opponent()
     else:
         opponent = greedy_opponent_from(opp_model)
-    env = DualStepVectorEnv(N, device=dev, opponent=opponent, table0=rank * N, opponent_obs=False)
+    ply_t = torch.zeros(1, dtype=torch.int64, device=dev)  # advanced by each dual step's last launch
+    env = DualStepVectorEnv(N, device=dev, opponent=opponent, table0=rank * N, opponent_obs=False,
+                            step_counter=ply_t if fused else None)
     obs, info = env.reset(seed=rank * N)
     mask = info["action_mask"]
     amp = torch.autocast("cuda", dtype=torch.bfloat16) if (args.bf16 and not fused) else torch.autocast("cuda", enabled=False)
 
-    ply_t = torch.zeros(1, dtype=torch.int64, device=dev)  # advanced inside the graph: fresh draws per replay
-
     def iteration(with_actor=True):
         with torch.no_grad(), amp:
             if with_actor and fused:
-                ply_t.add_(1)
                 a, logprob, entropy, value = agent_k.act(obs, mask, seed=1234, table0=rank * N, ply_base=ply_t)
             elif with_actor:
                 action, logprob, _, value = agent.get_action_and_value(obs.float(), mask.float())
