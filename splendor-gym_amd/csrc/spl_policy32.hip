@@ -262,6 +262,9 @@ struct ActArgs {
     const int32_t *gtab;
     int groups;
     int64_t image_stride;
+    // grouped launches: counts[G] | cursor[G] of the grouping scratch, zeroed by workgroup 0 for the
+    // next call's k_group_count (k_group_place has consumed them)
+    int32_t *group_reset;
 };
 
 // tanh in fp32 without branches, to a few ulp everywhere (the exact format's): |x| < 0.625:
@@ -738,6 +741,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     // rows [rbase, rend) of this workgroup: tables rbase.. directly, or positions of the grouped
     // order (one network per workgroup: the group whose workgroup range holds blockIdx.x)
     int64_t rbase = (int64_t)blockIdx.x * kRowsPerBlock, rend = a.n;
+    if (a.group_reset && blockIdx.x == 0 && threadIdx.x < 2 * a.groups) a.group_reset[threadIdx.x] = 0;
     if (a.order) {
         const int b = (int)blockIdx.x;
         if (b >= a.gtab[a.groups]) return;  // past the last group's workgroups (every wave leaves)
@@ -1205,24 +1209,26 @@ __global__ __launch_bounds__(256) void k_group_count(int n, int G, const int32_t
 // per table on a dozen hot addresses serialises in L2 (about 0.3 ms for 65 536 tables over 13
 // groups).  Workgroup 0 writes the launch tables: gtab[g] the group's first full (128-table)
 // workgroup of k_act32, gtab[G + 1 + g] its first position in `order`, ntab[g] its first narrow
-// (16-table tail) workgroup of k_act32_narrow.  The last workgroup to finish (ticket) zeroes counts
-// and cursors for the next call's k_group_count (no memset launch).
-__global__ __launch_bounds__(256) void k_group_place(int n, int G, const int32_t *group_of, int32_t *counts,
-                                                     int32_t *cursor, int32_t *gtab, int32_t *ticket, int32_t *order) {
-    __shared__ int32_t cnt[64], base[64], start[64];
-    __shared__ int last;
+// (16-table tail) workgroup of k_act32_narrow.  The grouped k_act32 launch that follows zeroes
+// counts and cursors for the next call's k_group_count (ActArgs.group_reset: no memset launch, and
+// no last-workgroup ticket here — 256 serialised atomics on one word cost this kernel ~7 us).
+__global__ __launch_bounds__(256) void k_group_place(int n, int G, const int32_t *group_of, const int32_t *counts,
+                                                     int32_t *cursor, int32_t *gtab, int32_t *order) {
+    __shared__ int32_t cnt[64], base[64], start[64], tot[64];
     if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+    if (threadIdx.x < G) tot[threadIdx.x] = counts[threadIdx.x];  // one batch of loads, not G dependent trips
+    __syncthreads();
     if (threadIdx.x == 0) {
         int pos = 0;
         for (int g = 0; g < G; ++g) {
             start[g] = pos;
-            pos += counts[g];
+            pos += tot[g];
         }
         if (blockIdx.x == 0) {
             int32_t *ntab = gtab + 2 * G + 2;
             int wg = 0, nw = 0;
             for (int g = 0; g < G; ++g) {
-                const int c = counts[g];
+                const int c = tot[g];
                 gtab[g] = wg;
                 ntab[g] = nw;
                 gtab[G + 1 + g] = start[g];
@@ -1243,23 +1249,11 @@ __global__ __launch_bounds__(256) void k_group_place(int n, int G, const int32_t
     if (threadIdx.x < G && cnt[threadIdx.x]) base[threadIdx.x] = start[threadIdx.x] + atomicAdd(&cursor[threadIdx.x], cnt[threadIdx.x]);
     __syncthreads();
     if (in) order[base[g] + rank] = i;
-    if (threadIdx.x == 0) {  // this workgroup's reads of counts and cursors are done
-        __threadfence();
-        last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
-    }
-    __syncthreads();
-    if (last) {
-        if (threadIdx.x < G) {
-            counts[threadIdx.x] = 0;
-            cursor[threadIdx.x] = 0;
-        }
-        if (threadIdx.x == 0) *ticket = 0;
-    }
 }
 
 constexpr int kMaxGroups = 64;
 
-int64_t splp32_group_scratch(int32_t n, int32_t groups) { return 4 * ((int64_t)5 * groups + 4 + n); }
+int64_t splp32_group_scratch(int32_t n, int32_t groups) { return 4 * ((int64_t)5 * groups + 3 + n); }
 
 template <template <bool, bool> class K>
 struct ActKernels {  // the four instantiations of one format's kernel template
@@ -1294,13 +1288,14 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
     if (groups > 0) {  // sort the tables by network, then one workgroup per 128 tables of one group
         if (groups > kMaxGroups) return spl_fail(SPL_E_ARG, "at most 64 networks per grouped call");
         if (critic) return spl_fail(SPL_E_ARG, "grouped evaluation serves actor-only images");
-        // scratch: counts[G] | cursor[G] | gtab[2G + 2] | ntab[G + 1] | ticket | order[n]
+        // scratch: counts[G] | cursor[G] | gtab[2G + 2] | ntab[G + 1] | order[n]
         int32_t *counts = static_cast<int32_t *>(scratch), *cursor = counts + groups, *gtab = cursor + groups;
-        int32_t *ticket = gtab + 2 * groups + 2 + groups + 1, *order = ticket + 1;
+        int32_t *order = gtab + 2 * groups + 2 + groups + 1;
         const hipStream_t s = (hipStream_t)stream;
         const dim3 g256((unsigned)((n + 255) / 256));
         hipLaunchKernelGGL(k_group_count, g256, dim3(256), 0, s, n, groups, group_of, counts);
-        hipLaunchKernelGGL(k_group_place, g256, dim3(256), 0, s, n, groups, group_of, counts, cursor, gtab, ticket, order);
+        hipLaunchKernelGGL(k_group_place, g256, dim3(256), 0, s, n, groups, group_of, counts, cursor, gtab, order);
+        a.group_reset = counts;  // counts[G] | cursor[G], zeroed by the k_act32 launch below
         a.order = order;
         a.gtab = gtab;
         a.groups = groups;

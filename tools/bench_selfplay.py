@@ -33,6 +33,7 @@ def main():
                     help="fused: spl_policy_act (fp32-accurate split-bf16 kernel, bf16 with --bf16) for agent and opponent; "
                          "torch: the nn.Module")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-steps", type=int, default=4, help="dual steps captured per hipGraph (bench.py: 4)")
     ap.add_argument("--opponent", choices=["pool", "frozen"], default="pool",
                     help="pool: the reference's opponent_supplier (current policy p=0.25, else one of 12 frozen "
                          "snapshots, drawn per episode; fused fp32 grouped kernel); frozen: one frozen greedy actor")
@@ -111,7 +112,8 @@ def main():
             torch.cuda.current_stream(dev).wait_stream(s)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
-                iteration()
+                for _ in range(args.graph_steps):
+                    iteration()
         except Exception as exc:  # capture unsupported: eager
             print(f"graph capture failed ({exc}); timing eager iterations", file=sys.stderr)
             graph = None
@@ -126,7 +128,9 @@ def main():
         barrier(dev)
         return max_over_ranks(time.perf_counter() - t0, device=dev)
 
-    full = timed(graph.replay if graph is not None else iteration, args.iters)
+    if graph is not None:  # whole graphs of graph_steps dual steps
+        args.iters = max(args.graph_steps, args.iters - args.iters % args.graph_steps)
+    full = (timed(graph.replay, args.iters // args.graph_steps) if graph is not None else timed(iteration, args.iters))
     env_only = timed(lambda: iteration(with_actor=False), args.iters)
     if rank == 0:
         steps = 2 * N * world * args.iters

@@ -57,6 +57,11 @@ for step in "$@"; do
               bash tools/pmc.sh ${TAG}_4p_32768 4 32768 store all || exit 1 ;;
     steptests) run pytest_step 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_env_api.py \
                    tests/test_gpu_opponent_pool.py -x -v --timeout 200 --timeout-method thread ;;
+    sptrace)  # kernel timeline of the config-5 dual step (pool opponent), one dual step per graph replay
+      run sptrace 300 rocprofv3 --kernel-trace --output-format csv -d $O/prof_sptrace_$TAG -o run -- \
+          python3 tools/bench_selfplay.py --opponent pool
+      python3 tools/dual_step_timeline.py $(find $O/prof_sptrace_$TAG -name '*kernel_trace.csv' | head -1) \
+          > $O/selfplay_trace_$TAG.txt && tail -14 $O/selfplay_trace_$TAG.txt ;;
     spprof) bash tools/gpu_sp_prof.sh || exit 1 ;;
     poolsize) for ps in 0 1 3 6 12; do run sps_$ps 200 python3 tools/bench_selfplay.py --opponent pool --pool-size $ps; done ;;
     pmcfinal)  # HBM traffic (FETCH_SIZE, WRITE_SIZE passes) of every kernel bench.py's lines quote, final tree
