@@ -67,8 +67,8 @@
 #define SPL_P32_SPREAD 1
 #endif
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
-// streaming, no per-tile barrier), 4 A fragments loaded once per tile (no per-group LDS reads),
-// 16 the ring without its per-chunk barrier (waves race the slots)
+// streaming: no LDS-DMA piece after the prologue, no per-tile barrier), 4 A fragments loaded once
+// per tile (no per-group LDS reads), 16 the ring without its barriers (waves race the slots)
 #ifndef SPL_POL_ABL
 #define SPL_POL_ABL 0
 #endif
@@ -824,7 +824,8 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     int dnext = 0;
     auto tick = [&](int s, int ks, int odd) {  // after k-step s of a tile of ks k-steps (s, ks, odd known at compile time)
         constexpr int kLast = G::kBlocksPerWave - 1;
-        if (odd) return;
+        constexpr bool kNoStream = (SPL_POL_ABL & 2) != 0;  // ablation 2: no streaming at all
+        if (odd || kNoStream) return;
         if (s < 2 * kLast) {
             const int j = s / kLast, blk = wave + kWaves * (s % kLast), ch = min(dnext + j, kTotal - 1);
             __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_void *)(ring + ((dnext + j) % kSlots) * kChunk + blk * 1024),
@@ -859,7 +860,7 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
         // slots; odd c just moves on to the next slot
         if ((c & 1) == 0) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
+            if (!(SPL_POL_ABL & 16)) __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
 #if !SPL_P32_SPREAD
 #pragma unroll
