@@ -553,14 +553,16 @@ def test_rollout_store_delegation_multiplayer(players):
 
 def test_dual_step_vector_env_matches_per_env_wrappers():
     """DualStepVectorEnv (fused device greedy_v1 opponent) == per-env DualStepNativeWrapper over
-    SplendorEnv with the host greedy_opponent_v1, including the PPO loop's reset after done."""
+    SplendorEnv with the host greedy_opponent_v1, including the PPO loop's reset after done; the
+    optional step counter (spl_dual_io_t.step_counter) advances by one per dual step."""
     import torch
     from splendor_gym.envs import SplendorEnv
     from splendor_gym.opponents import greedy_opponent_v1
     from splendor_gym.selfplay import DualStepVectorEnv
     from splendor_gym.wrappers import DualStepNativeWrapper
     n, steps, seed = 6, 150, 40
-    vec = DualStepVectorEnv(n, opponent="greedy_v1")
+    counter = torch.full((1,), 7, dtype=torch.int64, device="cuda")
+    vec = DualStepVectorEnv(n, opponent="greedy_v1", step_counter=counter)
     obs_v, info_v = vec.reset(seed=seed)
     envs = [DualStepNativeWrapper(SplendorEnv(), opponent_policy=greedy_opponent_v1, random_starts=False)
             for _ in range(n)]
@@ -587,6 +589,7 @@ def test_dual_step_vector_env_matches_per_env_wrappers():
                 per[i] = (a_obs, inf)
             assert np.array_equal(ao[i].cpu().numpy(), per[i][0]), (k, i)
     assert ended >= n  # every table finished at least one game and was re-dealt
+    assert int(counter.item()) == 7 + steps
 
 
 def test_dual_step_callable_opponent_and_illegal_actions():
