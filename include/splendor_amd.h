@@ -143,7 +143,9 @@ int spl_ctx_set_refill_fused(spl_ctx_t *ctx, int fused);
  * and stores the step's outputs) vs one wave per 64 tables (0).  1 (default) = auto: the six-wave
  * dealer variant (5) when every 128-table workgroup of it is resident at once (one per CU, e.g.
  * 32 768 tables), else the three-wave dealer variant (4: a third wave deals the pool refills beside the
- * other two) when it fits, else two-wave at 64 tables per workgroup; 2 = two-wave at 64; 3 = two-wave
+ * other two) when it fits, else at 2 players the quad variant (6) when every 256-table workgroup of it
+ * is resident at once (e.g. the headline's 65 536 tables), else two-wave at 64 tables per workgroup;
+ * 2 = two-wave at 64; 3 = two-wave
  * at 32; 4 = the three-wave dealer variant; 5 = the six-wave dealer variant (two dealer teams per
  * 128-table workgroup, roles given to waves by the SIMD they run on); 6 = the quad variant (four
  * two-wave teams per 256-table workgroup, one workgroup per CU, roles by SIMD; the partner hand-off
@@ -159,9 +161,10 @@ int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on);
  * Turned off for grids larger than the resident workgroup capacity (pairs might not run together).
  * Default: SPL_DELEG_EVERY (DESIGN.md §2 gives the measured A/B).  Results are identical either way. */
 int spl_ctx_set_rollout_delegation(spl_ctx_t *ctx, int every);
-/* Partner hand-off of the six-wave dealer's rollout store (k_rollout_store_dealer2_<P>p: per-step
- * outputs, one 384-thread workgroup per CU, grids resident at once; the two-wave kernels have none since
- * ABI 7's round-5 library): a 64-table team that falls `lead` or more steps behind the same team of the
+/* Partner hand-off of the rollout store in the kernels that run one workgroup per CU with the grid
+ * resident at once: the six-wave dealer (k_rollout_store_dealer2_<P>p, 384 threads) and the quad
+ * variant (k_rollout_store_quad_<P>p, 512 threads); the two-wave kernels (several workgroups per CU)
+ * have none since the round-5 library: a 64-table team that falls `lead` or more steps behind the same team of the
  * workgroup on the neighbouring XCC hands whole steps of observation rows (its state words, ~6 KB) to
  * that team's output wave, which encodes and stores them between its own steps (the XCCs drain the
  * rollout store at different rates under load).  0 = off, -1 = hand off whenever a slot
