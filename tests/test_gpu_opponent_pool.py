@@ -252,3 +252,31 @@ def test_grouped_calls_reuse_their_scratch():
         for i in range(4):
             sel = g == i
             assert torch.equal(out[sel], want[i][sel]), (call, i)
+
+
+def test_grouped_act_at_the_maximum_network_count():
+    """A pool at its largest (pool_size 61: 64 images, the grouping kernels' LDS tables and the
+    act launch's counter reset at their bounds): every table's action equals its network's own."""
+    import torch
+    from splendor_gym.fused_policy import FusedActorCritic, OpponentPool
+    ms = models(4, seed=31)
+    pool = OpponentPool(ms[0], pool_size=61)
+    assert pool.n_images == pool.MAX_IMAGES
+    for i in range(61):  # the snapshots cycle through three networks
+        pool.add_snapshot(ms[1 + i % 3])
+    assert len(pool.pool) == 61
+    slots = [0] + list(pool.pool)  # image slot of the current policy, then of each snapshot
+    net_of = {0: 0} | {slot: 1 + i % 3 for i, slot in enumerate(pool.pool)}
+    n = 6000
+    obs, mask = states(n, seed=9)
+    want = [FusedActorCritic(m, with_critic=False).greedy(obs, mask) for m in ms]
+    gen = torch.Generator(device="cpu").manual_seed(11)
+    for call in range(2):
+        pick = torch.randint(0, len(slots), (n,), generator=gen)
+        g = torch.tensor(slots, dtype=torch.int32)[pick].to(obs.device)
+        out = pool.act(obs, mask, g)
+        gi = g.cpu().numpy()
+        for slot in slots:
+            sel = torch.from_numpy(gi == slot).to(obs.device)
+            if sel.any():
+                assert torch.equal(out[sel], want[net_of[slot]][sel]), (call, slot)
