@@ -75,8 +75,13 @@ class DualStepVectorEnv:
         agent's act as ply_base, so each replay draws fresh actions without a counter launch."""
         if isinstance(opponent, str) and opponent not in _DEVICE_POLICIES:
             raise ValueError(f"unknown device opponent {opponent!r}; choose {sorted(_DEVICE_POLICIES)} or a callable")
+        if step_counter is not None and not (step_counter.dtype == torch.int64 and step_counter.numel() == 1):
+            raise ValueError("step_counter must be an int64 [1] tensor on the env's device")
         self.eng = Engine(num_envs, 2, device=device, refill_period=refill_period, table0=table0)
         self.num_envs, self.device = num_envs, self.eng.device
+        if step_counter is not None and step_counter.device != self.device:
+            self.eng.close()
+            raise ValueError("step_counter must be an int64 [1] tensor on the env's device")
         self.opponent = opponent
         self.policy_seed = int(policy_seed)
         self.want_opp_obs = opponent_obs
@@ -113,10 +118,7 @@ class DualStepVectorEnv:
                                   game_ended_on=p(self.game_ended_on), info_flags=p(self.info_flags),
                                   obs=p(e.obs), final_obs=p(e.final_obs), opp_obs=p(self.opp_obs),
                                   step_counter=p(step_counter))
-        if step_counter is not None and not (step_counter.dtype == torch.int64 and step_counter.numel() == 1
-                                             and step_counter.device == self.device):
-            raise ValueError("step_counter must be an int64 [1] tensor on the env's device")
-        self._step_counter = step_counter
+        self._step_counter = step_counter  # the launches point at it
         self._ply = 0
 
     # ------------------------------------------------------------------------------------
