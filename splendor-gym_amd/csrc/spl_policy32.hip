@@ -68,7 +68,8 @@
 #endif
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
 // streaming: no LDS-DMA piece after the prologue, no per-tile barrier), 4 A fragments loaded once
-// per tile (no per-group LDS reads), 16 the ring without its barriers (waves race the slots)
+// per tile (no per-group LDS reads), 16 the ring without its barriers (waves race the slots), 32 no
+// per-table epilogue (no softmax / sample / argmax)
 #ifndef SPL_POL_ABL
 #define SPL_POL_ABL 0
 #endif
@@ -663,65 +664,101 @@ constexpr int kAheadL1 = 2, kAheadHid = SPL_P32_AHEAD2;
 
 // The per-table epilogue over one table's 45 logits (`row`) and mask bytes: greedy masked argmax
 // (training_utils.py:263-276) or masked_categorical's sample, log-prob and entropy, plus the critic
-// value (ppo_splendor.py:40-59).
+// value (ppo_splendor.py:40-59).  Called by every lane of the wave: the four lanes r, r+16, r+32,
+// r+48 (lane group g) share table r's row, lane group g taking actions 12g .. 12g+11, and combine
+// through shuffles (one lane per table had left three quarters of the wave idle through 45 accurate
+// expf and the sampling scan: ~7 % of the exact sample+critic kernel, timing ablation bit 32).
+// Results: the greedy action is the same first maximum; the softmax sums are taken per lane group
+// and then added ((S0 + S1) + (S2 + S3)), and the sampling scan of group g starts from the sum of the
+// groups before it, so a draw can land on the other side of a boundary only where the two summation
+// orders round differently.  Only lanes of group 0 with `ok` (a row of this wave) write.
 template <bool kCritic, bool kSample>
-__device__ __forceinline__ void act_epilogue(const ActArgs &a, const float *row, const uint8_t *mrow, int64_t t,
-                                             float value) {
-    float lv[kAct];
-    uint64_t legal = 0;
+__device__ __forceinline__ void act_epilogue4(const ActArgs &a, const float *row, const uint8_t *mrow, int64_t t,
+                                              float value, int g, bool ok) {
+    constexpr int kPer = 12;  // actions per lane group (45 = 12 + 12 + 12 + 9)
+    const int k0 = kPer * g, r = threadIdx.x & 15;
+    float lv[kPer];
+    uint32_t legal = 0u, inr = 0u;
 #pragma unroll
-    for (int k = 0; k < kAct; ++k) {
-        lv[k] = row[k];
-        legal |= (uint64_t)(mrow[k] != 0) << k;
+    for (int j = 0; j < kPer; ++j) {
+        const int k = k0 + j;
+        const bool in = k < kAct;
+        lv[j] = in ? row[in ? k : 0] : 0.f;
+        legal |= (uint32_t)(in && mrow[in ? k : 0] != 0) << j;
+        inr |= (uint32_t)in << j;
     }
-    int act = 0;
+    int act;
     if constexpr (!kSample) {
         // logits.masked_fill(mask < 0.5, -inf).argmax(): first maximum; all-illegal -> 0
         float best = -__builtin_inff();
+        int bk = kAct;
 #pragma unroll
-        for (int k = 0; k < kAct; ++k) {
-            const bool better = ((legal >> k) & 1) && lv[k] > best;
-            best = better ? lv[k] : best;
-            act = better ? k : act;
+        for (int j = 0; j < kPer; ++j) {
+            const bool better = ((legal >> j) & 1) && lv[j] > best;
+            best = better ? lv[j] : best;
+            bk = better ? k0 + j : bk;
         }
+#pragma unroll
+        for (int off = 16; off <= 32; off <<= 1) {  // larger value, then the smaller action
+            const float ob = __shfl_xor(best, off);
+            const int ok_ = __shfl_xor(bk, off);
+            const bool take = ob > best || (ob == best && ok_ < bk);
+            best = take ? ob : best;
+            bk = take ? ok_ : bk;
+        }
+        act = bk < kAct ? bk : 0;
     } else {
         // masked_categorical: illegal -> -inf unless the row has no legal action; fp32 softmax
-        const uint64_t allow = legal ? legal : (1ull << kAct) - 1;
+        int any = legal != 0u;
+        any |= __shfl_xor(any, 16);
+        any |= __shfl_xor(any, 32);
+        const uint32_t allow = any ? legal : inr;
         float mx = -__builtin_inff();
 #pragma unroll
-        for (int k = 0; k < kAct; ++k) mx = ((allow >> k) & 1) ? fmaxf(mx, lv[k]) : mx;
-        float S = 0.f, T = 0.f;
+        for (int j = 0; j < kPer; ++j) mx = ((allow >> j) & 1) ? fmaxf(mx, lv[j]) : mx;
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float Sg = 0.f, Tg = 0.f;
 #pragma unroll
-        for (int k = 0; k < kAct; ++k) {
-            const float d = lv[k] - mx, p = ((allow >> k) & 1) ? expf(d) : 0.f;
-            lv[k] = p;
-            S += p;
-            T += p * d;
+        for (int j = 0; j < kPer; ++j) {
+            const float d = lv[j] - mx, p = ((allow >> j) & 1) ? expf(d) : 0.f;
+            lv[j] = p;
+            Sg += p;
+            Tg += p * d;
         }
+        float S = Sg + __shfl_xor(Sg, 16), T = Tg + __shfl_xor(Tg, 16);  // (S0 + S1), (S2 + S3)
+        S += __shfl_xor(S, 32);
+        T += __shfl_xor(T, 32);
         const float logS = logf(S);
         const uint64_t ply = a.ply + (a.ply_base ? *a.ply_base : 0ull);
         const uint4 rnd = philox4x32(make_uint4((uint32_t)(a.table0 + t), (uint32_t)((uint64_t)(a.table0 + t) >> 32),
                                                 (uint32_t)ply, (uint32_t)(ply >> 32)),
                                      make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32) ^ 0xA5C3E1F7u));
         const float target = (float)(rnd.x >> 8) * (1.f / 16777216.f) * S;
-        float cum = 0.f;
-        int last = 0;
-        bool found = false;
+        // the scan of group g starts from the groups before it, in order
+        const float s0 = __shfl(Sg, r), s1 = __shfl(Sg, r + 16), s2 = __shfl(Sg, r + 32);
+        float cum = g == 0 ? 0.f : g == 1 ? s0 : g == 2 ? s0 + s1 : (s0 + s1) + s2;
+        int hk = kAct, last = -1;
 #pragma unroll
-        for (int k = 0; k < kAct; ++k) {
-            const bool al = (allow >> k) & 1;
-            cum += lv[k];
-            last = al ? k : last;
-            const bool hit = al && !found && cum > target;
-            act = hit ? k : act;
-            found = found || hit;
+        for (int j = 0; j < kPer; ++j) {
+            const bool al = (allow >> j) & 1;
+            cum += lv[j];
+            last = al ? k0 + j : last;
+            hk = (al && hk == kAct && cum > target) ? k0 + j : hk;
         }
-        if (!found) act = last;
-        if (a.logprob) a.logprob[t] = row[act] - mx - logS;
-        if (a.entropy) a.entropy[t] = logS - T / S;
-        if (kCritic) a.value[t] = value;
+#pragma unroll
+        for (int off = 16; off <= 32; off <<= 1) {  // the first hit over the groups; the last allowed action
+            hk = min(hk, __shfl_xor(hk, off));
+            last = max(last, __shfl_xor(last, off));
+        }
+        act = hk < kAct ? hk : (last >= 0 ? last : 0);
+        if (g == 0 && ok) {
+            if (a.logprob) a.logprob[t] = row[act] - mx - logS;
+            if (a.entropy) a.entropy[t] = logS - T / S;
+            if (kCritic) a.value[t] = value;
+        }
     }
-    a.action[t] = act;
+    if (g == 0 && ok) a.action[t] = act;
 }
 
 // <false, false> greedy actor, <false, true> sampling actor, <true, true> critic + sampling actor
@@ -1043,7 +1080,14 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
         for (int i = lane; i < valid * kAct; i += 64)
             a.logits[table_of(i / kAct) * kAct + i % kAct] = lg[(i / kAct) * kLogitRow + i % kAct];
     }
-    if (g == 0 && r < valid) act_epilogue<kCritic, kSample>(a, lg + r * kLogitRow, ms + r * kAct, table_of(r), value);
+    if (SPL_POL_ABL & 32) {  // timing ablation: no per-table epilogue (action 0, value only)
+        if (g == 0 && r < valid) {
+            a.action[table_of(r)] = 0;
+            if (kCritic) a.value[table_of(r)] = value;
+        }
+        return;
+    }
+    act_epilogue4<kCritic, kSample>(a, lg + r * kLogitRow, ms + r * kAct, r < valid ? table_of(r) : 0, value, g, r < valid);
 }
 
 // the exact format's kernels keep round 3-4's names (k_act32<critic, sample>), the fp16-plane ones are k_act32h
@@ -1151,8 +1195,10 @@ __device__ __forceinline__ void act32_narrow_body(const uint8_t *__restrict__ Wb
         for (int i = lane; i < valid * kAct; i += 64)
             a.logits[(int64_t)a.order[tbase + i / kAct] * kAct + i % kAct] = lg[(i / kAct) * kLogitRow + i % kAct];
     }
-    if (wave == 0 && g == 0 && r < valid)
-        act_epilogue<false, kSample>(a, lg + r * kLogitRow, ms + r * kAct, (int64_t)__shfl(tid_own, r), 0.f);
+    if (wave == 0) {
+        const int64_t tab = (int64_t)__shfl(tid_own, r);
+        act_epilogue4<false, kSample>(a, lg + r * kLogitRow, ms + r * kAct, tab, 0.f, g, r < valid);
+    }
 }
 template <bool kSample>
 __global__ __launch_bounds__(kNarrowWaves * 64) void k_act32_narrow(const uint8_t *__restrict__ W, ActArgs a) {
