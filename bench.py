@@ -287,13 +287,17 @@ def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
     # the agent's sampling draws are keyed by (seed; table, ply_base): the dual step's last launch
     # advances ply_base (spl_dual_io_t.step_counter), so every captured step draws fresh actions
     ply_t = torch.zeros(1, dtype=torch.int64, device=dev)
-    env = DualStepVectorEnv(N, device=dev, opponent=pool, table0=rank * N, opponent_obs=False, step_counter=ply_t)
+    # the agent reads the env's compact uint8 copy of its observation (agent_obs_u8, written by the
+    # opponent's step beside the int32 obs dual_step returns): a quarter of the bytes
+    env = DualStepVectorEnv(N, device=dev, opponent=pool, table0=rank * N, opponent_obs=False, step_counter=ply_t,
+                            agent_obs_u8=True)
     obs, info = env.reset(seed=rank * N)
     mask = info["action_mask"]
+    agent_in = env.agent_obs_u8
 
     def iteration():
         with torch.no_grad():
-            a, _, _, _ = agent_k.act(obs, mask, seed=1234, table0=rank * N, ply_base=ply_t)
+            a, _, _, _ = agent_k.act(agent_in, mask, seed=1234, table0=rank * N, ply_base=ply_t)
             return env.dual_step(a)
 
     for _ in range(warmup):
@@ -335,12 +339,12 @@ def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
                "entropy": torch.empty(N, dtype=torch.float32, device=dev),
                "value": torch.empty(N, 1, dtype=torch.float32, device=dev)}
     with torch.no_grad():
-        agent_k.act(obs, mask, seed=77, table0=rank * N, out=act_out)
+        agent_k.act(agent_in, mask, seed=77, table0=rank * N, out=act_out)
         torch.cuda.synchronize(dev)
         region_mark("config5_actor", "start", "k_act32<true, true>", n_act)
         for i, (a, b) in enumerate(ev):
             a.record(strm)
-            agent_k.act(obs, mask, seed=77, ply=i, table0=rank * N, out=act_out)
+            agent_k.act(agent_in, mask, seed=77, ply=i, table0=rank * N, out=act_out)
             b.record(strm)
         torch.cuda.synchronize(dev)
         region_mark("config5_actor", "end")
@@ -368,7 +372,8 @@ def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
             "config": {"workload": f"BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused, precision "
                                    f"{precision}) + DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of "
                                    "12 frozen snapshots per episode, greedy, same precision), reset after done; hipGraph replays "
-                                   f"of {SELFPLAY_GRAPH_STEPS} dual steps",
+                                   f"of {SELFPLAY_GRAPH_STEPS} dual steps; the agent reads the compact uint8 copy of its "
+                                   "observation that the opponent's step writes beside the int32 rows",
                        "tables_per_gpu": N, "weights": "reference checkpoint runs/ppo_splendor/ppo_splendor_latest.pt"}}
 
 

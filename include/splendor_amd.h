@@ -44,7 +44,8 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 7  /* 7: spl_ctx_set_partner_lead, spl_debug_partner_stats (rollout-store partner hand-off);
+#define SPL_ABI_VERSION 8  /* 8: spl_step with both obs and obs_u8 writes both (the compact rows as a copy);
+                              7: spl_ctx_set_partner_lead, spl_debug_partner_stats (rollout-store partner hand-off);
                               6: SPL_F_FAULT + spl_ctx_faults (a lost hand-off in a rollout launch is reported);
                               5: spl_step_args_t.obs_u8 (compact observation), gate_terminated / gate_flags */
 
@@ -116,7 +117,9 @@ typedef struct spl_step_args_s {
                                 device consumer (spl_act_args_t.obs_u8), a quarter of obs's bytes:
                                 bytes 0..296 = obs (every value < 256 but move_count, byte 295 =
                                 move_count mod 256), byte 297 = move_count >> 8, 298-299 = 0.
-                                With obs_u8 set, obs must be NULL (only the bytes are written)     */
+                                With obs NULL only the bytes are written; with obs set too (ABI 8)
+                                both are, the bytes a copy of the rows (a fused actor's input
+                                beside the int32 observation the caller keeps)                   */
     const uint8_t *gate_terminated; /* [n] or NULL (spl_step only, with gate_flags): the dual step's
                                 gate fused into the opponent's move — where gate_terminated[t] != 0
                                 or gate_flags[t] has SPL_F_ILLEGAL / SPL_F_OOB (the agent's move

@@ -1096,6 +1096,52 @@ __device__ __forceinline__ void store_obs_u8_block(const uint8_t *rows_lds, int 
     for (int w = 4 * chunks + lane_id(); w < words; w += 64) reinterpret_cast<uint32_t *>(dst)[w] = src[w];
 }
 
+// The compact rows (spl_step_args_t.obs_u8 layout: 297 bytes, move_count >> 8, two zero bytes) of
+// the wave's staged 297-byte rows, stored beside their int32 block when a step writes both: 75 dwords
+// per row, consecutive lanes on consecutive dwords (256-byte stores); dword j < 74 of row r is the
+// staged bytes 297 r + 4 j .. + 3 (one v_alignbyte of the two staged dwords around them), dword 74
+// is byte 296, move_count >> 8 (`mhi` of lane r, whose table is row r), 0, 0.  Every lane runs
+// every iteration (the row's high byte comes by shuffle), the stores are predicated.  With a 16-byte
+// aligned dst each lane builds four consecutive dwords (one 16-byte store; a chunk crosses at most one
+// row end, whose dword 74 belongs to the chunk's first row), 19 iterations for 64 rows instead of 75.
+__device__ __forceinline__ void store_u8_from_rows(const uint8_t *rows_lds, int rows, uint8_t *dst, uint32_t mhi) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
+    uint32_t *out = reinterpret_cast<uint32_t *>(dst);
+    constexpr int kWords = kObsU8 / 4;  // 75
+    const int total = rows * kWords;
+    int q_first = 0;
+    if (((uintptr_t)dst & 15u) == 0) {
+        const int chunks = total >> 2;
+        v4i *out4 = reinterpret_cast<v4i *>(dst);
+        for (int it = 0; it < (chunks + 63) / 64; ++it) {
+            const int c = lane_id() + 64 * it, cc = c < chunks ? c : chunks - 1;
+            const int q0 = 4 * cc, r0 = q0 / kWords, j0 = q0 - kWords * r0;
+            const uint32_t h = (uint32_t)__shfl((int)mhi, r0);
+            v4i v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const bool next = j0 + i >= kWords;  // past row r0's end: row r0 + 1 from its byte 0
+                const int j = next ? j0 + i - kWords : j0 + i;
+                const int b = kObsDim * (next ? r0 + 1 : r0) + 4 * j;
+                uint32_t w = __builtin_amdgcn_alignbyte(src[(b >> 2) + 1], src[b >> 2], (uint32_t)(b & 3));
+                if (j0 + i == kWords - 1) w = (w & 0xFFu) | (h << 8);
+                v[i] = (int)w;
+            }
+            if (c < chunks) out4[c] = v;
+        }
+        q_first = chunks << 2;
+    }
+    for (int it = 0; it < (total - q_first + 63) / 64; ++it) {
+        const int q = q_first + lane_id() + 64 * it, qq = q < total ? q : total - 1;
+        const int r = qq / kWords, j = qq - kWords * r;
+        const int b = kObsDim * r + 4 * j;  // staged byte; b / 4 + 1 <= 4 677 < 64 * 300 / 4
+        uint32_t v = __builtin_amdgcn_alignbyte(src[(b >> 2) + 1], src[b >> 2], (uint32_t)(b & 3));
+        const uint32_t h = (uint32_t)__shfl((int)mhi, r);
+        if (j == kWords - 1) v = (v & 0xFFu) | (h << 8);
+        if (q < total) out[q] = v;
+    }
+}
+
 // Block store of this wave's masks: mask[t0 .. t0+rows) as int8 [rows][45].  The 64 x 45 mask
 // bits are first laid out as ONE bit stream in LDS (row r at bits 45r..45r+44; each stream
 // dword is cut from at most two rows), so every output dword is one nibble of the stream,
@@ -2156,7 +2202,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
     const bool valid = t < A.n;
     const int rows = min(64, A.n - t0);
     const bool want_final = S.autoreset && S.final_obs != nullptr;
-    const bool compact = S.obs_u8 != nullptr;  // obs_u8 rows instead of int32 obs rows
+    const bool compact = S.obs_u8 != nullptr && S.obs == nullptr;  // obs_u8 rows instead of int32 obs rows
     STAMP(0);
     if (rules_wave) {
         __builtin_amdgcn_s_setprio(SPL_WS_PRIO);  // as in the rollout: 27.9 -> 27.3 us
@@ -2256,6 +2302,8 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
             return;
         }
         store_obs_block<64, SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
+        if (S.obs_u8)  // both outputs: the compact copy of the same rows (a fused actor's input)
+            store_u8_from_rows(L.rows, rows, S.obs_u8 + (size_t)t0 * kObsU8, valid ? (uint32_t)get_moves(T.sw) >> 8 : 0u);
         STAMP(6);
         if (__any(valid && get_moves(T.sw) > 255)) {  // patch after this wave's block stores of the same dwords
             __builtin_amdgcn_s_waitcnt(0);
@@ -4042,7 +4090,6 @@ int spl_refill(spl_ctx_t *ctx, spl_arena_t *arena, void *stream) {
 static int check_step_args(const spl_step_args_t *a) {
     if (!a || !a->actions || !(a->obs || a->obs_u8) || !a->mask || !a->reward || !a->terminated || !a->flags)
         return fail(SPL_E_ARG, "actions/obs/mask/reward/terminated/flags are required");
-    if (a->obs && a->obs_u8) return fail(SPL_E_ARG, "obs and obs_u8 are exclusive");
     if ((uintptr_t)a->obs_u8 & 15u) return fail(SPL_E_ARG, "obs_u8 must be 16-byte aligned");
     if (!a->gate_terminated != !a->gate_flags) return fail(SPL_E_ARG, "gate_terminated and gate_flags go together");
     if (a->autoreset < 0 || a->autoreset > 2) return fail(SPL_E_ARG, "autoreset must be 0, 1 or 2");

@@ -69,7 +69,7 @@
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
 // streaming: no LDS-DMA piece after the prologue, no per-tile barrier), 4 A fragments loaded once
 // per tile (no per-group LDS reads), 16 the ring without its barriers (waves race the slots), 32 no
-// per-table epilogue (no softmax / sample / argmax)
+// per-table epilogue (no softmax / sample / argmax), 64 no observation loads (zero layer-1 operand)
 #ifndef SPL_POL_ABL
 #define SPL_POL_ABL 0
 #endif
@@ -819,7 +819,13 @@ __device__ __forceinline__ void act32_body(const uint8_t *__restrict__ W, ActArg
     const int64_t xt = valid > 0 ? (a.order ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : tbase + (r < valid ? r : 0)) : 0;
     pelx8 X[1][kKs1];
     ObsHi hi{0u, a.obs_u8 ? nullptr : a.obs + (size_t)xt * kObs, a.obs_u8 ? a.obs_u8 + (size_t)xt * 300 : nullptr};
+#if SPL_POL_ABL & 64  // timing ablation: no observation loads (zero operand planes)
+#pragma unroll
+    for (int s = 0; s < kKs1; ++s) X[0][s] = pelx8{};
+    hi.mask = 0u;
+#else
     hi.mask = load_obs<F>(hi.row32, hi.row8, g, X);
+#endif
     if constexpr (!kActor) {
         // get_value: no mask
     } else if (a.order) {

@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 LIB_NAME = "libsplendor_amd.so"
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # per-table flag bits (include/splendor_amd.h)
 POLICY_UNIFORM, POLICY_GREEDY_V1, POLICY_BASIC_PRIORITY = 0, 1, 2  # SPL_POLICY_* (device next_actions)

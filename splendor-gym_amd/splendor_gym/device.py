@@ -220,14 +220,16 @@ class Engine:
         return self.obs, self.mask
 
     def step(self, actions=None, autoreset=True, final_obs=True, next_actions=None, policy_seed=0, ply=0,
-             ep_return=None, ep_count=None, ply_base=None, policy=0, small=None, obs_u8=None, gate=None):
+             ep_return=None, ep_count=None, ply_base=None, policy=0, small=None, obs_u8=None, gate=None,
+             keep_obs=False):
         """One env step on every table (SplendorEnv.step semantics per table).  autoreset: False,
         True (same-step autoreset) or 2 (also re-deal tables terminal on entry, without a move).
         next_actions (optional int32 tensor) receives `policy`'s action (_native.POLICY_*) over
         the new state.  small: optional (reward, terminated, flags, winner) tensors that receive
         those outputs instead of self.reward/terminated/flags/winner.  obs_u8: optional uint8
         [n, 300] tensor that receives the compact observation (spl_step_args_t.obs_u8) INSTEAD of
-        self.obs (a device policy's input at a quarter of the bytes; self.obs is left as it was).
+        self.obs (a device policy's input at a quarter of the bytes; self.obs is left as it was), or with
+        keep_obs=True beside it (self.obs written as usual, obs_u8 a copy of its rows; ABI 8).
         gate: optional (terminated, flags) uint8 tensors of the agent's move in a dual step — tables
         where it ended the game or was not applied get action -1 (written into `actions`) and are not
         moved (spl_step_args_t.gate_*; spl_dual_gate fused into this launch)."""
@@ -249,10 +251,11 @@ class Engine:
                                        and obs_u8.is_contiguous() and obs_u8.numel() == self.n * OBS_U8):
             raise ValueError(f"obs_u8 must be a contiguous uint8 [{self.n}, {OBS_U8}] tensor on {self.device}")
         u8 = None if obs_u8 is None else obs_u8.data_ptr()
-        key = (rw.data_ptr(), tm.data_ptr(), fl.data_ptr(), wn.data_ptr(), code, fo, u8)
+        both = bool(keep_obs and u8)
+        key = (rw.data_ptr(), tm.data_ptr(), fl.data_ptr(), wn.data_ptr(), code, fo, u8, both)
         a = self._step_args.get(key)
         if a is None:
-            a = StepArgs(obs=None if u8 else self.obs.data_ptr(), obs_u8=u8, mask=self.mask.data_ptr(),
+            a = StepArgs(obs=None if (u8 and not both) else self.obs.data_ptr(), obs_u8=u8, mask=self.mask.data_ptr(),
                          reward=rw.data_ptr(), terminated=tm.data_ptr(), flags=fl.data_ptr(), winner=wn.data_ptr(),
                          final_obs=self.final_obs.data_ptr() if fo else None, autoreset=code, table0=self.table0)
             if len(self._step_args) >= 16:  # callers that pass fresh output tensors every call

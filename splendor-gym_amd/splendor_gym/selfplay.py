@@ -67,12 +67,24 @@ class DualInfo(Mapping):
         return len(set(self._d) | set(self._LAZY))
 
 
+def compact_rows(obs, out):
+    """out (uint8 [n, 300]) = the compact rows of int32 observations obs [n, 297] (spl_step_args_t.obs_u8:
+    bytes 0..296 the values mod 256, byte 297 = move_count >> 8, 298-299 zero)."""
+    out[:, :297] = (obs & 0xFF).to(torch.uint8)
+    out[:, 297] = ((obs[:, 295] >> 8) & 0xFF).to(torch.uint8)
+    out[:, 298:] = 0
+    return out
+
+
 class DualStepVectorEnv:
     def __init__(self, num_envs, device=None, opponent="random", policy_seed=0, refill_period=None, table0=0,
-                 opponent_obs=True, random_starts=False, step_counter=None):
+                 opponent_obs=True, random_starts=False, step_counter=None, agent_obs_u8=False):
         """step_counter: optional int64 [1] device tensor that every dual_step increments by one in its
         last launch (spl_dual_io_t.step_counter) — a graph-captured rollout loop passes it to the
-        agent's act as ply_base, so each replay draws fresh actions without a counter launch."""
+        agent's act as ply_base, so each replay draws fresh actions without a counter launch.
+        agent_obs_u8: keep `self.agent_obs_u8`, uint8 [n, 300], the compact rows (spl_step_args_t.obs_u8)
+        of the agent's observation, written by the opponent's step beside the int32 obs it returns
+        (ABI 8): a fused actor reads a quarter of the bytes (FusedActorCritic.act accepts them)."""
         if isinstance(opponent, str) and opponent not in _DEVICE_POLICIES:
             raise ValueError(f"unknown device opponent {opponent!r}; choose {sorted(_DEVICE_POLICIES)} or a callable")
         if step_counter is not None and not (step_counter.dtype == torch.int64 and step_counter.numel() == 1):
@@ -94,6 +106,7 @@ class DualStepVectorEnv:
         self.agent_reward, self.opp_reward = z(t.float32), z(t.float32)
         self.done, self.game_ended_on, self.info_flags = z(t.bool), z(t.int8), z(t.uint8)  # done: 0/1 bytes
         self.opp_obs = t.zeros(n, _native.OBS_DIM, dtype=t.int32, device=dev) if opponent_obs else None
+        self.agent_obs_u8 = t.zeros(n, _native.OBS_U8, dtype=t.uint8, device=dev) if agent_obs_u8 else None
         self.random_starts = bool(random_starts)
         from .fused_policy import OpponentPool
         self.pool = opponent if isinstance(opponent, OpponentPool) else None
@@ -129,6 +142,8 @@ class DualStepVectorEnv:
         if seeds is None and seed is not None:
             seeds = range(int(seed), int(seed) + self.num_envs)
         obs, mask = self.eng.reset(seeds=seeds)
+        if self.agent_obs_u8 is not None:  # the compact rows of the fresh deals (the reset writes int32 rows)
+            compact_rows(obs, self.agent_obs_u8)
         info = {"action_mask": mask, "to_play": obs[:, 294]}
         if self.pool is not None:  # every table starts an episode: draw its opponent
             self.pool.draw(self.opp_group, self.episode, None, self.eng.table0)
@@ -164,7 +179,8 @@ class DualStepVectorEnv:
             # phase B: the opponent's move, gated in the same launch (-1, no move, where the agent's move
             # was not applied or ended the game); autoreset 2 also re-deals the tables that ended on
             # the agent's move
-            e.step(opp, autoreset=2, final_obs=True, gate=(ta, fa))
+            e.step(opp, autoreset=2, final_obs=True, gate=(ta, fa), obs_u8=self.agent_obs_u8,
+                   keep_obs=self.agent_obs_u8 is not None)
             io = self._io
             io.opp_obs = self.opp_obs.data_ptr() if self.want_opp_obs else None
             if self.pool is not None:  # finish + the finished tables' next-opponent draw, one launch

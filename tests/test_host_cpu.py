@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_native.SIGNATURES), declared ^ set(_native.SIGNATURES)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.spl_abi_version() == _native.ABI_VERSION == 7
+    assert lib.spl_abi_version() == _native.ABI_VERSION == 8
 
 
 def test_abi_host_side_errors():

@@ -60,6 +60,28 @@ def main():
     res["fused_fp32_f16x2_greedy_us"] = timeit(lambda: fh.greedy(obs, mask))
     res["fused_bf16_sample_us"] = timeit(lambda: f16.act(obs, mask, seed=1, ply=2))
     res["fused_bf16_greedy_us"] = timeit(lambda: f16.greedy(obs, mask))
+    # the same calls on compact uint8 observation rows (Engine.step obs_u8: 300 B per table instead of
+    # 1 188; one more step writes them, so they are the next state's, timed alike)
+    u8 = torch.zeros(n, 300, dtype=torch.uint8, device=e.device)
+    e.step(a, next_actions=a, policy_seed=1, ply=9, obs_u8=u8)
+    res["fused_fp32_sample_u8obs_us"] = timeit(lambda: f.act(u8, mask, seed=1, ply=2))
+    res["fused_fp32_greedy_u8obs_us"] = timeit(lambda: f.greedy(u8, mask))
+    res["fused_fp32_f16x2_sample_u8obs_us"] = timeit(lambda: fh.act(u8, mask, seed=1, ply=2))
+    # the same state as int32 rows (bytes 0-296 widened, move_count's high byte at 297 folded in)
+    o32 = u8[:, :297].to(torch.int32).contiguous()
+    o32[:, 295] += 256 * u8[:, 297].to(torch.int32)
+    res["fused_fp32_sample_samestate_int32_us"] = timeit(lambda: f.act(o32, mask, seed=1, ply=2))
+    res["fused_fp32_greedy_samestate_int32_us"] = timeit(lambda: f.greedy(o32, mask))
+    res["int32_obs_max"] = int(obs.max().item())
+    res["int32_obs_min"] = int(obs.min().item())
+    # the reference's trained weights (config 5's agent) on the same two forms of the same state
+    from safetensors.torch import load_file
+    mt = ActorCritic().to(e.device).eval()
+    mt.load_state_dict(load_file(os.path.join(REPO, "tests", "golden", "ppo_splendor_latest.safetensors"),
+                                 device=str(e.device)))
+    ft = FusedActorCritic(mt)
+    res["trained_fp32_sample_int32_us"] = timeit(lambda: ft.act(o32, mask, seed=1, ply=2))
+    res["trained_fp32_sample_u8obs_us"] = timeit(lambda: ft.act(u8, mask, seed=1, ply=2))
 
     def torch_sample():
         with torch.no_grad():

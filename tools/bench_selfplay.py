@@ -82,7 +82,7 @@ def main():
         opponent = greedy_opponent_from(opp_model)
     ply_t = torch.zeros(1, dtype=torch.int64, device=dev)  # advanced by each dual step's last launch
     env = DualStepVectorEnv(N, device=dev, opponent=opponent, table0=rank * N, opponent_obs=False,
-                            step_counter=ply_t if fused else None)
+                            step_counter=ply_t if fused else None, agent_obs_u8=fused and not args.bf16)
     obs, info = env.reset(seed=rank * N)
     mask = info["action_mask"]
     amp = torch.autocast("cuda", dtype=torch.bfloat16) if (args.bf16 and not fused) else torch.autocast("cuda", enabled=False)
@@ -90,7 +90,8 @@ def main():
     def iteration(with_actor=True):
         with torch.no_grad(), amp:
             if with_actor and fused:
-                a, logprob, entropy, value = agent_k.act(obs, mask, seed=1234, table0=rank * N, ply_base=ply_t)
+                a, logprob, entropy, value = agent_k.act(obs if env.agent_obs_u8 is None else env.agent_obs_u8, mask,
+                                                         seed=1234, table0=rank * N, ply_base=ply_t)
             elif with_actor:
                 action, logprob, _, value = agent.get_action_and_value(obs.float(), mask.float())
                 a = action.to(torch.int32)
