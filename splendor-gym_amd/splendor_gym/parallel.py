@@ -67,13 +67,18 @@ def device_census(identity):
     """Every rank's device identity (device_identity), gathered on every rank: how many ranks, how
     many DISTINCT devices they run on, and whether any two share one (a rehearsal of N ranks on fewer
     cards is not an N-GPU figure)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if _single():
         ids = [identity]
     else:
         ids = [None] * dist.get_world_size()
         dist.all_gather_object(ids, identity)
     distinct = len(set(ids))
     return {"ranks": len(ids), "devices": distinct, "shared_device": distinct < len(ids), "identities": ids}
+
+
+def _single():
+    """No process group, or a group of one rank: the collectives below return their input."""
+    return not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1
 
 
 def _host_collectives():
@@ -85,7 +90,7 @@ def gather_returns(ep_return, ep_count, n_global=None):
     """All-gather per-table (return sum, episode count) shards into full [n_global] tensors on
     every rank.  Shards may differ in size by one (shard_range); they are padded to equal
     length for all_gather_into_tensor and trimmed after."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if _single():
         return ep_return.clone(), ep_count.clone()
     world = dist.get_world_size()
     if _host_collectives():
@@ -129,7 +134,7 @@ def gather_returns_host(ep_return, ep_count, n_global=None):
 
 def max_over_ranks(value, device=None):
     """Max of a host float over all ranks (the bench's slowest-rank time)."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if _single():
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64, device=None if _host_collectives() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -137,7 +142,7 @@ def max_over_ranks(value, device=None):
 
 
 def barrier(device=None):
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if not _single():
         if device is not None and device.type == "cuda" and not _host_collectives():
             dist.barrier(device_ids=[device.index])
         else:
