@@ -69,7 +69,8 @@
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
 // streaming: no LDS-DMA piece after the prologue, no per-tile barrier), 4 A fragments loaded once
 // per tile (no per-group LDS reads), 16 the ring without its barriers (waves race the slots), 32 no
-// per-table epilogue (no softmax / sample / argmax), 64 no observation loads (zero layer-1 operand)
+// per-table epilogue (no softmax / sample / argmax), 64 no observation loads (zero layer-1 operand);
+// the tail kernel k_act32_narrow: 128 its launch and index lookups only, 256 no layers (zero logits)
 #ifndef SPL_POL_ABL
 #define SPL_POL_ABL 0
 #endif
@@ -1116,6 +1117,9 @@ __global__ __launch_bounds__(kWaves * 64) void k_act32h(const uint8_t *__restric
 // workgroup of the network; tile_mma with the A planes kAheadGlobal k-steps ahead), and each
 // layer's outputs exchanged through LDS.  A tail wave-tile takes a small fraction of a full
 // workgroup's time (5 tile chains per wave instead of 35).
+// (8 k-steps ahead measured the same 21.7-22.0 us per call in config 5: the three layers' ~16 us are the
+// ~1 MB of one network's weights that every tail workgroup pulls through its CU, not the load latency;
+// profiles/r05/narrow_tail_r05zx_zy.txt)
 constexpr int kAheadGlobal = 3;
 
 constexpr int kNarrowWaves = 8;  // two hidden-layer tiles per wave (2 waves per SIMD: room for the A fragments)
@@ -1167,6 +1171,10 @@ __device__ __forceinline__ void act32_narrow_body(const uint8_t *__restrict__ Wb
     const int valid = (int)max<int64_t>(0, min<int64_t>(kRowsPerWave, gend - tbase));
     const int32_t tid_own = lane < valid ? a.order[tbase + lane] : 0;
     const int64_t xt = valid > 0 ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : 0;
+#if SPL_POL_ABL & 128  // timing ablation: the narrow kernel's launch and index lookups only
+    if (tid_own == -12345) a.action[0] = (int32_t)xt;
+    return;
+#endif
     pelx8 X[1][kKs1];
     ObsHi hi{0u, a.obs_u8 ? nullptr : a.obs + (size_t)xt * kObs, a.obs_u8 ? a.obs_u8 + (size_t)xt * 300 : nullptr};
     hi.mask = load_obs<F>(hi.row32, hi.row8, g, X);
@@ -1186,6 +1194,20 @@ __device__ __forceinline__ void act32_narrow_body(const uint8_t *__restrict__ Wb
         }
     }
     pelx8 H1[F::kPlanes][kKs2], H2[F::kPlanes][kKs2];
+#if SPL_POL_ABL & 256  // timing ablation: no layers (zero logits), the loads and the epilogue only
+    if (wave < kActTiles) {
+        for (int i = 0; i < 4; ++i) {
+            const int act = 16 * wave + 4 * g + i;
+            if (act < kAct) lg[r * kLogitRow + act] = (float)X[0][0][i] * 0.f;
+        }
+    }
+    (void)H1;
+    (void)H2;
+    (void)W;
+    if (false) {
+#else
+    {
+#endif
     narrow_layer<F>(W, 0, X, H1, xbuf, wave, lane, &hi);
     narrow_layer<F>(W, kTiles, H1, H2, xbuf, wave, lane, nullptr);
     if (wave < kActTiles) {  // logits: waves 0..2 take one 16-row tile each
@@ -1195,6 +1217,7 @@ __device__ __forceinline__ void act32_narrow_body(const uint8_t *__restrict__ Wb
             const int act = 16 * wave + 4 * g + i;
             if (act < kAct) lg[r * kLogitRow + act] = L[i];
         }
+    }
     }
     __syncthreads();
     if (wave == 0 && a.logits) {

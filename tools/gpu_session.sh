@@ -194,6 +194,25 @@ for step in "$@"; do
         done
       done
       for f in $O/pol_*_[12]_$TAG.out; do echo "$f $(cut -c1-160 $f)"; done ;;
+    spab)  # config-5 self-play, the in-tree library's variants ablate/lib_$v.so for v in $SPAB: the pool and
+           # compact-obs tests on each, then tools/bench_selfplay.py alternating (3 rounds), then a
+           # dual-step timeline of the last variant
+      for v in $SPAB; do  # SPAB_NOTEST=1: timing ablations (wrong results by design), no test run
+        [ "${SPAB_NOTEST:-0}" = "1" ] || SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_$v.so run pytest_sp_$v 400 python -u -m pytest \
+            tests/test_gpu_opponent_pool.py tests/test_gpu_compact_obs.py -x -q --timeout 200 --timeout-method thread
+      done
+      for i in 1 2 3; do
+        for v in $SPAB; do
+          SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_$v.so run sp_${v}_$i 200 python3 tools/bench_selfplay.py --opponent pool
+        done
+      done
+      for v in ${SPAB_TRACE:-$v}; do
+        SPLENDOR_AMD_LIB=splendor-gym_amd/ablate/lib_$v.so run spabtrace_$v 300 rocprofv3 --kernel-trace \
+            --output-format csv -d $O/prof_spabtrace_${v}_$TAG -o run -- python3 tools/bench_selfplay.py --opponent pool
+        python3 tools/dual_step_timeline.py $(find $O/prof_spabtrace_${v}_$TAG -name '*kernel_trace.csv' | head -1) \
+            > $O/selfplay_trace_${v}_$TAG.txt && tail -14 $O/selfplay_trace_${v}_$TAG.txt
+      done
+      for f in $O/sp_*_[123]_$TAG.out; do echo "$f $(tail -1 $f | cut -c1-200)"; done ;;
     polab)  # the fp32 actor: staged epilogue (product) vs after each tile (ablate/lib_nopipe.so), alternating
       for i in 1 2; do
         run pol_pipe_$i 200 python tools/bench_policy.py --fused-only --iters 30
