@@ -115,6 +115,11 @@ __device__ uint64_t *g_stamps;
         if ((threadIdx.x & 63) == 0 && g_stamps) g_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
         __builtin_amdgcn_sched_barrier(0);                                                       \
     } while (0)
+// a value instead of a time in stamp slot i (e.g. a wave's terminal-row count)
+#define STAMPV(i, v)                                                                             \
+    do {                                                                                         \
+        if ((threadIdx.x & 63) == 0 && g_stamps) g_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16 + (i)] = (uint64_t)(v); \
+    } while (0)
 // k_rollout keeps its stamps in registers (lane k holds step k's) so that stamping never waits
 // on the stores in flight; they are written to g_rstamps[wave][step][kRStamps] at the end.
 constexpr int kRStamps = 6;
@@ -151,6 +156,9 @@ __device__ uint64_t *g_wsend;   // [workgroup][2]: s_memrealtime at the output w
     } while (0)
 #define STAMP(i) \
     do {         \
+    } while (0)
+#define STAMPV(i, v) \
+    do {             \
     } while (0)
 #define RSTAMP(i, k) \
     do {             \
@@ -1740,16 +1748,15 @@ __device__ __forceinline__ ColRecipes col_recipes() {
 }
 
 // One table's observation row, column-parallel (wave-uniform call): word w of the table's state is
-// st[w * stride] in LDS (st and stride uniform); dst = the row's 297 int32 in global memory.
+// st[w * stride] in LDS (st and stride uniform); v[i] = column lane + 64 i of the row.
 template <int P>
-__device__ __forceinline__ void store_row_columns(const uint32_t *st, int stride, const Consts &L, const ColRecipes &C,
-                                                  int32_t *dst) {
+__device__ __forceinline__ void row_columns(const uint32_t *st, int stride, const Consts &L, const ColRecipes &C,
+                                            uint32_t (&v)[5]) {
     const uint32_t bank1 = st[SW_BANK1 * stride], misc = st[SW_MISC * stride];
     const int tp = (int)bget(bank1, 2), np = (tp + 1) % P;
     const uint32_t deck = st[SW_DECK * stride], owners = (st[SW_NOB1 * stride] >> 8) & 0x7FFFu;
     const uint8_t *cb = reinterpret_cast<const uint8_t *>(L.cards);
     const uint8_t *nb = reinterpret_cast<const uint8_t *>(L.nobles);
-    uint32_t v[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
         const uint32_t r = C.r[i];
@@ -1775,13 +1782,18 @@ __device__ __forceinline__ void store_row_columns(const uint32_t *st, int stride
         out = kind == CK_TERMINAL ? (((misc & ST_GAME_OVER) && tp == 0) ? 1u : 0u) : out;
         v[i] = out;
     }
+}
+template <int P>
+__device__ __forceinline__ void store_row_columns(const uint32_t *st, int stride, const Consts &L, const ColRecipes &C,
+                                                  int32_t *dst) {
+    uint32_t v[5];
+    row_columns<P>(st, stride, L, C, v);
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
         const int e = lane_id() + 64 * i;
         if (e < kObsDim) dst[e] = (int32_t)v[i];
     }
 }
-
 // spl_step_args_t.gate_*: the dual step's opponent moves only where the agent's move was applied
 // and left the game running (wrappers/dual_step_native.py:120-140, spl_dual_gate); elsewhere its
 // action becomes -1 (out of range: no move), written back so the caller sees the gated action.
@@ -2253,18 +2265,23 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         ws_sync();  // hand-off 2: first row halves staged
         STAMP(4);
         if (fin_all) {  // info["final_observation"] rows: each by the whole wave, from its listed words
+            // (four rows at a time, their LDS lookups overlapped, measured slower: 23.4 vs 23.2 us per step
+            // at 65 536 tables, 19.5 vs 18.1 at 16 384; profiles/r05/fin_group_ab_r05zz4.txt)
             const ColRecipes crc = col_recipes();
             for (uint64_t m = fin_all; m; m &= m - 1) {
                 const int r = __ffsll((unsigned long long)m) - 1;
                 store_row_columns<P>(&L.fst[0][r], 64, L, crc, S.final_obs + (size_t)(t0 + r) * kObsDim);
             }
         }
+        STAMP(7);
+        STAMPV(9, __popcll(fin_all) | (__popcll(__ballot((o.mask & kMaskDeferred) != 0)) << 8));
         if (o.mask & kMaskDeferred) o.mask = legal_of(T, L);
         STAMP(5);
         // masks and small outputs leave from this wave while the output wave streams the rows
         L.mask[lane] = o.mask;
         wave_lds_sync();
         store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+        STAMP(8);
         store_step_info(S, A.n, t, valid, o.flags);
         if (valid) {
             S.reward[t] = o.reward;

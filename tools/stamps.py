@@ -1,6 +1,7 @@
 """Per-phase timeline of k_step from in-kernel s_memrealtime stamps (diagnostic build only).
 
     python tools/stamps.py            # build lib_stamps.so (-DSPL_STAMPS) and run on the GPU
+    (STAMP_T: tables, default 65536; --build-only here, --run on the box)
 Lane 0 of every wave stamps 12 phase boundaries (see STAMP(i) in spl_engine.hip); we report, per
 phase, the median and max over waves of the time since the kernel's first stamp (10 ns ticks).
 Stamped builds fence the scheduler around each stamp: read the SHARES, not the absolute length.
@@ -16,7 +17,7 @@ NAMES = ["start", "loaded+prefetched", "pre-apply", "applied", "step logic", "fi
          "encoded", "barrier", "obs stored", "mask+final stored", "end"]
 # k_step_ws (the default spl_step kernel): stamps per wave, wave 0 = rules, wave 1 = output
 WS_RULES = ["start", "past hand-off 0", "rules done", "state to LDS (reset done)", "past hand-off 2 (row halves)", "legal mask",
-            "end (mask, small outputs, state stored)"]
+            "end (mask, small outputs, state stored)", "final rows stored (before 5)", "mask block issued (before 6)"]
 WS_OUT = ["start", "tables staged", "past hand-off 0", "past hand-off 1", "past hand-off 2 (rows encoded)", "final rows done",
           "obs stores issued", "end", "early board stores issued"]
 
@@ -26,7 +27,7 @@ sys.path[:0] = [sys.argv[1], os.path.join(sys.argv[1], "splendor-gym_amd")]
 import torch
 from splendor_gym import _native
 from splendor_gym.device import Engine
-T = 65536
+T = int(os.environ.get("STAMP_T", "65536"))
 e = Engine(T, 2, device="cuda:0", refill_period=0)
 e.lib.spl_debug_set_stamps.argtypes = [ctypes.c_void_p]
 e.reset(seeds=range(T))
@@ -82,6 +83,20 @@ def main():
             if col.size == 0:
                 continue
             print(f"{i:2d} {nm:26s} {np.median(col):10.2f} {np.percentile(col, 90):8.2f} {col.max():8.2f}")
+    if ws:  # the rules wave's tail by its terminal-row count (slot 9: rows | deferred-mask lanes << 8)
+        raw = np.array(runs, dtype=np.int64)[:, 0::2, 9].reshape(-1)
+        fin, dfr = raw & 255, raw >> 8
+        r = a[:, 0::2]
+        tail = (r[:, :, 7] - r[:, :, 4]).reshape(-1)
+        lm = (r[:, :, 5] - r[:, :, 7]).reshape(-1)
+        end = r[:, :, 6].reshape(-1)
+        for n in range(0, 8):
+            sel = fin == n
+            if sel.sum() == 0:
+                continue
+            print(f"rules waves with {n} terminal rows: {sel.sum():6d}, final rows {np.nanmedian(tail[sel]):.2f} us, "
+                  f"legal mask {np.nanmedian(lm[sel]):.2f} us (deferred lanes {np.median(dfr[sel]):.0f}), "
+                  f"end median {np.nanmedian(end[sel]):.2f} max {np.nanmax(end[sel]):.2f}")
     if ws:  # per XCC (workgroup i runs on XCC i % 8): the rules wave's hand-off 1 and the output wave's end
         wg = np.arange(a.shape[1] // 2) % 8
         for title, idx, ph in (("rules: past hand-off 1", 0, 4), ("output: end", 1, WS_OUT.index("end"))):
