@@ -82,6 +82,25 @@ def main():
     ft = FusedActorCritic(mt)
     res["trained_fp32_sample_int32_us"] = timeit(lambda: ft.act(o32, mask, seed=1, ply=2))
     res["trained_fp32_sample_u8obs_us"] = timeit(lambda: ft.act(u8, mask, seed=1, ply=2))
+    # the same call after 64 MB of other writes (the L2s hold none of the image: as in the dual step,
+    # where the opponents' images pass through first), timed per launch with events around the call
+    junk = torch.empty(64 << 20, dtype=torch.uint8, device=e.device)
+
+    def timed_after_flush(fn, flush):
+        ts = []
+        for i in range(args.iters + 5):
+            if flush:
+                junk.fill_(i & 255)
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record()
+            fn()
+            s1.record()
+            torch.cuda.synchronize()
+            if i >= 5:
+                ts.append(s0.elapsed_time(s1) * 1e3)
+        return sorted(ts)[len(ts) // 2]
+    res["trained_fp32_sample_u8obs_warm_median_us"] = timed_after_flush(lambda: ft.act(u8, mask, seed=1, ply=2), False)
+    res["trained_fp32_sample_u8obs_flushed_median_us"] = timed_after_flush(lambda: ft.act(u8, mask, seed=1, ply=2), True)
 
     def torch_sample():
         with torch.no_grad():
