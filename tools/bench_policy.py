@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--tables", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--fused-only", action="store_true", help="skip the torch timings")
+    ap.add_argument("--config5-only", action="store_true",
+                    help="only config 5's agent call: trained weights, compact rows, sample + critic (for PMC passes)")
     args = ap.parse_args()
     import torch
     from splendor_gym.device import Engine
@@ -54,6 +56,17 @@ def main():
         return s.elapsed_time(t) * 1e3 / args.iters
 
     res = {}
+    if args.config5_only:
+        from safetensors.torch import load_file
+        u8 = torch.zeros(n, 300, dtype=torch.uint8, device=e.device)
+        e.step(a, next_actions=a, policy_seed=1, ply=9, obs_u8=u8)
+        mt = ActorCritic().to(e.device).eval()
+        mt.load_state_dict(load_file(os.path.join(REPO, "tests", "golden", "ppo_splendor_latest.safetensors"),
+                                     device=str(e.device)))
+        ft = FusedActorCritic(mt)
+        res["trained_fp32_sample_u8obs_us"] = timeit(lambda: ft.act(u8, mask, seed=1, ply=2))
+        print(json.dumps(res))
+        return 0
     res["fused_fp32_sample_us"] = timeit(lambda: f.act(obs, mask, seed=1, ply=2))
     res["fused_fp32_greedy_us"] = timeit(lambda: f.greedy(obs, mask))
     res["fused_fp32_f16x2_sample_us"] = timeit(lambda: fh.act(obs, mask, seed=1, ply=2))

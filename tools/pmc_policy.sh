@@ -3,7 +3,7 @@
 # tools/bench_policy.py --fused-only at 65 536 tables), one rocprofv3 --pmc pass per counter group
 # (--kernel-trace only), then a per-kernel summary: MFMA busy fraction, wave-cycle split, LDS
 # instructions and bank conflicts, L2 (TCC) requests / hits and HBM bytes.
-#   tools/pmc_policy.sh TAG
+#   tools/pmc_policy.sh TAG     (POL_ARGS=--config5-only: config 5's agent call alone)
 set -o pipefail
 TAG=${1:-pol}
 export TMPDIR=/tmp
@@ -16,7 +16,7 @@ for grp in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_C
            "SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $grp --kernel-include-regex "k_act32" --output-format csv \
-      -d $O/p$i -o run -- python3 tools/bench_policy.py --fused-only --iters 5 > $O/p$i.log 2>&1 \
+      -d $O/p$i -o run -- python3 tools/bench_policy.py --fused-only --iters 5 $POL_ARGS > $O/p$i.log 2>&1 \
       || { echo "pass $i ($grp) failed"; tail -5 $O/p$i.log; }
 done
 python3 - "$O" <<'PY'
