@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--tables T] [--players P] [--mode rollout|step] [--only]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+`--gpus N` with N > 1 and no launcher in the environment (no WORLD_SIZE) starts its own N ranks
+(self_launch: one child process per GPU, this process never touches a GPU) and exits non-zero when
+the node shows fewer than N GPUs or the ranks do not land on N distinct devices, instead of
+reporting a one-GPU figure for an N-GPU request.  Under torchrun the ranks are the launcher's.
+
 One "step" = one SplendorEnv.step on every table of the batch (BASELINE.json config 3: legal
 mask + uniform-random policy, same-step autoreset, obs int32[297] + mask int8[45] + reward +
 terminated + flags + winner written per table-step, terminal rows to final_obs).  Actions come
@@ -352,6 +357,32 @@ def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
     fa, fc = actor_critic_mfma_flop(precision)
     flop = (fa + fc) * N
     tflops = flop / spread["median_s"] / 1e12
+    # the opponent pool's greedy call on its own: spl_policy_act_grouped = count +
+    # place + the grouped actor over each network's full 128-table workgroups + the narrow kernel over
+    # the groups' tails, eager, HIP events around each call on the launch stream, on the tables' current
+    # opponents and compact rows
+    oev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_act)]
+    for a, b in oev:
+        a.record(strm)
+        b.record(strm)
+    opp_args = (env.opp_obs_u8, env.eng.mask, env.opp_group)
+    opp_out = torch.empty(N, dtype=torch.int32, device=dev)
+    with torch.no_grad():
+        env.pool.act(*opp_args, out=opp_out)
+        torch.cuda.synchronize(dev)
+        region_mark("config5_opponent", "start", f"k_act32{'h' if precision != 'fp32' else ''}<false, false>", n_act)
+        for a, b in oev:
+            a.record(strm)
+            env.pool.act(*opp_args, out=opp_out)
+            b.record(strm)
+        torch.cuda.synchronize(dev)
+        region_mark("config5_opponent", "end")
+    ospread = launch_spread([a.elapsed_time(b) / 1e3 for a, b in oev])
+    groups = torch.bincount(env.opp_group.to(torch.int64).flatten())
+    full_wg = int((groups // 128).sum().item())
+    tails = int(((groups % 128) > 0).sum().item())
+    oflop = fa * N
+    otflops = oflop / ospread["median_s"] / 1e12
     env.close()
     l1, hid = MFMA_PRODUCTS[precision]
     kname = "k_act32<true, true>" if precision == "fp32" else "k_act32h<true, true>"
@@ -369,6 +400,17 @@ def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
                                       "median of 16 eager launches (HIP events on the launch stream); "
                                       "fp32_equivalent_tflops = the network's 2 x MACs per table at that time",
                          "traffic": None},
+            "opponent_roofline": {"bound": "mfma", "achieved": round(otflops, 1), "peak": F16_MFMA_PEAK_TFLOPS,
+                                  "unit": "TFLOP/s", "frac": round(otflops / F16_MFMA_PEAK_TFLOPS, 4),
+                                  "kernel": f"spl_policy_act_grouped: k_group_count + k_group_place + "
+                                            f"{kname.replace('true, true', 'false, false')} + k_act32_narrow",
+                                  "call_us": ospread["us"], "flop_per_call": oflop,
+                                  "networks": int((groups > 0).sum().item()), "full_workgroups": full_wg,
+                                  "tail_groups": tails,
+                                  "flop_note": f"16-bit MFMA work of the greedy actor per table: 2*(297*256*{l1} + "
+                                               f"256*256*{hid} + 256*45*{hid}) = {fa} (no critic); frac from the median "
+                                               f"of {n_act} eager calls (HIP events on the launch stream around the whole "
+                                               "grouped call, its two small grouping launches included)"},
             "config": {"workload": f"BASELINE config 5 per GPU: ActorCritic.get_action_and_value (fused, precision "
                                    f"{precision}) + DualStepVectorEnv.dual_step, opponent pool (current p=0.25 else 1 of "
                                    "12 frozen snapshots per episode, greedy, same precision), reset after done; hipGraph replays "
@@ -528,6 +570,23 @@ def c4_share_line(dev, rank, world, T, launches, warmup, pipeline=True, partner_
                                    "per-step rollout store [128, T, ...]", "tables_per_gpu": T, "players": P}}
 
 
+def self_launch(n, argv, device_count=None):
+    """`python bench.py --gpus N` without a launcher: N ranks of this script on this node, one per GPU
+    (parallel.launch_local_ranks; rank r drives cuda:r, rank 0 prints the JSON line).  This process
+    only counts the devices (torch.cuda.device_count() creates no HIP context) and waits; it exits
+    with the first failing rank's status.  Fewer than N devices: exit 2 with a message, nothing run.
+    No CPU baseline at N > 1 (it is reported at N = 1 only)."""
+    if device_count is None:
+        import torch
+        device_count = torch.cuda.device_count()
+    if device_count < n:
+        print(f"bench.py --gpus {n}: this node shows {device_count} GPU(s); an {n}-GPU run needs {n} "
+              f"(no figure reported)", file=sys.stderr, flush=True)
+        return 2
+    from splendor_gym.parallel import launch_local_ranks
+    return launch_local_ranks(n, [sys.executable, os.path.abspath(__file__), *argv])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -574,6 +633,8 @@ def main():
                     help="six-wave dealer rollout store: a team this many steps behind its neighbouring-XCC "
                          "partner hands it whole steps of rows (library default 4; 0 = off)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank_env = int(os.environ.get("RANK", "0"))
@@ -586,7 +647,7 @@ def main():
     from splendor_gym import _native
     from splendor_gym.device import Engine
     from splendor_gym.parallel import (barrier, device_census, device_identity, gather_returns, init_distributed,
-                                       local_device, max_over_ranks)
+                                       local_device, max_over_ranks, require_distinct_devices)
 
     rank, world, local = init_distributed()
     if world != args.gpus:
@@ -595,6 +656,11 @@ def main():
     torch.cuda.set_device(dev)
     # which physical GPU each rank drives: n_gpus counts distinct devices, not ranks
     census = device_census(device_identity(dev))
+    err = require_distinct_devices(census, world)
+    if err is not None:  # self-launched ranks sharing a card: not an N-GPU run
+        if rank == 0:
+            print(f"bench.py --gpus {args.gpus}: {err}", file=sys.stderr, flush=True)
+        sys.exit(3)
     if census["shared_device"] and rank == 0:
         print(f"warning: {census['ranks']} ranks share {census['devices']} device(s): {census['identities']}",
               file=sys.stderr)

@@ -44,7 +44,10 @@
 extern "C" {
 #endif
 
-#define SPL_ABI_VERSION 8  /* 8: spl_step with both obs and obs_u8 writes both (the compact rows as a copy);
+#define SPL_ABI_VERSION 9  /* 9: the arena holds a legal-mask cache ([2][n] u32 after the delegation flags,
+                                 spl_arena_bytes grows by 8 B per table; spl_step reads it), spl_host_mapped;
+                              8: spl_step with both obs and obs_u8 writes both (the compact rows as a copy);
+                                 splendor_dual.h spl_dual_io_t gained a trailing step_counter (zero-initialise);
                               7: spl_ctx_set_partner_lead, spl_debug_partner_stats (rollout-store partner hand-off);
                               6: SPL_F_FAULT + spl_ctx_faults (a lost hand-off in a rollout launch is reported);
                               5: spl_step_args_t.obs_u8 (compact observation), gate_terminated / gate_flags */
@@ -192,6 +195,11 @@ const char *spl_rollout_kernel_name(spl_ctx_t *ctx, int32_t n, int32_t players, 
 int spl_ctx_faults(spl_ctx_t *ctx, uint64_t *launch, int clear);
 const volatile uint64_t *spl_ctx_fault_word(spl_ctx_t *ctx);
 uint64_t spl_ctx_launches(spl_ctx_t *ctx);
+/* Whether host memory `host` is page-locked by HIP and mapped into the device at the SAME address
+ * (*same_address = 1), so a kernel may be handed the host pointer itself (SplendorEnv's pinned I/O
+ * block); 0 otherwise (e.g. registered rather than allocated pinned memory): the caller must then
+ * use device memory and copy.  Not part of the reference; host-side check only (hipHostGetDevicePointer). */
+int spl_host_mapped(const void *host, int32_t *same_address);
 
 int64_t spl_arena_bytes(int32_t n, int32_t players);
 /* Zero the arena and mark every table's pool as not dealt (must precede the first spl_reset

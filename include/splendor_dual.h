@@ -14,7 +14,10 @@
  *                    92-115), done and the info vectors; optionally the reference's opponent_obs
  *                    (the final observation on finished tables)
  *
- * Conventions as in splendor_amd.h.
+ * Conventions as in splendor_amd.h.  The dual glue has no version of its own: it changes with
+ * SPL_ABI_VERSION (splendor_amd.h).  ABI 8 appended spl_dual_io_t.step_counter; a caller must
+ * zero-initialise every spl_dual_io_t (`spl_dual_io_t io = {0};` / ctypes Structure()) so that a
+ * member it does not set is NULL = skip.
  */
 #ifndef SPLENDOR_DUAL_H
 #define SPLENDOR_DUAL_H

@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -39,12 +40,14 @@ struct KArena {
     int n;
     uint8_t *deleg;    // [n/128][kDelegTasks][num_words(P) x 64] u32 staged state words (rollout-store delegation)
     uint32_t *dflags;  // [n/128][kDelegFlagWords] its flags
+    uint32_t *legal;   // [2][n] legal-mask cache of the stored state (spl_layout.h)
 };
 
 struct KTables {
     const uint4 *cards;   // [90] {1,tier,points,oh_w | oh_b..oh_k | cost w,b,g,r | cost k,colour,0,0}
     const uint2 *nobles;  // [10] {1,req w,b,g | req r,k,points,0}
     const uint4 *lut;     // [kLutEntries] token-return MT outputs (top 3 bits, 10 per word)
+    uint32_t mtag;        // this context's legal-mask cache tag (1..65535)
 };
 
 struct KStep {
@@ -1368,8 +1371,11 @@ __device__ __forceinline__ void load_tab(Tab<P> &T, const KArena &A, int t) {
         for (int k = 0; k < 4; ++k) T.pw[q][k] = A.planes[(size_t)pw_index(q, k) * A.n + t];
 }
 
+// The table state and its legal-mask cache entry: `legal` is legal_moves of T (as computed under the
+// context tagged `tag`), or anything with tag 0 when the storing kernel does not know it.  Every
+// kernel that stores state goes through here, so no stale mask survives a state change.
 template <int P>
-__device__ __forceinline__ void store_tab(const Tab<P> &T, const KArena &A, int t) {
+__device__ __forceinline__ void store_tab(const Tab<P> &T, const KArena &A, int t, uint64_t legal, uint32_t tag) {
     SPL_CHECK(t >= 0 && t < A.n, BC_TABLE);
 #pragma unroll
     for (int w = 0; w < SW_COUNT; ++w) A.planes[(size_t)w * A.n + t] = T.sw[w];
@@ -1377,6 +1383,18 @@ __device__ __forceinline__ void store_tab(const Tab<P> &T, const KArena &A, int 
     for (int q = 0; q < P; ++q)
 #pragma unroll
         for (int k = 0; k < 4; ++k) A.planes[(size_t)pw_index(q, k) * A.n + t] = T.pw[q][k];
+    A.legal[t] = (uint32_t)legal;
+    A.legal[A.n + t] = ((uint32_t)(legal >> 32) & kLegalHiBits) | (tag << kLegalTagShift);
+}
+
+// the cached legal mask of table t's stored state, if it was computed under context tag `tag`
+struct LegalCache {
+    uint32_t lo, hi;
+    __device__ __forceinline__ bool known(uint32_t tag) const { return (hi >> kLegalTagShift) == tag; }
+    __device__ __forceinline__ uint64_t mask() const { return (uint64_t)lo | ((uint64_t)(hi & kLegalHiBits) << 32); }
+};
+__device__ __forceinline__ LegalCache load_legal(const KArena &A, int t) {
+    return LegalCache{A.legal[t], A.legal[A.n + t]};
 }
 
 __device__ __forceinline__ void load_tables_lds(Consts &L, const KTables &Tb) {
@@ -1929,7 +1947,7 @@ __global__ __launch_bounds__(64 * W) void k_step(KArena A, KTables Tb, KStep S) 
             const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
             S.next_actions[t] = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply);
         }
-        if (!abl(ABL_TAB_STORE)) store_tab(T, A, t);
+        if (!abl(ABL_TAB_STORE)) store_tab(T, A, t, o.mask, Tb.mtag);
         if (pool_dirty) store_pool(A, t, pool);
     }
     STAMP(11);
@@ -2077,7 +2095,7 @@ __global__ __launch_bounds__(64) void k_rollout(KArena A, KTables Tb, KStep S, i
 #endif
     if (valid) {
         if (S.next_actions) S.next_actions[t] = action;
-        store_tab(T, A, t);
+        store_tab(T, A, t, cur_mask, K > 0 ? Tb.mtag : 0u);  // cur_mask: the last step's mask of this state
         if (pool_dirty) store_pool(A, t, pool);
     }
 }
@@ -2225,8 +2243,10 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         // vmcnt(0) below (which the state needs anyway) covers them — no staging wave, no hand-off 0
         // (a barrier that the stamps put at 2.8 us, ~0.7 us after the state had landed)
         dma_tables_lds(L, Tb);
+        LegalCache lc{0u, 0u};
         if (valid) {
             load_tab(T, A, t);
+            lc = load_legal(A, t);  // legal_moves of this state, stored by the kernel that stored the state
             action = gated_action(S, t);
             if (S.autoreset) pool = load_pool(A, t);
         } else {
@@ -2236,7 +2256,10 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         const StepPre pre = step_prefetch(T, action, valid, A, t, Tb);
         STAMP(1);
         uint32_t *const mtx = reinterpret_cast<uint32_t *>(&L.rows[64 * kScratchStride]);
-        StepOut o = step_rules(T, action, pre, valid, L, Tb, mtx, false, 0ull, true);
+        // the pre-step check (envs/splendor_env.py:55-66: any legal move? is the action legal?) from the
+        // cached mask where it is this context's; tables whose cache is unknown (after an upload, or under
+        // another card table) evaluate legal_moves as before
+        StepOut o = step_rules(T, action, pre, valid, L, Tb, mtx, valid && lc.known(Tb.mtag), lc.mask(), true);
         // autoreset 2: a table terminal on entry is re-dealt without a move (dual-step opponent phase)
         const bool entry_reset = valid && S.autoreset == 2 && (o.flags & SPL_F_AFTER_TERMINAL);
         if (entry_reset) o.flags = 0u;
@@ -2260,11 +2283,12 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         ws_sync();  // hand-off 1: state words (deal scratch in `rows` free again)
         // this wave encodes the first half of every row while the output wave encodes the second
         // (encode 2.7 -> ~1.4 us before the obs stores start)
-        if (compact) encode_row_u8<0>(T, L.rows, L);
+        if (abl(ABL_ENCODE)) {
+        } else if (compact) encode_row_u8<0>(T, L.rows, L);
         else encode_row_half<0>(T, L.rows, L);
         ws_sync();  // hand-off 2: first row halves staged
         STAMP(4);
-        if (fin_all) {  // info["final_observation"] rows: each by the whole wave, from its listed words
+        if (fin_all && !abl(ABL_FINAL)) {  // info["final_observation"] rows: each by the whole wave, from its listed words
             // (four rows at a time, their LDS lookups overlapped, measured slower: 23.4 vs 23.2 us per step
             // at 65 536 tables, 19.5 vs 18.1 at 16 384; profiles/r05/fin_group_ab_r05zz4.txt)
             const ColRecipes crc = col_recipes();
@@ -2275,12 +2299,12 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         }
         STAMP(7);
         STAMPV(9, __popcll(fin_all) | (__popcll(__ballot((o.mask & kMaskDeferred) != 0)) << 8));
-        if (o.mask & kMaskDeferred) o.mask = legal_of(T, L);
+        if (o.mask & kMaskDeferred) o.mask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);
         STAMP(5);
         // masks and small outputs leave from this wave while the output wave streams the rows
         L.mask[lane] = o.mask;
         wave_lds_sync();
-        store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+        if (!abl(ABL_MASK_STORE)) store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
         STAMP(8);
         store_step_info(S, A.n, t, valid, o.flags);
         if (valid) {
@@ -2296,7 +2320,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
                 const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
                 S.next_actions[t] = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply);
             }
-            store_tab(T, A, t);
+            store_tab(T, A, t, o.mask, Tb.mtag);  // o.mask: legal_moves of the stored (stepped, autoreset) state
             if (pool_dirty) store_pool(A, t, pool);
         }
         STAMP(6);
@@ -2308,7 +2332,8 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         Tab<P> T;
 #pragma unroll
         for (int w = 0; w < kW; ++w) set_tab_word(T, w, L.st[w][lane]);
-        if (compact) encode_row_u8<1>(T, L.rows, L);
+        if (abl(ABL_ENCODE)) {
+        } else if (compact) encode_row_u8<1>(T, L.rows, L);
         else encode_row_half<1>(T, L.rows, L);
         ws_sync();  // hand-off 2
         STAMP(4);
@@ -2318,7 +2343,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
             STAMP(6);
             return;
         }
-        store_obs_block<64, SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
+        if (!abl(ABL_OBS_STORE)) store_obs_block<64, SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
         if (S.obs_u8)  // both outputs: the compact copy of the same rows (a fused actor's input)
             store_u8_from_rows(L.rows, rows, S.obs_u8 + (size_t)t0 * kObsU8, valid ? (uint32_t)get_moves(T.sw) >> 8 : 0u);
         STAMP(6);
@@ -2985,7 +3010,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
 #endif
         if (valid) {
             if (S.next_actions) S.next_actions[t] = action;
-            store_tab(T, A, t);
+            store_tab(T, A, t, cur_mask, K > 0 ? Tb.mtag : 0u);  // cur_mask: the last step's mask of this state
             if (pool_dirty) store_pool(A, t, pool);
         }
     } else {
@@ -3487,14 +3512,16 @@ __global__ __launch_bounds__(64) void k_reset(KArena A, KTables Tb, const uint64
         }
     }
     wave_lds_sync();
+    // env info mask, also the legal-mask cache of every stored state (reset or not)
+    const uint64_t lm = (valid && !is_terminal(T.sw)) ? legal_of(T, L) : 0ull;
     if (obs || mask_out) {
         encode_row(T, L.rows, L);
-        L.mask[lane] = (valid && !is_terminal(T.sw)) ? legal_of(T, L) : 0ull;  // env info mask
+        L.mask[lane] = lm;
         wave_lds_sync();
         if (obs) store_obs_block(L.rows, rows, obs + (size_t)t0 * kObsDim);
         if (mask_out) store_mask_block(L.mask, L.mbits, rows, mask_out + (size_t)t0 * 45);
     }
-    if (valid) store_tab(T, A, t);
+    if (valid) store_tab(T, A, t, lm, Tb.mtag);
 }
 
 // Pool refill: every table with consumed pool records gets ONE of them re-dealt per call, the
@@ -3713,7 +3740,7 @@ __global__ __launch_bounds__(64) void k_upload(KArena A, int first, int count, c
         }
         pack_pl(p, T.pw[q]);
     }
-    store_tab(T, A, t);
+    store_tab(T, A, t, 0ull, 0u);  // a crafted state: its legal mask is unknown until a step evaluates it
     uint8_t *rec = slot_rec(A, t, active_of(old_misc));
     for (int tt = 0; tt < 3; ++tt)
         for (int k = 0; k < tier_size(tt); ++k) rec[tier_base(tt) + k] = (uint8_t)(k < v.deck_len[tt] ? v.decks[tt][k] : 0xFF);
@@ -3740,6 +3767,7 @@ struct spl_ctx_s {
     int quad_resident[5];    // k_rollout_store_quad_<P>p: the same for the quad variant
     int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
     int partner_lead;    // six-wave dealer per-step store: partner hand-off lead in steps (0 off, < 0 forced)
+    uint32_t mtag;         // legal-mask cache tag of this context (its card table), 1..65535
     uint64_t *fault_host;  // host-mapped, fine-grained: the serial of a launch that faulted (0 = none), spl_ctx_faults
     uint64_t *fault_dev;   // its device address (KStep::fault)
     uint64_t launches;     // launch serial (KStep::fault_tag)
@@ -3762,7 +3790,7 @@ static inline int fail(int code, const std::string &msg) { return spl_fail(code,
         if (e_ != hipSuccess) return fail(SPL_E_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
-static KTables ktables(const spl_ctx_t *c) { return KTables{c->cards, c->nobles, c->lut}; }
+static KTables ktables(const spl_ctx_t *c) { return KTables{c->cards, c->nobles, c->lut, c->mtag}; }
 
 static int check_arena(const spl_ctx_t *ctx, const spl_arena_t *a) {
     if (!ctx) return fail(SPL_E_ARG, "null context");
@@ -3778,7 +3806,8 @@ static KArena karena(const spl_arena_t *a) {
     const ArenaLayout L = arena_layout(a->n, a->players);
     uint8_t *b = static_cast<uint8_t *>(a->base);
     return KArena{reinterpret_cast<uint32_t *>(b + L.planes), reinterpret_cast<uint32_t *>(b + L.pool), b + L.slots,
-                  b + L.pcg, a->n, b + L.deleg, reinterpret_cast<uint32_t *>(b + L.dflags)};
+                  b + L.pcg, a->n, b + L.deleg, reinterpret_cast<uint32_t *>(b + L.dflags),
+                  reinterpret_cast<uint32_t *>(b + L.legal)};
 }
 
 static int launch_check() {
@@ -3926,6 +3955,10 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     }
     spl_ctx_t *c = new spl_ctx_t();
     c->device = device;
+    {  // a tag per context: an arena stepped under another card table never reuses this one's masks
+        static std::atomic<uint32_t> serial{0u};
+        c->mtag = serial.fetch_add(1u) % 0xFFFFu + 1u;
+    }
     c->refill_period = 64;
     c->refill_fused = 1;
     c->deleg_every = SPL_DELEG_EVERY;
@@ -3989,6 +4022,15 @@ const volatile uint64_t *spl_ctx_fault_word(spl_ctx_t *ctx) {
 }
 
 uint64_t spl_ctx_launches(spl_ctx_t *ctx) { return ctx ? ctx->launches : 0; }
+
+int spl_host_mapped(const void *host, int32_t *same_address) {
+    if (!host || !same_address) return fail(SPL_E_ARG, "null argument");
+    void *dev = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&dev, const_cast<void *>(host), 0);
+    *same_address = (e == hipSuccess && dev == host) ? 1 : 0;
+    if (e != hipSuccess) (void)hipGetLastError();  // not page-locked by HIP: not an error of this call
+    return SPL_OK;
+}
 
 int spl_ctx_set_refill_period(spl_ctx_t *ctx, int period) {
     if (!ctx || period < 0) return fail(SPL_E_ARG, "bad refill period");

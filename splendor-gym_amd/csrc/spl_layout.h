@@ -92,8 +92,16 @@ __host__ __device__ constexpr int pt_progress_line(int side) { return DF_TASKS +
 __host__ __device__ constexpr int pt_done_line(int side) { return DF_TASKS + 2 * (side * kPartnerSlots + 1) + 1; }
 __host__ __device__ constexpr int pt_epoch_line(int side) { return DF_PROD_EPOCH + side; }
 
+// Legal-mask cache (ABI 9): [2][n] u32, legal_moves of the table's STORED state as written by the
+// kernel that stored it — word 0 mask bits 0..31, word 1 bits 32..44 | context tag << 16.  A reader
+// trusts it only when the tag equals its context's (a context is one card table: an edited table's
+// context gets a tag of its own), and every kernel that stores table state writes the mask it computed
+// or tag 0 (unknown).  spl_step reads it so its pre-step check needs no legal_moves evaluation.
+constexpr uint32_t kLegalHiBits = 0x1FFFu;
+constexpr int kLegalTagShift = 16;
+
 struct ArenaLayout {
-    int64_t planes, pool, slots, pcg, deleg, dflags, total;
+    int64_t planes, pool, slots, pcg, deleg, dflags, legal, total;
 };
 
 __host__ __device__ inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
@@ -106,7 +114,8 @@ __host__ __device__ inline ArenaLayout arena_layout(int64_t n, int P) {
     L.pcg = align256(L.slots + n * kSlotRecords * kSlotBytes);
     L.deleg = align256(L.pcg + n * kPcgBytes);
     L.dflags = align256(L.deleg + (n / 128) * kDelegTasks * (int64_t)kDelegPayload);
-    L.total = align256(L.dflags + (n / 128) * kDelegFlagWords * 4);
+    L.legal = align256(L.dflags + (n / 128) * kDelegFlagWords * 4);
+    L.total = align256(L.legal + 2 * n * 4);
     return L;
 }
 

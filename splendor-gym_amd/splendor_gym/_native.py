@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 LIB_NAME = "libsplendor_amd.so"
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # per-table flag bits (include/splendor_amd.h)
 POLICY_UNIFORM, POLICY_GREEDY_V1, POLICY_BASIC_PRIORITY = 0, 1, 2  # SPL_POLICY_* (device next_actions)
@@ -103,6 +103,7 @@ SIGNATURES = {
     "spl_ctx_faults": ([c_void_p, ctypes.POINTER(c_uint64), c_int32], c_int32),
     "spl_ctx_fault_word": ([c_void_p], c_void_p),
     "spl_ctx_launches": ([c_void_p], c_uint64),
+    "spl_host_mapped": ([c_void_p, ctypes.POINTER(c_int32)], c_int32),
     "spl_debug_set_spin_limit": ([c_int64], c_int32),
     "spl_debug_partner_stats": ([c_void_p, c_int32], c_int32),
     "spl_rollout_kernel_name": ([c_void_p, c_int32, c_int32, c_int32], ctypes.c_char_p),

@@ -74,11 +74,24 @@ class Engine:
         self.host_io = bool(host_io)
         self.io = (torch.zeros(off, dtype=torch.uint8, pin_memory=True) if self.host_io
                    else torch.zeros(off, dtype=torch.uint8, device=dev))
+        if self.host_io and not self._host_mapped(self.io.data_ptr()):
+            # the caching host allocator handed out memory the device does not see at the same address
+            # (e.g. registered instead of allocated pinned memory): device I/O block instead;
+            # SplendorEnv then copies the action in and the outputs out (host_io is False)
+            self.host_io = False
+            self.io = torch.zeros(off, dtype=torch.uint8, device=dev)
         for name, dt, shape, o, nb in offs:
             setattr(self, name, self.io[o:o + nb].view(dt).view(shape))
         self.io_step_bytes = offs[6][3]  # obs .. winner
         with torch.cuda.device(dev):
             check(self.lib, self.lib.spl_arena_init(self.ctx, ctypes.byref(self.desc), self.stream()))
+
+    def _host_mapped(self, ptr):
+        """Whether pinned host memory at `ptr` is mapped into the device at the same address
+        (spl_host_mapped), so the kernels may be handed the host pointer itself."""
+        same = ctypes.c_int32(0)
+        check(self.lib, self.lib.spl_host_mapped(ctypes.c_void_p(ptr), ctypes.byref(same)))
+        return bool(same.value)
 
     def _create_ctx(self, cards=None):
         """A library context over the card table `cards` (int32 [90, 8]; None = the canonical

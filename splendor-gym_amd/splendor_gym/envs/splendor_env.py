@@ -44,7 +44,15 @@ class SplendorEnv(Env):
         if self._eng is None:
             from ..device import Engine
             e = Engine(1, self.num_players, device=self._device, refill_period=0, host_io=True)
-            h, base = e.io.numpy(), e.io.data_ptr()  # the pinned I/O block the kernels read and write
+            base = e.io.data_ptr()
+            if e.host_io:  # the pinned I/O block the kernels read and write
+                h, self._push, self._pull = e.io.numpy(), None, None
+            else:          # pinned memory not mapped at its own address: device block + copies per call
+                hb = e.torch.zeros(e.io.numel(), dtype=e.torch.uint8)
+                h = hb.numpy()
+                a0, a1 = e.actions.data_ptr() - base, e.actions.data_ptr() - base + 4
+                self._push = lambda: e.io[a0:a1].copy_(hb[a0:a1])
+                self._pull = lambda: hb[:e.io_step_bytes].copy_(e.io[:e.io_step_bytes])
 
             def view(t, dt, count):
                 return np.frombuffer(h, dtype=dt, count=count, offset=t.data_ptr() - base)
@@ -61,6 +69,8 @@ class SplendorEnv(Env):
         into the pinned I/O block: wait for the launch, then read them."""
         e, v = self._eng, self._v
         e.torch.cuda.current_stream(e.device).synchronize()
+        if self._pull is not None:
+            self._pull()
         self._out = dict(reward=float(v["reward"][0]), terminated=int(v["terminated"][0]), flags=int(v["flags"][0]),
                          winner=int(v["winner"][0]))
         return v["obs"].copy(), v["mask"].copy()
@@ -94,6 +104,8 @@ class SplendorEnv(Env):
         a = max(min(a, 2**31 - 1), -(2**31))
         self._flush_view()
         self._v["actions"][0] = a  # read by the kernel from pinned memory (no kernel is in flight here)
+        if self._push is not None:
+            self._push()
         self._launch()              # = e.step(e.actions, autoreset=False)
         self._view = None
         obs, mask = self._fetch()
@@ -184,7 +196,7 @@ class SplendorEnv(Env):
         self._flush_view()
         e.legal()
         e.torch.cuda.current_stream(e.device).synchronize()  # the mask lands in the pinned I/O block
-        return e.mask[0].numpy().copy()
+        return e.mask[0].cpu().numpy().copy()
 
     def render(self):
         """Print the reference logger's compact text of the table (envs/splendor_env.py:119-126)."""

@@ -147,3 +147,69 @@ def barrier(device=None):
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
+
+
+# env var a self-launched rank carries (launch_local_ranks): the ranks must run on distinct devices
+SELF_LAUNCHED_ENV = "SPLENDOR_SELF_LAUNCHED"
+
+
+def free_port(addr="127.0.0.1"):
+    """A TCP port on `addr` that nothing listens on right now (the rendezvous port of a local group)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind((addr, 0))
+        return s.getsockname()[1]
+
+
+def launch_local_ranks(n, cmd, env=None, port=None, poll_s=0.2, stream=None):
+    """Run `cmd` (an argv list) as ranks 0..n-1 of one process group on this node: what
+    `torch.distributed.run --nnodes 1 --nproc-per-node n --master-addr 127.0.0.1` does, for a caller
+    that was started without a launcher (`python bench.py --gpus 8`).
+
+    Each child gets RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT and
+    SPLENDOR_SELF_LAUNCHED=1, inherits stdout / stderr, and picks its own device
+    (`local_device(LOCAL_RANK)`): this process never touches a GPU, so the children are started from
+    a process without a HIP context.  Waits for all of them; when one exits non-zero the others are
+    terminated (their exact PIDs) so none is left waiting in a collective.  Returns 0 when every rank
+    exited 0, else the first non-zero exit status seen (a signal -s maps to 128 + s)."""
+    import subprocess
+    import sys
+    import time
+    if n < 1:
+        raise ValueError("n must be >= 1")
+    port = port or free_port()
+    base = dict(os.environ if env is None else env)
+    base.update(WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    base[SELF_LAUNCHED_ENV] = "1"
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(list(cmd), env=e))
+    status = 0
+    live = list(procs)
+    while live:
+        time.sleep(poll_s)
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"rank {procs.index(p)} exited with status {rc}; stopping the other ranks",
+                      file=stream or sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+    for p in procs:
+        p.wait()
+    return status
+
+
+def require_distinct_devices(census, world):
+    """A self-launched run (launch_local_ranks) is an N-GPU figure only if its N ranks drove N distinct
+    devices: returns the error text when they did not, else None (an external launcher's shared-device
+    rehearsal is labelled instead, bench.node_fields)."""
+    if os.environ.get(SELF_LAUNCHED_ENV) != "1" or census["devices"] >= world:
+        return None
+    return (f"{world} ranks found only {census['devices']} distinct device(s) ({census['identities']}): "
+            f"an N-GPU run needs N GPUs; no figure is reported")

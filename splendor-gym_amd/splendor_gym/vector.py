@@ -179,8 +179,10 @@ class SplendorVectorEnv:
     def reset(self, *, seed=None, options=None):
         """Reset every table.  This is also the recovery from a faulted launch: a fault seen
         since the last clear (step() raised LaunchFault for it) is cleared once every table has been
-        re-dealt, and reported as info["recovered_fault"] = the faulted launch's serial."""
-        fault = self.engine.faults()
+        re-dealt, and reported as info["recovered_fault"] = the faulted launch's serial.  The fault word
+        is read after the re-deal has been enqueued and the device has drained: a launch
+        still in flight at the call that faults later is covered by this reset too, since the re-deal
+        follows it in stream order."""
         if self._unchecked and self.check_actions == "deferred":
             self._queue_check()
         self._raise_pending(block_all=True)
@@ -190,6 +192,8 @@ class SplendorVectorEnv:
         b = self._next_block()
         self.engine.reset(seeds=seeds, obs_out=b.obs, mask_out=b.mask)
         self._seeded = True
+        self.engine.torch.cuda.synchronize(self.device)
+        fault = self.engine.faults()
         info = {"action_mask": self._out(b.mask), "to_play": self._out(b.to_play)}
         if fault:  # every table was just re-dealt: the undefined state is gone
             self.engine.clear_faults()

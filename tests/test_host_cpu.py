@@ -1,6 +1,7 @@
 """CPU-only tests: C-ABI exports, host-side seeding/layout logic, the device RNG formulation
 compiled for the host, and the gloo multi-process sharding path."""
 import ctypes
+import json
 import os
 import re
 import subprocess
@@ -30,7 +31,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_native.SIGNATURES), declared ^ set(_native.SIGNATURES)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.spl_abi_version() == _native.ABI_VERSION == 8
+    assert lib.spl_abi_version() == _native.ABI_VERSION == 9
 
 
 def test_abi_host_side_errors():
@@ -114,10 +115,10 @@ def test_arena_layout_sizes():
             b = int(lib.spl_arena_bytes(n, P))
             # state planes + 5 pool planes + 4 deck slot records x 128 B + 64 B PCG record, then per pair
             # of 64-table workgroups 24 staged steps (64 tables x 25 state words) and 50 flag lines
-            # (rollout-store delegation)
+            # (rollout-store delegation), then the legal-mask cache (2 u32 planes, ABI 9)
             deleg = (n // 128) * (24 * 64 * 25 * 4 + 50 * 128)
-            assert b >= (words + 5) * 4 * n + 512 * n + 64 * n + deleg
-            assert b % 256 == 0 and b <= (words + 5) * 4 * n + 576 * n + deleg + 6 * 256
+            assert b >= (words + 5) * 4 * n + 512 * n + 64 * n + deleg + 8 * n
+            assert b % 256 == 0 and b <= (words + 5) * 4 * n + 584 * n + deleg + 7 * 256
 
 
 def test_table_dtype_matches_oracle_struct():
@@ -260,6 +261,74 @@ def test_gloo_device_census_flags_shared_devices(same):
         assert rec["n_gpus"] == (1 if same else 2) and rec["ranks"] == 2 and rec["shared_device"] is same
         assert ("whole node" in rec["metric"]) is (not same)
         assert len(rec["devices"]) == 2
+
+
+_LAUNCHED_RANK = r'''
+import json, os, sys
+sys.path[:0] = [sys.argv[1], os.path.join(sys.argv[1], "splendor-gym_amd")]
+import torch
+from splendor_gym.parallel import (device_census, gather_returns, init_distributed, max_over_ranks,
+                                   require_distinct_devices, shard_range)
+rank, world, local = init_distributed(backend="gloo")
+same = sys.argv[3] == "same"
+census = device_census("hostA/pci 0000:05:00" if same else f"hostA/pci 0000:0{local + 5}:00")
+err = require_distinct_devices(census, world)
+if err is not None:
+    print(err, file=sys.stderr)
+    sys.exit(3)
+lo, hi = shard_range(1001, rank, world)
+ids = torch.arange(lo, hi, dtype=torch.float32)
+ret, cnt = gather_returns(ids * 0.5, (ids % 7).to(torch.int64), n_global=1001)
+t = max_over_ranks(float(rank) + 0.25)
+with open(os.path.join(sys.argv[2], f"rank{rank}.json"), "w") as f:
+    json.dump({"rank": rank, "world": world, "local": local, "env": os.environ["SPLENDOR_SELF_LAUNCHED"],
+               "census": census, "ret_ok": ret.tolist() == [i * 0.5 for i in range(1001)],
+               "cnt_ok": cnt.tolist() == [i % 7 for i in range(1001)], "max": t}, f)
+'''
+
+
+def test_self_launched_ranks_over_gloo(tmp_path):
+    """VERDICT r05 item 1: bench.py --gpus N without a launcher starts N ranks itself
+    (parallel.launch_local_ranks).  Two ranks over gloo on CPU: each gets its rank / local rank /
+    world and the rendezvous, the census sees two devices, gather_returns and max_over_ranks agree."""
+    from splendor_gym.parallel import launch_local_ranks
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    rc = launch_local_ranks(2, [sys.executable, "-c", _LAUNCHED_RANK, REPO, str(tmp_path), "distinct"], env=env)
+    assert rc == 0
+    recs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+    for r, rec in enumerate(recs):
+        assert rec["rank"] == r and rec["local"] == r and rec["world"] == 2 and rec["env"] == "1"
+        assert rec["census"]["devices"] == 2 and not rec["census"]["shared_device"]
+        assert rec["ret_ok"] and rec["cnt_ok"] and rec["max"] == 1.25
+
+
+def test_self_launched_ranks_on_one_device_fail(tmp_path):
+    """Self-launched ranks that land on ONE device exit non-zero (no N-GPU figure from a shared card)."""
+    from splendor_gym.parallel import launch_local_ranks
+    rc = launch_local_ranks(2, [sys.executable, "-c", _LAUNCHED_RANK, REPO, str(tmp_path), "same"])
+    assert rc == 3
+    assert not list(tmp_path.glob("rank*.json"))
+
+
+def test_launcher_stops_the_other_ranks_when_one_fails():
+    """A failing rank ends the launch with its status and the others are terminated (none is left
+    waiting in a collective)."""
+    import time
+    from splendor_gym.parallel import launch_local_ranks
+    code = "import os, sys, time\nif os.environ['RANK'] == '1': sys.exit(5)\ntime.sleep(120)\n"
+    t = time.perf_counter()
+    rc = launch_local_ranks(2, [sys.executable, "-c", code])
+    assert rc == 5 and time.perf_counter() - t < 60
+
+
+def test_bench_gpus_n_refuses_fewer_devices(capsys):
+    """`python bench.py --gpus 2` on a node with one GPU exits 2 with a device-count message and runs
+    nothing; at --gpus 1 bench.main never enters the launcher."""
+    sys.path.insert(0, REPO)
+    import bench
+    assert bench.self_launch(2, ["--gpus", "2"], device_count=1) == 2
+    assert "shows 1 GPU(s); an 2-GPU run needs 2" in capsys.readouterr().err
+    assert bench.self_launch(8, ["--gpus", "8"], device_count=0) == 2
 
 
 def test_single_hip_runtime_after_load():
