@@ -105,7 +105,8 @@ __device__ uint32_t g_bounds_flags;
 #endif
 enum : uint32_t {
     BC_TABLE = 1, BC_SLOT = 2, BC_DECK = 4, BC_LUT = 8, BC_SCRATCH = 16, BC_BYTE = 32, BC_ROWS = 64, BC_CARD = 128,
-    BC_SPIN = 256  // a wave gave up waiting for an LDS hand-off (dealer rollout)
+    BC_SPIN = 256,  // a wave gave up waiting for an LDS hand-off (dealer rollout)
+    BC_BARRIER = 512  // a wave of a multi-team workgroup made another number of s_barriers than 1 + K
 };
 
 // Phase stamps for the diagnostic build only (-DSPL_STAMPS, tools/stamps.py): lane 0 of every
@@ -2132,6 +2133,9 @@ struct PtShared {
     uint32_t seq[2];  // output wave -> poller: tasks posted (pseq), partner tasks seen (cseq)
     uint64_t in[3];   // poller -> output wave: partner progress; pseq << 32 | my next slot's flag;
                       // cseq << 32 | the partner's next slot's flag
+    uint64_t qcons[2];  // quad kernel: in[2] by the parity of the rules step that polled it (the output
+                        // wave's step k reads the rules wave's step k - 1, published before the barrier
+                        // the output wave has passed: guide row 3's barrier between poll and loads)
 };
 
 template <int P>
@@ -2400,21 +2404,26 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void *base) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7FFFFFF0, 0x00020000);
 }
 constexpr int kSc1 = 16;  // buffer-op aux bit: sc1 (write-through store / L1-bypassing load)
+// a flag poll: relaxed agent-scope atomic load = global_load_dword sc1 (MI355X_MICROARCH.md: L1
+// bypassed, L2-served), the poll form of the guide's hand-off rows
 __device__ __forceinline__ uint32_t flag_load(const uint32_t *f) {
-    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc_of(f), 0, 0, kSc1);
+    return __hip_atomic_load(const_cast<uint32_t *>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void flag_store(uint32_t *f, uint32_t v) {  // lane 0 only
     if (lane_id() == 0) __builtin_amdgcn_raw_buffer_store_b32(v, rsrc_of(f), 0, 0, kSc1);
 }
 // a delegated step: the wave's 64 tables' state words after the step -> a delegation slot
-// ([word][lane], 256 contiguous bytes per word), sc1 (write-through) dword stores
+// ([word][lane], 256 contiguous bytes per word), sc1 (write-through) dword stores: relaxed agent-scope
+// atomic stores = global_store_dword sc1; slots are 128-byte aligned (kDelegPayload = 50 lines), so each
+// 128-byte line is written whole by one store instruction of this wave (the guide's row 3 store cell)
 template <int P>
 __device__ __forceinline__ void stage_state(const Tab<P> &T, uint8_t *slot) {
-    const __amdgpu_buffer_rsrc_t r = rsrc_of(slot);
+    uint32_t *const base = reinterpret_cast<uint32_t *>(slot);
 #pragma unroll
     for (int w = 0; w < num_words(P); ++w)
-        __builtin_amdgcn_raw_buffer_store_b32(tab_word(T, w), r, (w * 64 + lane_id()) * 4, 0, kSc1);
+        __hip_atomic_store(base + w * 64 + lane_id(), tab_word(T, w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+static_assert(kDelegPayload % 128 == 0, "partner / delegation slots stay 128-byte aligned");
 // a delegation slot -> the staged tables' state (sc1 loads)
 template <int P>
 __device__ __forceinline__ void unstage_state(const uint8_t *slot, Tab<P> &T) {
@@ -2553,6 +2562,13 @@ constexpr uint64_t kPartnerWait = 500000;  // 5 ms of s_memrealtime (100 MHz): t
 __device__ __forceinline__ uint32_t pt_flag(uint32_t e, int k, uint32_t st) { return e << 16 | (uint32_t)k << 2 | st; }
 __device__ unsigned long long g_partner_stats[2];  // tasks stored by the partner / claimed back (diagnostics)
 
+// READY(launch, step) posted by an agent-scope atomic add (the guide's row 3: "each storing wave for
+// itself", after that wave's s_waitcnt vmcnt(0)).  `seen` is the producer's snapshot of the slot's flag
+// when it chose the slot: 0 or a value of an earlier launch, which nobody else writes in this launch (the
+// consumer writes only flags READY in this launch), so adding target - seen leaves exactly `target`.
+__device__ __forceinline__ void pt_post_ready(uint32_t *f, uint32_t target, uint32_t seen) {
+    if (lane_id() == 0) (void)__hip_atomic_fetch_add(f, target - seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // lane 0 moves a task flag READY -> TAKEN (agent scope: performed past the XCC's L2); wave-uniform
 __device__ __forceinline__ bool pt_claim(uint32_t *f, uint32_t ready) {
     uint32_t seen = 0u;
@@ -2574,15 +2590,23 @@ __device__ __forceinline__ void pt_store_task(const uint8_t *slot, uint8_t *rows
     wave_lds_sync();  // the block's LDS reads are done before the next task's rows land
 }
 // consumer (the partner team's output wave): `v` = the flag of the partner's slot cseq; if it is READY,
-// claim it and store the task's rows (staged through `rows`); true if the slot held a task
+// claim it and store the task's rows (staged through `rows`); true if the slot held a task.  Which
+// form makes the staged words visible (MI355X_MICROARCH.md, "Valid forms" / the hand-off table):
+//   acquire = false: the quad kernel in its steps — the flag was polled by the rules wave (global_load_dword
+//     sc1) before an s_barrier this wave has passed since (row 3: agent-atomic flag, barrier between the
+//     poll and every load, sc1 global stores / buffer_load_dword sc1 loads, one workgroup per CU);
+//   acquire = true: everywhere else (the six-wave dealer, whose poller is not separated from this wave by
+//     a barrier, and every drain after the steps) — the consumer's "always" form: one poll, the claim,
+//     ONE agent acquire, then the loads (this wave's own loads need no further wait).
 template <int P>
 __device__ __forceinline__ bool pt_serve_v(const PartnerLink &pl, uint32_t &cseq, uint32_t v, uint8_t *rows,
-                                           const Consts &C, int32_t *obs, int n) {
+                                           const Consts &C, int32_t *obs, int n, bool acquire) {
     if ((v & 3u) != kPtReady || (v >> 16) != pl.e) return false;
     const int j = (pl.side ^ 1) * kPartnerSlots + (int)(cseq % kPartnerSlots);
     ++cseq;  // tasks fill the ring in order: the next one is in the next slot, whoever stores this one
     uint32_t *f = pl.line(pt_ready_line(j));
     if (!pt_claim(f, v)) return true;
+    if (acquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const int k = (int)((v >> 2) & 0x3FFFu);
     pt_store_task<P>(pl.slot(j), rows, C, obs + ((size_t)k * (size_t)n + (size_t)pl.t0p) * kObsDim);
     // the slot's words were read (the encode used them) before it is free again; no vmcnt wait: the
@@ -2601,12 +2625,13 @@ __device__ __forceinline__ void pt_drain(const PartnerLink &pl, uint32_t &cseq, 
                                          int32_t *obs, int n) {
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        if (pt_serve_v<P>(pl, cseq, (uint32_t)__builtin_amdgcn_readfirstlane(pt_next_flag(pl, cseq)), rows, C, obs, n))
+        if (pt_serve_v<P>(pl, cseq, (uint32_t)__builtin_amdgcn_readfirstlane(pt_next_flag(pl, cseq)), rows, C, obs, n,
+                          true))
             continue;
         const uint32_t dn = (uint32_t)__builtin_amdgcn_readfirstlane(flag_load(pl.line(pt_done_line(pl.side ^ 1))));
         if (dn == pl.e) {  // its READY flags were stored before DONE: what is left of them, then out
             while (pt_serve_v<P>(pl, cseq, (uint32_t)__builtin_amdgcn_readfirstlane(pt_next_flag(pl, cseq)), rows, C,
-                                 obs, n)) {
+                                 obs, n, true)) {
             }
             return;
         }
@@ -2619,11 +2644,11 @@ __device__ __forceinline__ void pt_drain(const PartnerLink &pl, uint32_t &cseq, 
 // waiting), then every task the partner has not taken is claimed back by the same compare-and-swap
 // and its rows are stored here: each handed-off step's rows are stored once, whatever happened after
 template <int P>
-__device__ __forceinline__ void pt_close(const PartnerLink &pl, int ppend, int ppend_k, uint32_t pseq, uint8_t *rows,
-                                         const Consts &C, int32_t *obs, int n, int t0) {
+__device__ __forceinline__ void pt_close(const PartnerLink &pl, int ppend, int ppend_k, uint32_t ppend_seen, uint32_t pseq,
+                                         uint8_t *rows, const Consts &C, int32_t *obs, int n, int t0) {
     if (ppend >= 0) {
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the staged words have completed
-        flag_store(pl.line(pt_ready_line(ppend)), pt_flag(pl.e, ppend_k, kPtReady));
+        pt_post_ready(pl.line(pt_ready_line(ppend)), pt_flag(pl.e, ppend_k, kPtReady), ppend_seen);
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // every READY flag has completed before DONE
     flag_store(pl.line(pt_done_line(pl.side)), pl.e);
@@ -2648,11 +2673,13 @@ __device__ __forceinline__ void pt_close(const PartnerLink &pl, int ppend, int p
 // ends the dealer quietly: a batch posted after that is never dealt, so the rules wave's wait for it
 // runs out and faults the launch (lds_wait_ge).  A faulted workgroup's dealer ends after its batch.
 // the dealer wave's poll of the pair's words for its output wave (a snapshot; tags say which slots)
-__device__ __forceinline__ void pt_publish(PtShared &X, uint32_t a, uint32_t b, uint32_t ps, uint32_t c, uint32_t cs) {
+__device__ __forceinline__ void pt_publish(PtShared &X, uint32_t a, uint32_t b, uint32_t ps, uint32_t c, uint32_t cs,
+                                           int qpar = -1) {
     if (lane_id() == 0) {
         __hip_atomic_store(&X.in[0], (uint64_t)a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_store(&X.in[1], (uint64_t)ps << 32 | b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_store(&X.in[2], (uint64_t)cs << 32 | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(qpar < 0 ? &X.in[2] : &X.qcons[qpar], (uint64_t)cs << 32 | c, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 __device__ __forceinline__ void pt_poll(PtShared &X, const PartnerLink &pl) {
@@ -2797,6 +2824,13 @@ struct WaveRole {
     int role, block;
 };
 // kTeams: 64-table teams per workgroup (the six-wave dealer 2, the quad kernel 4; one workgroup per CU)
+// Barrier invariant: without a dealer wave the two waves of a team hand off through
+// ws_sync(), an s_barrier of the WHOLE workgroup — in the quad kernel (kTeams = 4) all eight waves pass
+// each barrier together.  That is correct only because every wave makes exactly 1 + K ws_sync() calls
+// (one before the roles split, one per step) and none returns early: a per-team early exit or an extra
+// barrier would deadlock the workgroup or pair different steps.  Only the dealer variants leave early
+// (their fault path), and they hand off through LDS counters, not barriers.  The bounds-check build
+// counts each wave's barriers and flags BC_BARRIER when a wave ends with another count.
 template <int P, int TPW, bool kStore, bool kDealer = false, class LdsT = WsLDS<P>, int kTeams = 1>
 __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep S, int K, int refill,
                                            int deleg_every, WaveRole wr = WaveRole{-1, -1}) {
@@ -2853,6 +2887,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 L.pt.seq[0] = L.pt.seq[1] = 0u;
                 L.pt.in[0] = 0ull;
                 L.pt.in[1] = L.pt.in[2] = ~0ull;  // no snapshot yet (tags match no sequence number)
+                L.pt.qcons[0] = L.pt.qcons[1] = ~0ull;
             }
         }
     }
@@ -2898,6 +2933,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         const uint64_t ply0 = S.ply + (S.ply_base ? *S.ply_base : 0ull);
         uint64_t cur_mask = 0ull;
         uint32_t pv[3] = {0u, 0u, 0u}, pps = 0u, pcs = 0u;  // quad kernel's partner poller (loaded a step ahead)
+        int nsync = 0;  // ws_sync() calls in the steps (the barrier invariant above)
         const uint64_t below = (1ull << lane) - 1ull;
 #ifdef SPL_STAMPS
         int rst_lo[kWsStamps] = {0}, rst_hi[kWsStamps] = {0};
@@ -2967,10 +3003,10 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             } else {
                 if (pl.on) {  // the quad kernel's partner poller (the rules wave issues no row stores): the
                               // words loaded last step go to the output wave's snapshots, then new loads
-                    if (k > 0)
+                    if (k > 0)  // the consumer's entry by this step's parity (PtShared::qcons)
                         pt_publish(L.pt, (uint32_t)__builtin_amdgcn_readfirstlane(pv[0]),
                                    (uint32_t)__builtin_amdgcn_readfirstlane(pv[1]), pps,
-                                   (uint32_t)__builtin_amdgcn_readfirstlane(pv[2]), pcs);
+                                   (uint32_t)__builtin_amdgcn_readfirstlane(pv[2]), pcs, k & 1);
                     pps = lds_poll(&L.pt.seq[0]);
                     pcs = lds_poll(&L.pt.seq[1]);
                     pv[0] = flag_load(pl.line(pt_progress_line(pl.side ^ 1)));
@@ -2978,6 +3014,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                     pv[2] = flag_load(pl.line(pt_ready_line((pl.side ^ 1) * kPartnerSlots + (int)(pcs % kPartnerSlots))));
                 }
                 ws_sync();  // hand-off of step k
+                ++nsync;
             }
             WSSTAMP(3, k);
         }
@@ -3008,6 +3045,8 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 g_wsstamps[(((size_t)sid * 2 + 0) * 64 + lane) * kWsStamps + i] =
                     ((uint64_t)(uint32_t)rst_hi[i] << 32) | (uint32_t)rst_lo[i];
 #endif
+        SPL_CHECK(kDealer || nsync == K, BC_BARRIER);
+        (void)nsync;
         if (valid) {
             if (S.next_actions) S.next_actions[t] = action;
             store_tab(T, A, t, cur_mask, K > 0 ? Tb.mtag : 0u);  // cur_mask: the last step's mask of this state
@@ -3039,18 +3078,22 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
         // tasks seen (cseq); the flags and the partner's progress come from the poller's LDS snapshots
         uint32_t pseq = 0u, cseq = 0u;
         int ppend = -1, ppend_k = 0;
+        uint32_t ppend_seen = 0u;  // the staged task's slot flag as the producer saw it (pt_post_ready)
+        int osync = 0;             // ws_sync() calls in the steps (the barrier invariant above)
         for (int k = 0; k < K; ++k) {
             if (pl.on) {
                 if (ppend >= 0) {  // the task staged last step: its words have completed, then READY
                     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-                    flag_store(pl.line(pt_ready_line(ppend)), pt_flag(pl.e, ppend_k, kPtReady));
+                    pt_post_ready(pl.line(pt_ready_line(ppend)), pt_flag(pl.e, ppend_k, kPtReady), ppend_seen);
                     ppend = -1;
                 }
                 // at most one of the partner's tasks per step, between this team's steps (the poller's
-                // snapshot of its next slot, if it is for the task this wave expects)
-                const uint64_t nx = lds_poll64(&L.pt.in[2]);
-                if ((uint32_t)(nx >> 32) == cseq && pt_serve_v<P>(pl, cseq, (uint32_t)nx, L.rows, L, S.obs, A.n) &&
-                    lane == 0)
+                // snapshot of its next slot, if it is for the task this wave expects).  The quad kernel
+                // reads the snapshot its rules wave published at step k - 1, before the s_barrier of step
+                // k - 1 that this wave has passed (PtShared::qcons); the six-wave dealer acquires instead.
+                const uint64_t nx = kDealer ? lds_poll64(&L.pt.in[2]) : lds_poll64(&L.pt.qcons[(k + 1) & 1]);
+                if ((uint32_t)(nx >> 32) == cseq &&
+                    pt_serve_v<P>(pl, cseq, (uint32_t)nx, L.rows, L, S.obs, A.n, kDealer) && lane == 0)
                     __hip_atomic_store(&L.pt.seq[1], cseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             if constexpr (kDealer) {
@@ -3060,12 +3103,13 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                         if (valid) S.flags[(per_step ? (size_t)j * (size_t)A.n : 0) + t] = (uint8_t)SPL_F_FAULT;
                     // steps before k that were handed to the partner: DONE, and those it has not taken are
                     // stored here (they were stepped before the fault)
-                    if (pl.on) pt_close<P>(pl, ppend, ppend_k, pseq, L.rows, L, S.obs, A.n, t0);
+                    if (pl.on) pt_close<P>(pl, ppend, ppend_k, ppend_seen, pseq, L.rows, L, S.obs, A.n, t0);
                     signal_fault(S);
                     return;
                 }
             } else {
                 ws_sync();  // hand-off of step k
+                ++osync;
             }
             WSSTAMP(0, k);
             const int b = k & 1;
@@ -3088,10 +3132,11 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             const bool big_moves = __any(valid && get_moves(T.sw) > 255);
             const bool deleg_now = dl.producer && deleg_step(k, K, dl.every);
             bool handed = false;  // partner hand-off of this step's rows
+            uint32_t sf = 0u;     // the snapshot of the slot's flag it would go to
             if (pl.on && !big_moves) {
                 const uint32_t pp = (uint32_t)lds_poll64(&L.pt.in[0]);
                 const uint64_t ms = lds_poll64(&L.pt.in[1]);
-                const uint32_t sf = (uint32_t)ms;
+                sf = (uint32_t)ms;
                 const bool ahead = pl.lead < 0 || ((pp >> 16) == pl.e && (int)(pp & 0xFFFFu) >= k + pl.lead);
                 // the slot is free (or stale), by a snapshot taken for this very slot
                 handed = ahead && (uint32_t)(ms >> 32) == pseq && ((sf & 3u) == 0u || (sf >> 16) != pl.e);
@@ -3101,6 +3146,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 stage_state(T, pl.slot(j));
                 ppend = j;
                 ppend_k = k;
+                ppend_seen = (uint32_t)__builtin_amdgcn_readfirstlane(sf);
                 ++pseq;
                 if (lane == 0) __hip_atomic_store(&L.pt.seq[0], pseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else if (!deleg_now || big_moves) {  // a delegated step's rows are encoded by the partner
@@ -3166,8 +3212,10 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 flag_store(pl.line(pt_progress_line(pl.side)), pl.e << 16 | (uint32_t)(k + 1));
             WSSTAMP(3, k);
         }
+        SPL_CHECK(kDealer || osync == K, BC_BARRIER);
+        (void)osync;
         if (pl.on) {
-            pt_close<P>(pl, ppend, ppend_k, pseq, L.rows, L, S.obs, A.n, t0);
+            pt_close<P>(pl, ppend, ppend_k, ppend_seen, pseq, L.rows, L, S.obs, A.n, t0);
             pt_drain<P>(pl, cseq, L.rows, L, S.obs, A.n);  // then the partner's, until it is done
         }
 #ifdef SPL_STAMPS

@@ -43,8 +43,11 @@ def main():
         assert np.array_equal(e.obs.cpu().numpy(), ref["obs"]), k
         out["steps"] += n
     # every rollout kernel at 2 / 3 / 4 players, per-step store and in place, fused refills
-    for P, pipe in ((2, True), (2, False), (3, True), (4, True), (4, "half"), (2, "always"), (4, "dealer")):
-        r = Engine(512, P, pipeline=pipe)
+    # (the quad and six-wave dealer kernels with the partner hand-off forced: lead -1; the quad kernel's
+    # barrier count is checked per wave, BC_BARRIER)
+    for P, pipe, lead in ((2, True, None), (2, False, None), (3, True, None), (4, True, None), (4, "half", None),
+                          (2, "always", None), (4, "dealer", None), (2, "quad", -1), (4, "dealer2", -1)):
+        r = Engine(512, P, pipeline=pipe, partner_lead=lead)
         r.reset(seeds=range(512))
         a = torch.zeros(512, dtype=torch.int32, device=r.device)
         r.sample_uniform(out=a, seed=1, ply=0)

@@ -2,7 +2,11 @@
 // the quad kernel's shape (four output waves per workgroup, 256 workgroups) beside one output wave
 // per workgroup (1024 workgroups): the per-step [K][T][297] int32 rows (76 KB per 64-row block) and,
 // with MASK, the [K][T][45] int8 masks, K = 128 steps (10 GB per launch, the headline's).
-//   hipcc -O3 --offload-arch=gfx950 tools/microbench_quad_map.hip -o tools/mbq_map.bin && ./tools/mbq_map.bin
+//   hipcc -O3 --offload-arch=gfx950 tools/microbench_quad_map.hip -o tools/mbq_map.bin && ./tools/mbq_map.bin [T] [rounds]
+// T = 32768 (round 6): config 4's per-GPU share, 4 players x 32 768 tables under the
+// six-wave dealer's shape (two output waves per workgroup on adjacent blocks, one workgroup per CU,
+// 256 workgroups) — the same [K][T][297] rows and [K][T][45] masks (the observation row of every player
+// count is 297 int32).
 // Maps (wave w of workgroup b, nb workgroups, xmap(b) = (b % 8) * (nb / 8) + b / 8, XCD-contiguous):
 //   0 identity        block = b * W + w
 //   1 quad (current)  block = W * xmap(b) + w     (a workgroup's W blocks adjacent)
@@ -10,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -59,8 +64,9 @@ static float timeit(F f, int reps) {
     return ms / reps;
 }
 
-int main() {
-    const int T = 65536, K = 128;
+int main(int argc, char **argv) {
+    const int T = argc > 1 ? atoi(argv[1]) : 65536, K = 128;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 2;
     const size_t bytes = (size_t)K * T * OBS * 4, mbytes = (size_t)K * T * 45;
     v4i *out, *mask;
     CHECK(hipMalloc(&out, bytes));
@@ -72,7 +78,18 @@ int main() {
     };
     printf("# [K][T] row stores + masks, K=%d T=%d: %.2f GB per launch\n", K, T, (bytes + mbytes) / 1e9);
     const double nb2 = (double)bytes + mbytes;
-    for (int round = 0; round < 2; ++round) {
+    if (T != 65536) {  // the C4 share's shape: 2 output waves per workgroup (six-wave dealer), 256 workgroups
+        for (int round = 0; round < rounds; ++round) {
+            rep("W=2 map 1 dealer2 (adjacent blocks) NT", timeit([&] { k_map<true, 1, 2, true><<<waves / 2, 128>>>(out, mask, T, K); }, 4), nb2);
+            rep("W=1 map 1 XCD-contiguous NT", timeit([&] { k_map<true, 1, 1, true><<<waves, 64>>>(out, mask, T, K); }, 4), nb2);
+            rep("W=2 map 1 dealer2 (adjacent blocks) plain", timeit([&] { k_map<false, 1, 2, true><<<waves / 2, 128>>>(out, mask, T, K); }, 4), nb2);
+            rep("W=2 map 0 identity NT", timeit([&] { k_map<true, 0, 2, true><<<waves / 2, 128>>>(out, mask, T, K); }, 4), nb2);
+        }
+        CHECK(hipFree(out));
+        CHECK(hipFree(mask));
+        return 0;
+    }
+    for (int round = 0; round < rounds; ++round) {
         rep("W=1 map 0 identity NT", timeit([&] { k_map<true, 0, 1, true><<<waves, 64>>>(out, mask, T, K); }, 4), nb2);
         rep("W=1 map 1 XCD-contiguous NT", timeit([&] { k_map<true, 1, 1, true><<<waves, 64>>>(out, mask, T, K); }, 4), nb2);
         rep("W=4 map 1 quad (adjacent blocks) NT", timeit([&] { k_map<true, 1, 4, true><<<waves / 4, 256>>>(out, mask, T, K); }, 4), nb2);
