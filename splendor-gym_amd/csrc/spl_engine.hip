@@ -1376,7 +1376,7 @@ __device__ __forceinline__ void load_tab(Tab<P> &T, const KArena &A, int t) {
 // context tagged `tag`), or anything with tag 0 when the storing kernel does not know it.  Every
 // kernel that stores state goes through here, so no stale mask survives a state change.
 template <int P>
-__device__ __forceinline__ void store_tab(const Tab<P> &T, const KArena &A, int t, uint64_t legal, uint32_t tag) {
+__device__ __forceinline__ void store_words(const Tab<P> &T, const KArena &A, int t) {  // state words only
     SPL_CHECK(t >= 0 && t < A.n, BC_TABLE);
 #pragma unroll
     for (int w = 0; w < SW_COUNT; ++w) A.planes[(size_t)w * A.n + t] = T.sw[w];
@@ -1384,8 +1384,15 @@ __device__ __forceinline__ void store_tab(const Tab<P> &T, const KArena &A, int 
     for (int q = 0; q < P; ++q)
 #pragma unroll
         for (int k = 0; k < 4; ++k) A.planes[(size_t)pw_index(q, k) * A.n + t] = T.pw[q][k];
+}
+__device__ __forceinline__ void store_legal(const KArena &A, int t, uint64_t legal, uint32_t tag) {
     A.legal[t] = (uint32_t)legal;
     A.legal[A.n + t] = ((uint32_t)(legal >> 32) & kLegalHiBits) | (tag << kLegalTagShift);
+}
+template <int P>
+__device__ __forceinline__ void store_tab(const Tab<P> &T, const KArena &A, int t, uint64_t legal, uint32_t tag) {
+    store_words(T, A, t);
+    store_legal(A, t, legal, tag);
 }
 
 // the cached legal mask of table t's stored state, if it was computed under context tag `tag`
@@ -2213,12 +2220,25 @@ __device__ __forceinline__ void ws_sync() {
 // envs/splendor_env.py:81) and stores the masks, small outputs, next action and state.  The
 // output wave also stages the constant tables while the rules wave's state loads
 // are in flight.  (Terminal rows written per lane by the rules wave instead: 27.5 -> 29.0 us.)  Same outputs, bit for bit, as k_step (the GPU parity suite runs through it).
+// SPL_STEP_TAIL (default 1, round 6): a third wave per 64 tables, the TAIL wave, takes the legal mask
+// of the new state (engine legal_moves, envs/splendor_env.py:81), the mask block, the fused policy's
+// next action and the legal-mask cache entry off the rules wave's tail; hand-off 2 (rules -> output: row
+// halves staged) becomes an LDS counter, so the tail wave never waits on the other two after hand-off 1.
+// 0: round 5's two waves (the rules wave evaluates the mask after hand-off 2).  Same outputs either way.
+#ifndef SPL_STEP_TAIL
+#define SPL_STEP_TAIL 1
+#endif
+constexpr bool kStepTail = SPL_STEP_TAIL != 0;
+constexpr int kStepThreads = kStepTail ? 192 : 128;
+
 template <int P>
 struct __align__(16) StepWsLDS : Consts {
     static constexpr int kW = SW_COUNT + 4 * P;  // state words per table
     uint32_t st[kW][64];   // state after the step (and autoreset)
     uint32_t fst[kW][64];  // pre-reset state of the tables that ended (final_observation)
     uint64_t mask[64];
+    uint64_t omask[64];    // rules -> tail wave: each lane's step mask (kMaskDeferred: legal_moves to evaluate)
+    uint32_t halves;       // rules -> output wave: row halves staged (hand-off 2 with the tail wave)
     uint32_t mbits[96];
     // observation staging (rows of 297 bytes, or 300 for obs_u8); before hand-off 1 the rules wave's
     // deal scratch + LaneMT
@@ -2226,11 +2246,42 @@ struct __align__(16) StepWsLDS : Consts {
 };
 static_assert(sizeof(StepWsLDS<4>) <= 40960, "k_step_ws_* needs four workgroups per CU");
 
+// Bounded LDS waits (the dealer rollout's and the three-wave step's): a wait that runs out faults the
+// launch — the serial goes to the context's host-mapped fault word — instead of spinning forever.
+constexpr uint32_t kSpinLimit = 1u << 22;
+__device__ uint32_t g_spin_limit = kSpinLimit;
+__device__ __forceinline__ void signal_fault(const KStep &S) {
+    if (S.fault && lane_id() == 0)  // a vector store (system scope: write-through to the host-mapped word)
+        __hip_atomic_store(S.fault, S.fault_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// hand-off 2 of the three-wave step (rules -> output wave) as an LDS counter: a bounded wait (a lost
+// hand-off faults the launch loudly, as the dealer rollout's waits do, instead of spinning)
+__device__ __forceinline__ void step_publish(uint32_t *p) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's row halves have landed in LDS
+    if (lane_id() == 0) __hip_atomic_store(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool step_wait(const uint32_t *p) {
+    const uint32_t limit = g_spin_limit;
+    for (uint32_t spins = 0;; ++spins) {
+        const uint32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // later LDS reads stay below the poll
+        if (v) return true;
+        if (spins >= limit) {
+            SPL_CHECK(false, BC_SPIN);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
 template <int P>
 __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, KStep S) {
     constexpr int kW = StepWsLDS<P>::kW;
     const int lane = lane_id();
-    const bool rules_wave = threadIdx.x < 64;
+    const int role = (int)(threadIdx.x >> 6);  // 0 rules, 1 output, 2 tail (kStepTail)
+    const bool rules_wave = role == 0;
     const int t0 = wg_block() * 64;
     const int t = t0 + lane;
     const bool valid = t < A.n;
@@ -2238,6 +2289,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
     const bool want_final = S.autoreset && S.final_obs != nullptr;
     const bool compact = S.obs_u8 != nullptr && S.obs == nullptr;  // obs_u8 rows instead of int32 obs rows
     STAMP(0);
+    if (kStepTail && rules_wave && lane == 0) L.halves = 0u;  // read only after hand-off 1
     if (rules_wave) {
         __builtin_amdgcn_s_setprio(SPL_WS_PRIO);  // as in the rollout: 27.9 -> 27.3 us
         Tab<P> T;
@@ -2283,6 +2335,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
             autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], mtx, o, pool_dirty);
 #pragma unroll
         for (int w = 0; w < kW; ++w) L.st[w][lane] = tab_word(T, w);
+        if (kStepTail) L.omask[lane] = o.mask;  // the tail wave evaluates the deferred lanes' masks
         STAMP(3);
         ws_sync();  // hand-off 1: state words (deal scratch in `rows` free again)
         // this wave encodes the first half of every row while the output wave encodes the second
@@ -2290,7 +2343,8 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         if (abl(ABL_ENCODE)) {
         } else if (compact) encode_row_u8<0>(T, L.rows, L);
         else encode_row_half<0>(T, L.rows, L);
-        ws_sync();  // hand-off 2: first row halves staged
+        if (kStepTail) step_publish(&L.halves);  // hand-off 2 (the tail wave takes no part)
+        else ws_sync();                          // hand-off 2: first row halves staged
         STAMP(4);
         if (fin_all && !abl(ABL_FINAL)) {  // info["final_observation"] rows: each by the whole wave, from its listed words
             // (four rows at a time, their LDS lookups overlapped, measured slower: 23.4 vs 23.2 us per step
@@ -2303,12 +2357,14 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         }
         STAMP(7);
         STAMPV(9, __popcll(fin_all) | (__popcll(__ballot((o.mask & kMaskDeferred) != 0)) << 8));
-        if (o.mask & kMaskDeferred) o.mask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);
-        STAMP(5);
-        // masks and small outputs leave from this wave while the output wave streams the rows
-        L.mask[lane] = o.mask;
-        wave_lds_sync();
-        if (!abl(ABL_MASK_STORE)) store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+        if (!kStepTail) {
+            if (o.mask & kMaskDeferred) o.mask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);
+            STAMP(5);
+            // masks and small outputs leave from this wave while the output wave streams the rows
+            L.mask[lane] = o.mask;
+            wave_lds_sync();
+            if (!abl(ABL_MASK_STORE)) store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+        }
         STAMP(8);
         store_step_info(S, A.n, t, valid, o.flags);
         if (valid) {
@@ -2320,15 +2376,19 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
                 if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_add);
                 if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
             }
-            if (S.next_actions) {
-                const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
-                S.next_actions[t] = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply);
+            if (kStepTail) {
+                store_words(T, A, t);  // the legal-mask cache entry is the tail wave's
+            } else {
+                if (S.next_actions) {
+                    const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
+                    S.next_actions[t] = policy_action(S.policy, o.mask, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply);
+                }
+                store_tab(T, A, t, o.mask, Tb.mtag);  // o.mask: legal_moves of the stored (stepped, autoreset) state
             }
-            store_tab(T, A, t, o.mask, Tb.mtag);  // o.mask: legal_moves of the stored (stepped, autoreset) state
             if (pool_dirty) store_pool(A, t, pool);
         }
         STAMP(6);
-    } else {
+    } else if (role == 1) {
         STAMP(1);
         STAMP(2);
         ws_sync();  // hand-off 1 (the rules wave's table DMA landed before it)
@@ -2339,7 +2399,11 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         if (abl(ABL_ENCODE)) {
         } else if (compact) encode_row_u8<1>(T, L.rows, L);
         else encode_row_half<1>(T, L.rows, L);
-        ws_sync();  // hand-off 2
+        if (kStepTail) {
+            if (!step_wait(&L.halves)) signal_fault(S);  // hand-off 2 lost: the launch says so (rows stale)
+        } else {
+            ws_sync();  // hand-off 2
+        }
         STAMP(4);
         STAMP(5);
         if (compact) {
@@ -2356,6 +2420,26 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
             if (valid && get_moves(T.sw) > 255) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
         }
         STAMP(7);
+    } else if (kStepTail) {
+        // the TAIL wave: from hand-off 1 on, the new state's legal mask (engine legal_moves, deferred
+        // lanes only: reset tables carry the fresh deal's, terminal ones none), the mask block, the fused
+        // policy's next action and the legal-mask cache entry
+        ws_sync();  // hand-off 1
+        Tab<P> T;
+#pragma unroll
+        for (int w = 0; w < kW; ++w) set_tab_word(T, w, L.st[w][lane]);
+        uint64_t m = L.omask[lane];
+        if (m & kMaskDeferred) m = abl(ABL_LEGAL_POST) ? 0ull : legal_of(T, L);
+        L.mask[lane] = m;
+        wave_lds_sync();
+        if (!abl(ABL_MASK_STORE)) store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+        if (valid) {
+            if (S.next_actions) {
+                const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
+                S.next_actions[t] = policy_action(S.policy, m, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply);
+            }
+            store_legal(A, t, m, Tb.mtag);  // m: legal_moves of the state the rules wave stores
+        }
     }
 }
 
@@ -2363,7 +2447,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
 template <int P>
 struct StepWsKernel;
 #define SPL_STEP_WS_KERNEL(NAME, P_)                                                   \
-    __global__ __launch_bounds__(128) void NAME(KArena A, KTables Tb, KStep S) {         \
+    __global__ __launch_bounds__(kStepThreads) void NAME(KArena A, KTables Tb, KStep S) { \
         __shared__ StepWsLDS<P_> L;                                                      \
         step_ws<P_>(L, A, Tb, S);                                                        \
     }                                                                                    \
@@ -2496,12 +2580,6 @@ __device__ __forceinline__ void lds_publish(uint32_t *p, uint32_t v) {
 //     spl_ctx_faults reads without synchronising (Engine / SplendorVectorEnv / bench.py raise on it).
 // spl_debug_set_spin_limit lowers the limit so a test can force the path (BC_SPIN still marks it in
 // the bounds-check build).
-constexpr uint32_t kSpinLimit = 1u << 22;
-__device__ uint32_t g_spin_limit = kSpinLimit;
-__device__ __forceinline__ void signal_fault(const KStep &S) {
-    if (S.fault && lane_id() == 0)  // a vector store (system scope: write-through to the host-mapped word)
-        __hip_atomic_store(S.fault, S.fault_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 // true once *p >= v; false when the wait ran out or another wave of the workgroup already faulted
 __device__ __forceinline__ bool lds_wait_ge(DealerLDS &D, const uint32_t *p, uint32_t v) {
     const uint32_t limit = g_spin_limit;
@@ -4244,7 +4322,7 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     const KArena A = karena(arena);
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (kStepWs) {
-        DISPATCH_P(arena->players, hipLaunchKernelGGL(StepWsKernel<PP>::fn, dim3(blocks_for(arena->n)), dim3(128), 0, s, A,
+        DISPATCH_P(arena->players, hipLaunchKernelGGL(StepWsKernel<PP>::fn, dim3(blocks_for(arena->n)), dim3(kStepThreads), 0, s, A,
                                                       ktables(ctx), S));
     } else {
         DISPATCH_P(arena->players,

@@ -1161,13 +1161,15 @@ __device__ __forceinline__ void act32_narrow_body(const uint8_t *__restrict__ Wb
     __shared__ uint8_t ms[kMaskWave];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
     const int b = (int)blockIdx.x, G = a.groups;
-    const int32_t *ntab = a.gtab + 2 * G + 2;  // per group: first narrow workgroup; ntab[G] = total
-    if (b >= ntab[G]) return;                  // past the last tail's workgroups (every wave leaves)
-    int grp = 0;
-    for (int i = 1; i < G; ++i) grp = ntab[i] <= b ? i : grp;
+    // this workgroup's (network, tile of its tail) from the XCD-aware map k_group_place wrote (round 6):
+    // every tile of one network's tail runs on ONE XCD (blocks b and b + 8 share one), so the network's
+    // image is pulled into that XCD's L2 once and its other tiles hit there; -1: no tile (leave)
+    const int e = a.order[(size_t)a.n + b];
+    if (e < 0) return;
+    const int grp = e >> 8, tile = e & 255;
     const uint8_t *W = Wbase + (size_t)grp * a.image_stride;
     const int64_t gfirst = a.gtab[G + 1 + grp], gend = a.gtab[G + 2 + grp];
-    const int64_t tbase = gfirst + (gend - gfirst) / kRowsPerBlock * kRowsPerBlock + (int64_t)(b - ntab[grp]) * kRowsPerWave;
+    const int64_t tbase = gfirst + (gend - gfirst) / kRowsPerBlock * kRowsPerBlock + (int64_t)tile * kRowsPerWave;
     const int valid = (int)max<int64_t>(0, min<int64_t>(kRowsPerWave, gend - tbase));
     const int32_t tid_own = lane < valid ? a.order[tbase + lane] : 0;
     const int64_t xt = valid > 0 ? (int64_t)__shfl(tid_own, r < valid ? r : 0) : 0;
@@ -1288,10 +1290,16 @@ __global__ __launch_bounds__(256) void k_group_count(int n, int G, const int32_t
 // (16-table tail) workgroup of k_act32_narrow.  The grouped k_act32 launch that follows zeroes
 // counts and cursors for the next call's k_group_count (ActArgs.group_reset: no memset launch, and
 // no last-workgroup ticket here — 256 serialised atomics on one word cost this kernel ~7 us).
+// narrow workgroups launched per grouped call: 8 XCDs x (tiles of at most ceil(G / 8) networks, 8 each)
+static_assert(kRowsPerBlock / kRowsPerWave == 8, "a tail holds at most 8 sixteen-table tiles");
+__host__ __device__ constexpr int narrow_grid(int G) { return 64 * ((G + 7) / 8); }
 __global__ __launch_bounds__(256) void k_group_place(int n, int G, const int32_t *group_of, const int32_t *counts,
                                                      int32_t *cursor, int32_t *gtab, int32_t *order) {
     __shared__ int32_t cnt[64], base[64], start[64], tot[64];
     if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+    int32_t *const nmap = order + n;  // narrow block -> (network << 8 | tail tile), -1 none
+    if (blockIdx.x == 0)
+        for (int i = threadIdx.x; i < narrow_grid(G); i += 256) nmap[i] = -1;
     if (threadIdx.x < G) tot[threadIdx.x] = counts[threadIdx.x];  // one batch of loads, not G dependent trips
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1314,6 +1322,13 @@ __global__ __launch_bounds__(256) void k_group_place(int n, int G, const int32_t
             gtab[G] = wg;
             ntab[G] = nw;
             gtab[2 * G + 1] = pos;
+            // the tails' tiles, XCD-aware: network g's on XCD g % 8 (blocks 8 s + g % 8), consecutive s
+            int fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int g = 0; g < G; ++g) {
+                const int tiles = (tot[g] % kRowsPerBlock + kRowsPerWave - 1) / kRowsPerWave, x = g & 7;
+                for (int i = 0; i < tiles; ++i) nmap[8 * (fill[x] + i) + x] = g << 8 | i;
+                fill[x] += tiles;
+            }
         }
     }
     __syncthreads();
@@ -1329,7 +1344,10 @@ __global__ __launch_bounds__(256) void k_group_place(int n, int G, const int32_t
 
 constexpr int kMaxGroups = 64;
 
-int64_t splp32_group_scratch(int32_t n, int32_t groups) { return 4 * ((int64_t)5 * groups + 3 + n); }
+// counts[G] | cursor[G] | gtab[2G + 2] | ntab[G + 1] | order[n] | nmap[narrow_grid(G)]
+int64_t splp32_group_scratch(int32_t n, int32_t groups) {
+    return 4 * ((int64_t)5 * groups + 3 + n + narrow_grid(groups));
+}
 
 template <template <bool, bool> class K>
 struct ActKernels {  // the four instantiations of one format's kernel template
@@ -1384,7 +1402,7 @@ int splp32_act(const uint8_t *img, bool has_critic, bool critic, bool sample, in
     if (fmt) ActKernels<HalfK>::launch(W, critic, sample, grid, block, s, a);
     else ActKernels<ExactK>::launch(W, critic, sample, grid, block, s, a);
     if (groups > 0) {  // the groups' tails: at most 8 wave-tiles of 16 tables per group
-        const dim3 ngrid((unsigned)(groups * (kRowsPerBlock / kRowsPerWave))), nblock(kNarrowWaves * 64);
+        const dim3 ngrid((unsigned)narrow_grid(groups)), nblock(kNarrowWaves * 64);
         if (fmt && sample) hipLaunchKernelGGL(k_act32h_narrow<true>, ngrid, nblock, 0, s, W, a);
         else if (fmt) hipLaunchKernelGGL(k_act32h_narrow<false>, ngrid, nblock, 0, s, W, a);
         else if (sample) hipLaunchKernelGGL(k_act32_narrow<true>, ngrid, nblock, 0, s, W, a);

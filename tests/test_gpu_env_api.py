@@ -306,6 +306,43 @@ def test_single_env_matches_oracle_with_stream_continuation():
             np.testing.assert_array_equal(obs, ref["obs"][0])
 
 
+def test_single_env_without_a_same_address_host_mapping_matches_oracle(monkeypatch):
+    """SplendorEnv hands the kernels its pinned I/O block's host address only when
+    spl_host_mapped says the device sees it at that address; otherwise (forced here) it steps through a
+    device block with copies, with the same results as the oracle, masks and errors included."""
+    from splendor_gym.device import Engine
+    monkeypatch.setattr(Engine, "_host_mapped", lambda self, ptr: False)
+    orc = Oracle()
+    env = make_env()
+    vec = OracleVec(orc, 1, 2, [77])
+    obs, info = env.reset(seed=77)
+    assert not env._eng.host_io and env._eng.io.is_cuda
+    np.testing.assert_array_equal(obs, vec.obs[0])
+    np.testing.assert_array_equal(env.legal_mask(), info["action_mask"])
+    rs = np.random.default_rng(3)
+    for _ in range(120):
+        legal = np.flatnonzero(info["action_mask"])
+        a = int(rs.choice(legal)) if len(legal) else 0
+        obs, r, term, trunc, info = env.step(a)
+        ref = vec.step(np.array([a], np.int32), want_final=True)
+        np.testing.assert_array_equal(obs, ref["final_obs"][0] if term else ref["obs"][0])
+        assert np.float32(r) == ref["reward"][0]
+        if term:
+            obs, info = env.reset()
+            np.testing.assert_array_equal(obs, ref["obs"][0])
+    with pytest.raises(ValueError):
+        env.step(45)
+
+
+def test_pinned_io_block_is_mapped_at_its_own_address():
+    """The probe itself on this box: torch's pinned host allocator hands out hipHostMalloc memory that
+    the device sees at the same address (so SplendorEnv takes the zero-copy path)."""
+    env = make_env()
+    env.reset(seed=1)
+    e = env._eng
+    assert e.host_io and e._host_mapped(e.io.data_ptr())
+
+
 def test_vector_env_matches_single_envs_and_autoresets():
     import torch
     from splendor_gym import SplendorVectorEnv
