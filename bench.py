@@ -60,8 +60,10 @@ STATE_BYTES = {2: 64, 3: 83, 4: 102}
 # + flags u8 + winner i8
 OUT_BYTES = 297 * 4 + 45 + 4 + 1 + 1 + 1
 OBS_ROW = 297 * 4
-# SURVEY.md §8d drop-in figure for k_step: 2*S_P + obs + mask + action + reward + terminated
-STEP_ALGO_BYTES = {p: 2 * s + 297 * 4 + 45 + 4 + 4 + 1 for p, s in STATE_BYTES.items()}  # 2p: 1370
+# SURVEY.md §8d drop-in figure for k_step: 2*S_P + obs + mask + action + reward + terminated, + 16 B of
+# the legal-mask cache (round 6, ABI 9: 8 B read with the state, 8 B written with it; not part of S_P)
+LEGAL_CACHE_BYTES = 16
+STEP_ALGO_BYTES = {p: 2 * s + LEGAL_CACHE_BYTES + 297 * 4 + 45 + 4 + 4 + 1 for p, s in STATE_BYTES.items()}  # 2p: 1386
 # pool refill period per player count: three pool deals per table must cover the resets between
 # refills (random games last ~77 plies at 2p, ~29 at 4p)
 REFILL_EVERY = {2: 64, 3: 32, 4: 16}
@@ -629,6 +631,9 @@ def main():
                     help="rollout store: every n-th step the odd-XCC workgroups' rows are stored by their "
                          "even-XCC partners (0 = off, the library default: a 1.5 %% gain, "
                          "profiles/r03/deleg_ab_r03a.txt)")
+    ap.add_argument("--step-tail", choices=("auto", "0", "1"), default="auto",
+                    help="spl_step kernel shape: auto (the library's choice by grid size), 0 two waves, 1 three waves "
+                         "(a tail wave takes the legal mask off the rules wave); same results")
     ap.add_argument("--partner-lead", type=int, default=None,
                     help="six-wave dealer rollout store: a team this many steps behind its neighbouring-XCC "
                          "partner hands it whole steps of rows (library default 4; 0 = off)")
@@ -671,7 +676,8 @@ def main():
     pipe = {"auto": True, "always": "always", "half": "half", "off": False, "dealer": "dealer",
             "dealer2": "dealer2", "quad": "quad"}[args.pipeline]
     eng = Engine(T, P, device=dev, refill_period=R, table0=table0, refill_fused=args.refill == "fused",
-                 pipeline=pipe, delegation=args.delegation, partner_lead=args.partner_lead)
+                 pipeline=pipe, delegation=args.delegation, partner_lead=args.partner_lead,
+                 step_tail=None if args.step_tail == "auto" else int(args.step_tail))
     eng.reset(seeds=range(table0, table0 + T))
     lib = eng.lib
     buf = [torch.zeros(T, dtype=torch.int32, device=dev) for _ in range(2)]
@@ -736,8 +742,10 @@ def main():
 
     def kernel_name(variant):
         """The kernel the variant launches, as rocprofv3 names it (one name per instantiation)."""
-        if variant == "step":
-            return f"k_step_ws_{P}p"
+        if variant == "step":  # spl_step's shape: three waves (wst) up to two workgroups per CU unless forced
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count
+            tail = args.step_tail == "1" or (args.step_tail == "auto" and -(-T // 64) <= 2 * cus)
+            return f"k_step_{'wst' if tail else 'ws'}_{P}p"
         return eng.rollout_kernel_name(per_step=variant == "rollout_store")
 
     def events(n):
@@ -861,7 +869,8 @@ def main():
         launches = K // per
         if v == "step":
             algo = STEP_ALGO_BYTES[P] * T
-            algo_note = f"{STEP_ALGO_BYTES[P]} B per table-step (SURVEY.md §8d: 2*S_P + obs + mask + action + reward + terminated)"
+            algo_note = (f"{STEP_ALGO_BYTES[P]} B per table-step (SURVEY.md §8d: 2*S_P + obs + mask + action + reward + "
+                         f"terminated = {STEP_ALGO_BYTES[P] - LEGAL_CACHE_BYTES}, + {LEGAL_CACHE_BYTES} B of legal-mask cache)")
         else:
             # state read+write once per launch, first/next actions, per-step outputs, terminal rows
             term_per_launch = rec["terminations"] / launches

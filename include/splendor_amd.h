@@ -45,7 +45,8 @@ extern "C" {
 #endif
 
 #define SPL_ABI_VERSION 9  /* 9: the arena holds a legal-mask cache ([2][n] u32 after the delegation flags,
-                                 spl_arena_bytes grows by 8 B per table; spl_step reads it), spl_host_mapped;
+                                 spl_arena_bytes grows by 8 B per table; spl_step reads it), spl_host_mapped,
+                                 spl_ctx_set_step_tail;
                               8: spl_step with both obs and obs_u8 writes both (the compact rows as a copy);
                                  splendor_dual.h spl_dual_io_t gained a trailing step_counter (zero-initialise);
                               7: spl_ctx_set_partner_lead, spl_debug_partner_stats (rollout-store partner hand-off);
@@ -177,6 +178,12 @@ int spl_ctx_set_rollout_delegation(spl_ctx_t *ctx, int every);
  * is free (tests).  Other kernels ignore it.  Default SPL_PARTNER_LEAD (4; DESIGN.md §2 gives the
  * measured A/B).  Results are identical either way. */
 int spl_ctx_set_partner_lead(spl_ctx_t *ctx, int lead);
+/* spl_step's kernel shape (round 6): 1 = three waves per 64 tables (k_step_wst_<P>p: a TAIL wave takes
+ * the new state's legal mask, the mask block, the fused policy's action and the legal-mask cache off the
+ * rules wave), 0 = two waves (k_step_ws_<P>p), -1 = auto (default): three waves up to two workgroups per
+ * CU, two above (measured: 17.4 -> 14.7 us per step at 16 384 tables, 22.4 -> 22.9 us at 65 536).
+ * Results are identical either way. */
+int spl_ctx_set_step_tail(spl_ctx_t *ctx, int mode);
 /* The name of the kernel spl_rollout launches for n tables of `players` players under the context's
  * settings (e.g. "k_rollout_store_2p", "k_rollout_inplace_half_4p"): every instantiation has a name
  * of its own, so a rocprofv3 summary row maps to one variant.  NULL (spl_last_error) on bad input. */

@@ -2220,16 +2220,15 @@ __device__ __forceinline__ void ws_sync() {
 // envs/splendor_env.py:81) and stores the masks, small outputs, next action and state.  The
 // output wave also stages the constant tables while the rules wave's state loads
 // are in flight.  (Terminal rows written per lane by the rules wave instead: 27.5 -> 29.0 us.)  Same outputs, bit for bit, as k_step (the GPU parity suite runs through it).
-// SPL_STEP_TAIL (default 1, round 6): a third wave per 64 tables, the TAIL wave, takes the legal mask
-// of the new state (engine legal_moves, envs/splendor_env.py:81), the mask block, the fused policy's
-// next action and the legal-mask cache entry off the rules wave's tail; hand-off 2 (rules -> output: row
-// halves staged) becomes an LDS counter, so the tail wave never waits on the other two after hand-off 1.
-// 0: round 5's two waves (the rules wave evaluates the mask after hand-off 2).  Same outputs either way.
-#ifndef SPL_STEP_TAIL
-#define SPL_STEP_TAIL 1
-#endif
-constexpr bool kStepTail = SPL_STEP_TAIL != 0;
-constexpr int kStepThreads = kStepTail ? 192 : 128;
+// The TAIL wave (round 6; k_step_wst_<P>p): a third wave per 64 tables takes the legal mask of the new
+// state (engine legal_moves, envs/splendor_env.py:81), the mask block, the fused policy's next action
+// and the legal-mask cache entry off the rules wave's tail; hand-off 2 (rules -> output: row halves
+// staged) becomes an LDS counter, so the tail wave never waits on the other two after hand-off 1.
+// Without it (k_step_ws_<P>p, round 5's two waves) the rules wave evaluates the mask after hand-off 2.
+// Same outputs either way.  Measured alternating on one box (profiles/r06/stepab_r06g.txt, graph
+// events per step): 16 384 tables 17.4 -> 14.7 us with the tail wave; 65 536 tables 22.4 -> 22.9 us
+// (four workgroups per CU: 12 waves share the SIMDs and the LDS) — so spl_step picks it by grid size
+// (spl_ctx_set_step_tail: auto = at most ctx->step_tail_blocks workgroups).
 
 template <int P>
 struct __align__(16) StepWsLDS : Consts {
@@ -2276,7 +2275,7 @@ __device__ __forceinline__ bool step_wait(const uint32_t *p) {
     }
 }
 
-template <int P>
+template <int P, bool kStepTail>
 __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, KStep S) {
     constexpr int kW = StepWsLDS<P>::kW;
     const int lane = lane_id();
@@ -2443,21 +2442,24 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
     }
 }
 
-// one kernel name per player count (see RolloutKernel)
-template <int P>
+// one kernel name per player count and shape (see RolloutKernel)
+template <int P, bool kTail>
 struct StepWsKernel;
-#define SPL_STEP_WS_KERNEL(NAME, P_)                                                   \
-    __global__ __launch_bounds__(kStepThreads) void NAME(KArena A, KTables Tb, KStep S) { \
-        __shared__ StepWsLDS<P_> L;                                                      \
-        step_ws<P_>(L, A, Tb, S);                                                        \
-    }                                                                                    \
-    template <>                                                                          \
-    struct StepWsKernel<P_> {                                                            \
-        static constexpr void (*fn)(KArena, KTables, KStep) = NAME;                      \
+#define SPL_STEP_WS_KERNEL(NAME, P_, TAIL_)                                                  \
+    __global__ __launch_bounds__(TAIL_ ? 192 : 128) void NAME(KArena A, KTables Tb, KStep S) { \
+        __shared__ StepWsLDS<P_> L;                                                           \
+        step_ws<P_, TAIL_>(L, A, Tb, S);                                                      \
+    }                                                                                         \
+    template <>                                                                               \
+    struct StepWsKernel<P_, TAIL_> {                                                          \
+        static constexpr void (*fn)(KArena, KTables, KStep) = NAME;                           \
     };
-SPL_STEP_WS_KERNEL(k_step_ws_2p, 2)
-SPL_STEP_WS_KERNEL(k_step_ws_3p, 3)
-SPL_STEP_WS_KERNEL(k_step_ws_4p, 4)
+SPL_STEP_WS_KERNEL(k_step_ws_2p, 2, false)
+SPL_STEP_WS_KERNEL(k_step_ws_3p, 3, false)
+SPL_STEP_WS_KERNEL(k_step_ws_4p, 4, false)
+SPL_STEP_WS_KERNEL(k_step_wst_2p, 2, true)
+SPL_STEP_WS_KERNEL(k_step_wst_3p, 3, true)
+SPL_STEP_WS_KERNEL(k_step_wst_4p, 4, true)
 #undef SPL_STEP_WS_KERNEL
 
 // Rollout-store delegation (rollout_ws<P, 64, true>, spl_ctx_set_rollout_delegation).  The
@@ -3894,6 +3896,8 @@ struct spl_ctx_s {
     int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
     int partner_lead;    // six-wave dealer per-step store: partner hand-off lead in steps (0 off, < 0 forced)
     uint32_t mtag;         // legal-mask cache tag of this context (its card table), 1..65535
+    int step_tail;         // spl_step shape: -1 auto (the tail wave up to step_tail_blocks workgroups), 0 two waves, 1 three
+    int64_t step_tail_blocks;
     uint64_t *fault_host;  // host-mapped, fine-grained: the serial of a launch that faulted (0 = none), spl_ctx_faults
     uint64_t *fault_dev;   // its device address (KStep::fault)
     uint64_t launches;     // launch serial (KStep::fault_tag)
@@ -4089,6 +4093,12 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     c->refill_fused = 1;
     c->deleg_every = SPL_DELEG_EVERY;
     c->partner_lead = SPL_PARTNER_LEAD;
+    c->step_tail = -1;
+    {
+        int cus = 0;
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        c->step_tail_blocks = 2 * (int64_t)cus;  // up to two workgroups per CU (32 768 tables on 256 CUs)
+    }
     c->pipeline = 1;
     memcpy(c->ws_resident, ws_resident, sizeof(ws_resident));
     memcpy(c->dealer_resident, dealer_resident, sizeof(dealer_resident));
@@ -4168,6 +4178,12 @@ int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on) {
     if (!ctx) return fail(SPL_E_ARG, "null ctx");
     if (on < 0 || on > 6) return fail(SPL_E_ARG, "rollout pipeline must be 0..6");
     ctx->pipeline = on;
+    return SPL_OK;
+}
+
+int spl_ctx_set_step_tail(spl_ctx_t *ctx, int mode) {
+    if (!ctx || mode < -1 || mode > 1) return fail(SPL_E_ARG, "step tail mode must be -1 (auto), 0 or 1");
+    ctx->step_tail = mode;
     return SPL_OK;
 }
 
@@ -4322,8 +4338,14 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     const KArena A = karena(arena);
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (kStepWs) {
-        DISPATCH_P(arena->players, hipLaunchKernelGGL(StepWsKernel<PP>::fn, dim3(blocks_for(arena->n)), dim3(kStepThreads), 0, s, A,
-                                                      ktables(ctx), S));
+        const unsigned blocks = blocks_for(arena->n);
+        const bool tail = ctx->step_tail > 0 || (ctx->step_tail < 0 && (int64_t)blocks <= ctx->step_tail_blocks);
+        if (tail)
+            DISPATCH_P(arena->players, hipLaunchKernelGGL((StepWsKernel<PP, true>::fn), dim3(blocks), dim3(192), 0, s, A,
+                                                          ktables(ctx), S))
+        else
+            DISPATCH_P(arena->players, hipLaunchKernelGGL((StepWsKernel<PP, false>::fn), dim3(blocks), dim3(128), 0, s, A,
+                                                          ktables(ctx), S))
     } else {
         DISPATCH_P(arena->players,
                    hipLaunchKernelGGL((k_step<PP, kStepWaves>), dim3((unsigned)((arena->n + 64 * kStepWaves - 1) / (64 * kStepWaves))),

@@ -1322,16 +1322,20 @@ __global__ __launch_bounds__(256) void k_group_place(int n, int G, const int32_t
             gtab[G] = wg;
             ntab[G] = nw;
             gtab[2 * G + 1] = pos;
-            // the tails' tiles, XCD-aware: network g's on XCD g % 8 (blocks 8 s + g % 8), consecutive s
-            int fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int g = 0; g < G; ++g) {
-                const int tiles = (tot[g] % kRowsPerBlock + kRowsPerWave - 1) / kRowsPerWave, x = g & 7;
-                for (int i = 0; i < tiles; ++i) nmap[8 * (fill[x] + i) + x] = g << 8 | i;
-                fill[x] += tiles;
-            }
         }
     }
     __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x < 8) {
+        // the tails' tiles, XCD-aware, one thread per XCD x: network g's tiles on XCD g % 8 (blocks
+        // 8 s + g % 8, consecutive s); written after every thread's -1 above (two barriers since)
+        const int x = threadIdx.x;
+        int fill = 0;
+        for (int g = x; g < G; g += 8) {
+            const int tiles = (tot[g] % kRowsPerBlock + kRowsPerWave - 1) / kRowsPerWave;
+            for (int i = 0; i < tiles; ++i) nmap[8 * (fill + i) + x] = g << 8 | i;
+            fill += tiles;
+        }
+    }
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int g = i < n ? group_of[i] : -1;
     const bool in = g >= 0 && g < G;

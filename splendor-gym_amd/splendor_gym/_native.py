@@ -99,6 +99,7 @@ SIGNATURES = {
     "spl_ctx_set_rollout_pipeline": ([c_void_p, c_int32], c_int32),
     "spl_ctx_set_rollout_delegation": ([c_void_p, c_int32], c_int32),
     "spl_ctx_set_partner_lead": ([c_void_p, c_int32], c_int32),
+    "spl_ctx_set_step_tail": ([c_void_p, c_int32], c_int32),
     "spl_ctx_token_lut": ([c_void_p, c_void_p, c_int64], c_int64),
     "spl_ctx_faults": ([c_void_p, ctypes.POINTER(c_uint64), c_int32], c_int32),
     "spl_ctx_fault_word": ([c_void_p], c_void_p),

@@ -34,7 +34,7 @@ class Engine:
     DEFAULT_REFILL = {2: 64, 3: 32, 4: 16}
 
     def __init__(self, num_tables, num_players=2, device=None, refill_period=None, table0=0, refill_fused=True,
-                 pipeline=True, delegation=None, cards=None, partner_lead=None, host_io=False):
+                 pipeline=True, delegation=None, cards=None, partner_lead=None, host_io=False, step_tail=None):
         torch = _native.require_gpu()
         self.torch = torch
         self.lib = _native.load_library()
@@ -47,6 +47,7 @@ class Engine:
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self._settings = (refill_period, refill_fused, pipeline, delegation, partner_lead)
+        self._step_tail = step_tail
         self.ctx = None
         self._fault_carry = 0  # a fault seen on a context replaced by set_card_table
         self._create_ctx(cards)
@@ -128,6 +129,10 @@ class Engine:
         # -1 = whenever a slot is free); same results
         if partner_lead is not None:
             check(self.lib, self.lib.spl_ctx_set_partner_lead(self.ctx, int(partner_lead)))
+        # step(): three waves per 64 tables (a tail wave takes the legal mask off the rules wave) or two;
+        # None = the library's choice by grid size (spl_ctx_set_step_tail); same results
+        if self._step_tail is not None:
+            check(self.lib, self.lib.spl_ctx_set_step_tail(self.ctx, int(self._step_tail)))
 
     def set_card_table(self, cards=None):
         """Evaluate the tables from now on with card table `cards` (int32 [90, 8]; None = canonical):

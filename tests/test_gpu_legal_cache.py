@@ -193,3 +193,33 @@ def test_a_new_card_table_does_not_reuse_the_old_contexts_masks():
     assert not int(e.flags[0]) & _native.F_ILLEGAL
     _, tag2 = cache_of(e)
     assert (tag2 != tag0).all() and len(set(tag2.tolist())) == 1
+
+
+@pytest.mark.parametrize("P,n", [(2, 4096), (2, 65536), (4, 2048), (3, 1000)])
+def test_step_shapes_are_bit_identical(P, n):
+    """spl_step's two kernel shapes (spl_ctx_set_step_tail: 0 two waves, 1 three with the tail wave that
+    evaluates the new state's legal mask, stores the mask block, draws the fused policy's action and
+    writes the legal-mask cache) give the same outputs bit for bit, step by step, with autoreset,
+    final observations and the device policy; the auto choice depends on the grid size only."""
+    import torch
+    seed = 9
+    two = engine(n, P, refill_period=16, step_tail=0)
+    three = engine(n, P, refill_period=16, step_tail=1)
+    for e in (two, three):
+        e.reset(seeds=range(n))
+    a2 = torch.zeros(n, dtype=torch.int32, device=two.device)
+    two.sample_uniform(out=a2, seed=seed, ply=0)
+    a3 = a2.clone()
+    for k in range(48):
+        n2, n3 = torch.empty_like(a2), torch.empty_like(a3)
+        two.step(a2, next_actions=n2, policy_seed=seed, ply=k + 1)
+        three.step(a3, next_actions=n3, policy_seed=seed, ply=k + 1)
+        for name in ("obs", "mask", "reward", "terminated", "flags", "winner"):
+            assert torch.equal(getattr(two, name), getattr(three, name)), (k, name)
+        term = two.terminated.bool()
+        assert torch.equal(two.final_obs[term], three.final_obs[term]), k
+        assert torch.equal(n2, n3), k
+        a2, a3 = n2, n3
+    assert two.download().tobytes() == three.download().tobytes()
+    assert check_cache(two, "two waves") == check_cache(two, "two waves")
+    check_cache(three, "three waves")
