@@ -4339,7 +4339,10 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (kStepWs) {
         const unsigned blocks = blocks_for(arena->n);
-        const bool tail = ctx->step_tail > 0 || (ctx->step_tail < 0 && (int64_t)blocks <= ctx->step_tail_blocks);
+        // auto: the tail wave up to two workgroups per CU, and for compact-only outputs (obs_u8 without the
+        // int32 rows: a quarter of the row stores, so the rules wave's tail is the longer one)
+        const bool tail = ctx->step_tail > 0 ||
+                          (ctx->step_tail < 0 && ((int64_t)blocks <= ctx->step_tail_blocks || a->obs == nullptr));
         if (tail)
             DISPATCH_P(arena->players, hipLaunchKernelGGL((StepWsKernel<PP, true>::fn), dim3(blocks), dim3(192), 0, s, A,
                                                           ktables(ctx), S))

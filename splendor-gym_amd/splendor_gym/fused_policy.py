@@ -20,6 +20,12 @@ products of order <= 2 accumulated in fp32 on v_mfma_f32_16x16x32_bf16, the obse
 a few ulp (csrc/spl_policy32.hip, k_act32) — so logits and values equal the fp32 module's to within
 fp32 rounding (tests/test_gpu_policy.py).  precision="fp32_f16x2": round 4's faster form, two fp16
 planes per operand (22 significant bits), fp32 within 2^-22 per operand (k_act32h).
+The trade-off: the default buys an EXACT operand representation, not a smaller output
+error.  Against a float64 evaluation of the same module at 65 536 tables the end-to-end logit error is
+4.7e-7 for "fp32", 3.0e-7 for "fp32_f16x2" and 5.4e-7 for torch fp32 itself (both forms' error is the
+fp32 rounding of the sums; tests/test_gpu_policy.py::test_exact_format_error_against_float64 pins all
+three), while "fp32_f16x2" is ~35 % faster (bench.py's config5_selfplay_f16x2 line).  The pool and the
+agent default to "fp32" so that no operand is rounded before the products, as in the reference.
 precision="bf16" (opt-in): bf16 MFMA with fp32 accumulation, logits to bf16 accuracy.  Call
 ``refresh()`` after the module's weights change (e.g. after each PPO update).
 """

@@ -1,10 +1,11 @@
 """Full-size and configuration-5 checks on the GPU:
 
   * the exact headline variant of bench.py (2 players, 65 536 tables, spl_rollout of K = 128 steps,
-    pool refill every 64 steps fused into the launch, two-wave kernel at 64 tables per workgroup,
-    per-step rollout store with non-temporal stores; delegation off, the default) equals chained
-    spl_step launches bit for bit,
-    and a 256-table subset of the chain is replayed through the CPU oracle;
+    pool refill every 64 steps fused into the launch, the quad kernel k_rollout_store_quad_2p — four
+    two-wave teams in one 512-thread workgroup per CU, partner hand-off at lead 4 — per-step rollout
+    store with non-temporal stores), with the hand-off forced too, and the two-wave kernel
+    (k_rollout_store_2p, four workgroups per CU), equal chained spl_step launches bit for bit, and a
+    256-table subset of the chain is replayed through the CPU oracle;
   * 4-player sharding invariance (two shards == one engine);
   * BASELINE config 5: batched self-play with the fused fp32 ActorCritic as agent AND opponent
     (DualStepVectorEnv) equals the same loop driven by the torch fp32 module, table by table —
@@ -44,10 +45,11 @@ def store(K, n, dev):
                                                  (4, 32768, 16, None, True), (4, 32768, 16, -1, True),
                                                  (2, 32768, 64, -1, "dealer2")])
 def test_headline_rollout_65536_equals_step_chain_and_oracle(P, n, R, lead, pipeline):
-    """bench.py's headline (2p x 65 536: two-wave kernel at 64 tables per workgroup, four workgroups per
-    CU, fused refills) and C4's per-GPU share (4p x 32 768 of 262 144 on 8 GPUs: the six-wave dealer,
-    one workgroup per CU) at full size: two 128-step rollout launches equal the spl_step chain bit for
-    bit; every 256th table is replayed through the CPU oracle.  lead -1 forces the partner hand-off
+    """bench.py's headline (2p x 65 536: the auto choice, the quad kernel — four two-wave teams in one
+    workgroup per CU — with fused refills; and the two-wave kernel at four workgroups per CU, "always")
+    and C4's per-GPU share (4p x 32 768 of 262 144 on 8 GPUs: the six-wave dealer, one workgroup per CU)
+    at full size: two 128-step rollout launches equal the spl_step chain bit for bit; every 256th table
+    is replayed through the CPU oracle.  lead -1 forces the partner hand-off
     whenever a task slot is free: the six-wave dealer and the quad kernel (one
     workgroup per CU, 4 teams: the headline's 65 536 tables in 256 workgroups) then hand rows between
     every pair of workgroups with the most slot reuse their rings allow (dealer2 also at 2p x 32 768),
