@@ -348,13 +348,14 @@ def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
     with torch.no_grad():
         agent_k.act(agent_in, mask, seed=77, table0=rank * N, out=act_out)
         torch.cuda.synchronize(dev)
-        region_mark("config5_actor", "start", "k_act32<true, true>", n_act)
+        region_mark(f"config5_actor_{precision}", "start",
+                    "k_act32<true, true>" if precision == "fp32" else "k_act32h<true, true>", n_act)
         for i, (a, b) in enumerate(ev):
             a.record(strm)
             agent_k.act(agent_in, mask, seed=77, ply=i, table0=rank * N, out=act_out)
             b.record(strm)
         torch.cuda.synchronize(dev)
-        region_mark("config5_actor", "end")
+        region_mark(f"config5_actor_{precision}", "end")
     spread = launch_spread([a.elapsed_time(b) / 1e3 for a, b in ev])
     fa, fc = actor_critic_mfma_flop(precision)
     flop = (fa + fc) * N
@@ -372,13 +373,14 @@ def selfplay_line(dev, rank, world, N, iters, warmup, precision="fp32"):
     with torch.no_grad():
         env.pool.act(*opp_args, out=opp_out)
         torch.cuda.synchronize(dev)
-        region_mark("config5_opponent", "start", f"k_act32{'h' if precision != 'fp32' else ''}<false, false>", n_act)
+        region_mark(f"config5_opponent_{precision}", "start", f"k_act32{'h' if precision != 'fp32' else ''}<false, false>",
+                    n_act)
         for a, b in oev:
             a.record(strm)
             env.pool.act(*opp_args, out=opp_out)
             b.record(strm)
         torch.cuda.synchronize(dev)
-        region_mark("config5_opponent", "end")
+        region_mark(f"config5_opponent_{precision}", "end")
     ospread = launch_spread([a.elapsed_time(b) / 1e3 for a, b in oev])
     groups = torch.bincount(env.opp_group.to(torch.int64).flatten())
     full_wg = int((groups // 128).sum().item())
