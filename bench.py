@@ -579,13 +579,18 @@ def self_launch(n, argv, device_count=None):
     (parallel.launch_local_ranks; rank r drives cuda:r, rank 0 prints the JSON line).  This process
     only counts the devices (torch.cuda.device_count() creates no HIP context) and waits; it exits
     with the first failing rank's status.  Fewer than N devices: exit 2 with a message, nothing run.
-    No CPU baseline at N > 1 (it is reported at N = 1 only)."""
+    No CPU baseline at N > 1 (it is reported at N = 1 only).  SPLENDOR_SHARED_DEVICE_REHEARSAL=1 lets N ranks share
+    fewer GPUs (with SPLENDOR_DIST_BACKEND=gloo): the line then says "shared-device rehearsal", not a node figure."""
     if device_count is None:
         import torch
         device_count = torch.cuda.device_count()
-    if device_count < n:
+    from splendor_gym.parallel import REHEARSAL_ENV
+    if device_count < n and os.environ.get(REHEARSAL_ENV) != "1":
         print(f"bench.py --gpus {n}: this node shows {device_count} GPU(s); an {n}-GPU run needs {n} "
               f"(no figure reported)", file=sys.stderr, flush=True)
+        return 2
+    if device_count < 1:
+        print(f"bench.py --gpus {n}: no GPU visible", file=sys.stderr, flush=True)
         return 2
     from splendor_gym.parallel import launch_local_ranks
     return launch_local_ranks(n, [sys.executable, os.path.abspath(__file__), *argv])

@@ -151,6 +151,9 @@ def barrier(device=None):
 
 # env var a self-launched rank carries (launch_local_ranks): the ranks must run on distinct devices
 SELF_LAUNCHED_ENV = "SPLENDOR_SELF_LAUNCHED"
+# opt-in for a rehearsal of N self-launched ranks on fewer GPUs (the line is then labelled a shared-device
+# rehearsal, never a node figure; collectives need SPLENDOR_DIST_BACKEND=gloo, RCCL refuses a shared card)
+REHEARSAL_ENV = "SPLENDOR_SHARED_DEVICE_REHEARSAL"
 
 
 def free_port(addr="127.0.0.1"):
@@ -209,7 +212,7 @@ def require_distinct_devices(census, world):
     """A self-launched run (launch_local_ranks) is an N-GPU figure only if its N ranks drove N distinct
     devices: returns the error text when they did not, else None (an external launcher's shared-device
     rehearsal is labelled instead, bench.node_fields)."""
-    if os.environ.get(SELF_LAUNCHED_ENV) != "1" or census["devices"] >= world:
+    if os.environ.get(SELF_LAUNCHED_ENV) != "1" or census["devices"] >= world or os.environ.get(REHEARSAL_ENV) == "1":
         return None
     return (f"{world} ranks found only {census['devices']} distinct device(s) ({census['identities']}): "
             f"an N-GPU run needs N GPUs; no figure is reported")

@@ -310,6 +310,22 @@ def test_self_launched_ranks_on_one_device_fail(tmp_path):
     assert not list(tmp_path.glob("rank*.json"))
 
 
+def test_self_launched_rehearsal_on_one_device_is_labelled(tmp_path):
+    """SPLENDOR_SHARED_DEVICE_REHEARSAL=1: self-launched ranks on one device run (gloo) and are reported as
+    a shared-device rehearsal (bench.node_fields), not refused."""
+    from splendor_gym.parallel import launch_local_ranks
+    env = dict(os.environ, SPLENDOR_SHARED_DEVICE_REHEARSAL="1")
+    rc = launch_local_ranks(2, [sys.executable, "-c", _LAUNCHED_RANK, REPO, str(tmp_path), "same"], env=env)
+    assert rc == 0
+    sys.path.insert(0, REPO)
+    import bench
+    for r in range(2):
+        rec = json.load(open(tmp_path / f"rank{r}.json"))
+        assert rec["census"]["shared_device"] and rec["census"]["devices"] == 1
+        line = bench.node_fields(rec["census"], "env-steps/sec (whole node), 2p 65536 tables/GPU")
+        assert "shared-device rehearsal" in line["metric"] and line["n_gpus"] == 1 and line["ranks"] == 2
+
+
 def test_launcher_stops_the_other_ranks_when_one_fails():
     """A failing rank ends the launch with its status and the others are terminated (none is left
     waiting in a collective)."""
