@@ -574,6 +574,20 @@ def c4_share_line(dev, rank, world, T, launches, warmup, pipeline=True, partner_
                                    "per-step rollout store [128, T, ...]", "tables_per_gpu": T, "players": P}}
 
 
+STEP_SHAPE_SUFFIX = {0: "ws", 1: "wst", 2: "wso"}
+
+
+def step_shape(mode, tables, cus=None):
+    """spl_step's kernel shape for `tables` tables of full int32 outputs: the forced mode, or the library's
+    auto rule (spl_engine.hip spl_step: three waves up to two 64-table workgroups per CU, else two)."""
+    if mode != "auto":
+        return int(mode)
+    if cus is None:
+        import torch
+        cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    return 1 if -(-int(tables) // 64) <= 2 * int(cus) else 0
+
+
 def self_launch(n, argv, device_count=None):
     """`python bench.py --gpus N` without a launcher: N ranks of this script on this node, one per GPU
     (parallel.launch_local_ranks; rank r drives cuda:r, rank 0 prints the JSON line).  This process
@@ -638,9 +652,10 @@ def main():
                     help="rollout store: every n-th step the odd-XCC workgroups' rows are stored by their "
                          "even-XCC partners (0 = off, the library default: a 1.5 %% gain, "
                          "profiles/r03/deleg_ab_r03a.txt)")
-    ap.add_argument("--step-tail", choices=("auto", "0", "1"), default="auto",
+    ap.add_argument("--step-tail", choices=("auto", "0", "1", "2"), default="auto",
                     help="spl_step kernel shape: auto (the library's choice by grid size), 0 two waves, 1 three waves "
-                         "(a tail wave takes the legal mask off the rules wave); same results")
+                         "(a tail wave takes the legal mask off the rules wave), 2 two waves with the output wave "
+                         "taking it between its row stores; same results")
     ap.add_argument("--partner-lead", type=int, default=None,
                     help="six-wave dealer rollout store: a team this many steps behind its neighbouring-XCC "
                          "partner hands it whole steps of rows (library default 4; 0 = off)")
@@ -749,10 +764,8 @@ def main():
 
     def kernel_name(variant):
         """The kernel the variant launches, as rocprofv3 names it (one name per instantiation)."""
-        if variant == "step":  # spl_step's shape: three waves (wst) up to two workgroups per CU unless forced
-            cus = torch.cuda.get_device_properties(dev).multi_processor_count
-            tail = args.step_tail == "1" or (args.step_tail == "auto" and -(-T // 64) <= 2 * cus)
-            return f"k_step_{'wst' if tail else 'ws'}_{P}p"
+        if variant == "step":  # spl_step's shape (include/splendor_amd.h spl_ctx_set_step_tail), as the library picks it
+            return f"k_step_{STEP_SHAPE_SUFFIX[step_shape(args.step_tail, T)]}_{P}p"
         return eng.rollout_kernel_name(per_step=variant == "rollout_store")
 
     def events(n):

@@ -178,11 +178,11 @@ int spl_ctx_set_rollout_delegation(spl_ctx_t *ctx, int every);
  * is free (tests).  Other kernels ignore it.  Default SPL_PARTNER_LEAD (4; DESIGN.md §2 gives the
  * measured A/B).  Results are identical either way. */
 int spl_ctx_set_partner_lead(spl_ctx_t *ctx, int lead);
-/* spl_step's kernel shape (round 6): 1 = three waves per 64 tables (k_step_wst_<P>p: a TAIL wave takes
- * the new state's legal mask, the mask block, the fused policy's action and the legal-mask cache off the
- * rules wave), 0 = two waves (k_step_ws_<P>p), -1 = auto (default): three waves up to two workgroups per
- * CU, two above (measured: 17.4 -> 14.7 us per step at 16 384 tables, 22.4 -> 22.9 us at 65 536).
- * Results are identical either way. */
+/* spl_step's kernel shape (round 6): 0 = two waves (k_step_ws_<P>p: the rules wave evaluates the new
+ * state's legal mask after the row halves), 1 = three waves per 64 tables (k_step_wst_<P>p: a TAIL wave
+ * takes the new state's legal mask, the mask block, the fused policy's action and the legal-mask cache off
+ * the rules wave), 2 = two waves with the OUTPUT wave evaluating the mask between the halves of its row
+ * stores (k_step_wso_<P>p); -1 = auto (default, by grid size: DESIGN.md §4.3).  Results are identical. */
 int spl_ctx_set_step_tail(spl_ctx_t *ctx, int mode);
 /* The name of the kernel spl_rollout launches for n tables of `players` players under the context's
  * settings (e.g. "k_rollout_store_2p", "k_rollout_inplace_half_4p"): every instantiation has a name

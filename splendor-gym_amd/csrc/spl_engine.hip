@@ -1096,6 +1096,46 @@ __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int row
     for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) dst[b] = (int32_t)rows_lds[b];
 }
 
+// store_obs_block (64 rows) with `mid()` issued between its first and second half: work that fills the
+// wave's store-issue stalls instead of following the whole block (k_step_wso's legal mask)
+template <bool NT, class Mid>
+__device__ __forceinline__ void store_obs_block_mid(const uint8_t *rows_lds, int rows, int32_t *dst, Mid mid) {
+    if (rows != 64) {
+        mid();
+        store_obs_block<64, NT>(rows_lds, rows, dst);
+        return;
+    }
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
+    v4i *out = reinterpret_cast<v4i *>(dst);
+    constexpr int U = 5, kFull = 64 * kObsDim / 4, kIters = kFull / (64 * U);  // 4752 = 14 x 320 + 272
+    int d = lane_id();
+#pragma unroll 1
+    for (int it = 0; it < kIters / 2; ++it, d += 64 * U) {
+        uint32_t w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
+    }
+    __asm__ volatile("" ::: "memory");
+    mid();
+    __asm__ volatile("" ::: "memory");
+#pragma unroll 1
+    for (int it = kIters / 2; it < kIters; ++it, d += 64 * U) {
+        uint32_t w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
+#pragma unroll
+        for (int u = 0; u < U; ++u) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
+    }
+    uint32_t w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) w[u] = (d + 64 * u < kFull) ? src[d + 64 * u] : 0u;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (d + 64 * u < kFull) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
+}
+
 // Block store of `rows` compact rows (300 bytes each) staged in LDS to dst (16-byte aligned).
 __device__ __forceinline__ void store_obs_u8_block(const uint8_t *rows_lds, int rows, uint8_t *dst) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
@@ -2275,8 +2315,11 @@ __device__ __forceinline__ bool step_wait(const uint32_t *p) {
     }
 }
 
-template <int P, bool kStepTail>
+// kShape: 0 two waves (the rules wave takes the new state's mask), 1 three waves (the TAIL wave takes
+// it), 2 two waves with the OUTPUT wave taking it in the middle of its row-block stores (k_step_wso)
+template <int P, int kShape>
 __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, KStep S) {
+    constexpr bool kStepTail = kShape == 1, kOMask = kShape == 2, kRulesMask = kShape == 0;
     constexpr int kW = StepWsLDS<P>::kW;
     const int lane = lane_id();
     const int role = (int)(threadIdx.x >> 6);  // 0 rules, 1 output, 2 tail (kStepTail)
@@ -2334,7 +2377,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
             autoreset_table(T, A, t, pool, &L.rows[lane * kScratchStride], mtx, o, pool_dirty);
 #pragma unroll
         for (int w = 0; w < kW; ++w) L.st[w][lane] = tab_word(T, w);
-        if (kStepTail) L.omask[lane] = o.mask;  // the tail wave evaluates the deferred lanes' masks
+        if (!kRulesMask) L.omask[lane] = o.mask;  // the tail / output wave evaluates the deferred lanes' masks
         STAMP(3);
         ws_sync();  // hand-off 1: state words (deal scratch in `rows` free again)
         // this wave encodes the first half of every row while the output wave encodes the second
@@ -2356,7 +2399,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         }
         STAMP(7);
         STAMPV(9, __popcll(fin_all) | (__popcll(__ballot((o.mask & kMaskDeferred) != 0)) << 8));
-        if (!kStepTail) {
+        if (kRulesMask) {
             if (o.mask & kMaskDeferred) o.mask = abl(ABL_LEGAL_POST) ? (uint64_t)action : legal_of(T, L);
             STAMP(5);
             // masks and small outputs leave from this wave while the output wave streams the rows
@@ -2375,8 +2418,8 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
                 if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_add);
                 if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
             }
-            if (kStepTail) {
-                store_words(T, A, t);  // the legal-mask cache entry is the tail wave's
+            if (!kRulesMask) {
+                store_words(T, A, t);  // the legal-mask cache entry is the tail / output wave's
             } else {
                 if (S.next_actions) {
                     const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
@@ -2405,16 +2448,39 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         }
         STAMP(4);
         STAMP(5);
+        uint64_t m = 0ull;  // kOMask: the new state's legal mask, evaluated between the row stores
+        auto mask_now = [&]() {
+            m = L.omask[lane];
+            if (m & kMaskDeferred) m = abl(ABL_LEGAL_POST) ? 0ull : legal_of(T, L);
+        };
         if (compact) {
             store_obs_u8_block(L.rows, rows, S.obs_u8 + (size_t)t0 * kObsU8);
-            STAMP(6);
-            return;
+            if (kOMask) mask_now();
+        } else {
+            if (abl(ABL_OBS_STORE)) {
+                if (kOMask) mask_now();
+            } else if (kOMask) {
+                store_obs_block_mid<SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim, mask_now);
+            } else {
+                store_obs_block<64, SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
+            }
+            if (S.obs_u8)  // both outputs: the compact copy of the same rows (a fused actor's input)
+                store_u8_from_rows(L.rows, rows, S.obs_u8 + (size_t)t0 * kObsU8, valid ? (uint32_t)get_moves(T.sw) >> 8 : 0u);
         }
-        if (!abl(ABL_OBS_STORE)) store_obs_block<64, SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
-        if (S.obs_u8)  // both outputs: the compact copy of the same rows (a fused actor's input)
-            store_u8_from_rows(L.rows, rows, S.obs_u8 + (size_t)t0 * kObsU8, valid ? (uint32_t)get_moves(T.sw) >> 8 : 0u);
         STAMP(6);
-        if (__any(valid && get_moves(T.sw) > 255)) {  // patch after this wave's block stores of the same dwords
+        if (kOMask) {  // the mask block, the fused policy's action and the legal-mask cache entry
+            L.mask[lane] = m;
+            wave_lds_sync();
+            if (!abl(ABL_MASK_STORE)) store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+            if (valid) {
+                if (S.next_actions) {
+                    const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
+                    S.next_actions[t] = policy_action(S.policy, m, T, L, S.policy_seed, (uint64_t)(S.table0 + t), ply);
+                }
+                store_legal(A, t, m, Tb.mtag);  // m: legal_moves of the state the rules wave stores
+            }
+        }
+        if (!compact && __any(valid && get_moves(T.sw) > 255)) {  // patch after this wave's block stores of the same dwords
             __builtin_amdgcn_s_waitcnt(0);
             if (valid && get_moves(T.sw) > 255) S.obs[(size_t)t * kObsDim + 295] = get_moves(T.sw);
         }
@@ -2443,23 +2509,26 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
 }
 
 // one kernel name per player count and shape (see RolloutKernel)
-template <int P, bool kTail>
+template <int P, int kShape>
 struct StepWsKernel;
-#define SPL_STEP_WS_KERNEL(NAME, P_, TAIL_)                                                  \
-    __global__ __launch_bounds__(TAIL_ ? 192 : 128) void NAME(KArena A, KTables Tb, KStep S) { \
-        __shared__ StepWsLDS<P_> L;                                                           \
-        step_ws<P_, TAIL_>(L, A, Tb, S);                                                      \
-    }                                                                                         \
-    template <>                                                                               \
-    struct StepWsKernel<P_, TAIL_> {                                                          \
-        static constexpr void (*fn)(KArena, KTables, KStep) = NAME;                           \
+#define SPL_STEP_WS_KERNEL(NAME, P_, SHAPE_)                                                    \
+    __global__ __launch_bounds__(SHAPE_ == 1 ? 192 : 128) void NAME(KArena A, KTables Tb, KStep S) { \
+        __shared__ StepWsLDS<P_> L;                                                              \
+        step_ws<P_, SHAPE_>(L, A, Tb, S);                                                        \
+    }                                                                                            \
+    template <>                                                                                  \
+    struct StepWsKernel<P_, SHAPE_> {                                                            \
+        static constexpr void (*fn)(KArena, KTables, KStep) = NAME;                              \
     };
-SPL_STEP_WS_KERNEL(k_step_ws_2p, 2, false)
-SPL_STEP_WS_KERNEL(k_step_ws_3p, 3, false)
-SPL_STEP_WS_KERNEL(k_step_ws_4p, 4, false)
-SPL_STEP_WS_KERNEL(k_step_wst_2p, 2, true)
-SPL_STEP_WS_KERNEL(k_step_wst_3p, 3, true)
-SPL_STEP_WS_KERNEL(k_step_wst_4p, 4, true)
+SPL_STEP_WS_KERNEL(k_step_ws_2p, 2, 0)
+SPL_STEP_WS_KERNEL(k_step_ws_3p, 3, 0)
+SPL_STEP_WS_KERNEL(k_step_ws_4p, 4, 0)
+SPL_STEP_WS_KERNEL(k_step_wst_2p, 2, 1)
+SPL_STEP_WS_KERNEL(k_step_wst_3p, 3, 1)
+SPL_STEP_WS_KERNEL(k_step_wst_4p, 4, 1)
+SPL_STEP_WS_KERNEL(k_step_wso_2p, 2, 2)
+SPL_STEP_WS_KERNEL(k_step_wso_3p, 3, 2)
+SPL_STEP_WS_KERNEL(k_step_wso_4p, 4, 2)
 #undef SPL_STEP_WS_KERNEL
 
 // Rollout-store delegation (rollout_ws<P, 64, true>, spl_ctx_set_rollout_delegation).  The
@@ -4182,7 +4251,7 @@ int spl_ctx_set_rollout_pipeline(spl_ctx_t *ctx, int on) {
 }
 
 int spl_ctx_set_step_tail(spl_ctx_t *ctx, int mode) {
-    if (!ctx || mode < -1 || mode > 1) return fail(SPL_E_ARG, "step tail mode must be -1 (auto), 0 or 1");
+    if (!ctx || mode < -1 || mode > 2) return fail(SPL_E_ARG, "step shape must be -1 (auto), 0, 1 or 2");
     ctx->step_tail = mode;
     return SPL_OK;
 }
@@ -4341,13 +4410,16 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
         const unsigned blocks = blocks_for(arena->n);
         // auto: the tail wave up to two workgroups per CU, and for compact-only outputs (obs_u8 without the
         // int32 rows: a quarter of the row stores, so the rules wave's tail is the longer one)
-        const bool tail = ctx->step_tail > 0 ||
-                          (ctx->step_tail < 0 && ((int64_t)blocks <= ctx->step_tail_blocks || a->obs == nullptr));
-        if (tail)
-            DISPATCH_P(arena->players, hipLaunchKernelGGL((StepWsKernel<PP, true>::fn), dim3(blocks), dim3(192), 0, s, A,
+        const int shape = ctx->step_tail >= 0 ? ctx->step_tail
+                                              : (((int64_t)blocks <= ctx->step_tail_blocks || a->obs == nullptr) ? 1 : 0);
+        if (shape == 1)
+            DISPATCH_P(arena->players, hipLaunchKernelGGL((StepWsKernel<PP, 1>::fn), dim3(blocks), dim3(192), 0, s, A,
+                                                          ktables(ctx), S))
+        else if (shape == 2)
+            DISPATCH_P(arena->players, hipLaunchKernelGGL((StepWsKernel<PP, 2>::fn), dim3(blocks), dim3(128), 0, s, A,
                                                           ktables(ctx), S))
         else
-            DISPATCH_P(arena->players, hipLaunchKernelGGL((StepWsKernel<PP, false>::fn), dim3(blocks), dim3(128), 0, s, A,
+            DISPATCH_P(arena->players, hipLaunchKernelGGL((StepWsKernel<PP, 0>::fn), dim3(blocks), dim3(128), 0, s, A,
                                                           ktables(ctx), S))
     } else {
         DISPATCH_P(arena->players,

@@ -58,3 +58,11 @@ def test_algorithmic_bytes_constants():
     # SURVEY.md §8d (1370 / 1446) + the 16 B of the legal-mask cache (round 6)
     assert bench.STEP_ALGO_BYTES[2] == 1370 + 16 and bench.STEP_ALGO_BYTES[4] == 1446 + 16
     assert bench.OUT_BYTES == 1240
+
+
+def test_step_shape_names_follow_the_library_rule():
+    """bench.py names spl_step's kernel as the library picks it (spl_engine.hip spl_step: three waves up to
+    two 64-table workgroups per CU, two above; a forced --step-tail wins)."""
+    assert bench.step_shape("auto", 65536, cus=256) == 0 and bench.step_shape("auto", 32768, cus=256) == 1
+    assert bench.step_shape("auto", 16384, cus=256) == 1 and bench.step_shape("2", 65536, cus=256) == 2
+    assert [bench.STEP_SHAPE_SUFFIX[i] for i in range(3)] == ["ws", "wst", "wso"]

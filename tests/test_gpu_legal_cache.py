@@ -195,16 +195,17 @@ def test_a_new_card_table_does_not_reuse_the_old_contexts_masks():
     assert (tag2 != tag0).all() and len(set(tag2.tolist())) == 1
 
 
-@pytest.mark.parametrize("P,n", [(2, 4096), (2, 65536), (4, 2048), (3, 1000)])
-def test_step_shapes_are_bit_identical(P, n):
-    """spl_step's two kernel shapes (spl_ctx_set_step_tail: 0 two waves, 1 three with the tail wave that
-    evaluates the new state's legal mask, stores the mask block, draws the fused policy's action and
-    writes the legal-mask cache) give the same outputs bit for bit, step by step, with autoreset,
-    final observations and the device policy; the auto choice depends on the grid size only."""
+@pytest.mark.parametrize("P,n,other", [(2, 4096, 1), (2, 65536, 1), (4, 2048, 1), (3, 1000, 1),
+                                       (2, 4096, 2), (2, 65536, 2), (4, 2048, 2), (3, 1000, 2)])
+def test_step_shapes_are_bit_identical(P, n, other):
+    """spl_step's kernel shapes (spl_ctx_set_step_tail: 0 two waves; 1 three, the tail wave evaluating the
+    new state's legal mask, storing the mask block, drawing the fused policy's action and writing the
+    legal-mask cache; 2 two waves with the output wave doing that between its row stores) give the same
+    outputs bit for bit, step by step, with autoreset, final observations and the device policy."""
     import torch
     seed = 9
     two = engine(n, P, refill_period=16, step_tail=0)
-    three = engine(n, P, refill_period=16, step_tail=1)
+    three = engine(n, P, refill_period=16, step_tail=other)
     for e in (two, three):
         e.reset(seeds=range(n))
     a2 = torch.zeros(n, dtype=torch.int32, device=two.device)
