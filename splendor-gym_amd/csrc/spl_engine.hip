@@ -219,6 +219,11 @@ __device__ __forceinline__ int wg_block() { return wg_block_of(blockIdx.x); }
 #ifndef SPL_WS_PRIO
 #define SPL_WS_PRIO 1
 #endif
+// per-step rollout-store rows and masks non-temporal (1, round 2's choice) or plain (0): A/B switch
+#ifndef SPL_ROLL_NT
+#define SPL_ROLL_NT 1
+#endif
+constexpr bool kRollNT = SPL_ROLL_NT != 0;
 
 constexpr int kMaskStreamWords = 64 * 45 / 32;  // 90
 
@@ -2735,7 +2740,7 @@ __device__ __forceinline__ void pt_store_task(const uint8_t *slot, uint8_t *rows
     unstage_state(slot, T);
     encode_row(T, rows_lds, C);
     wave_lds_sync();
-    store_obs_block<64, true>(rows_lds, 64, dst);
+    store_obs_block<64, kRollNT>(rows_lds, 64, dst);
     wave_lds_sync();  // the block's LDS reads are done before the next task's rows land
 }
 // consumer (the partner team's output wave): `v` = the flag of the partner's slot cseq; if it is READY,
@@ -3308,7 +3313,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
             } else if (deleg_now) {
                 const int j = k / dl.every;
                 if (big_moves) {  // a patched row: stored here, the partner skips the task
-                    store_obs_block<TPW, true>(L.rows, rows, obs + (size_t)t0 * kObsDim);
+                    store_obs_block<TPW, kRollNT>(L.rows, rows, obs + (size_t)t0 * kObsDim);
                     flag_store(ready_flag(j), dl.epoch << 1 | 1u);
                 } else {
                     stage_state(T, slot_of(j));
@@ -3318,14 +3323,14 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 }
             } else if (abl(ABL_OBS_STORE)) {
             } else if (per_step) {
-                store_obs_block<TPW, true>(L.rows, rows, obs + (size_t)t0 * kObsDim);
+                store_obs_block<TPW, kRollNT>(L.rows, rows, obs + (size_t)t0 * kObsDim);
             } else {
                 store_obs_block<TPW, false>(L.rows, rows, obs + (size_t)t0 * kObsDim);
             }
             WSSTAMP(2, k);
             if (abl(ABL_MASK_STORE)) {
             } else if (per_step) {
-                store_mask_block<true>(L.mask[b], L.mbits, rows, S.mask + blk * 45 + (size_t)t0 * 45);
+                store_mask_block<kRollNT>(L.mask[b], L.mbits, rows, S.mask + blk * 45 + (size_t)t0 * 45);
             } else {
                 store_mask_block<false>(L.mask[b], L.mbits, rows, S.mask + blk * 45 + (size_t)t0 * 45);
             }
@@ -3392,7 +3397,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 unstage_state(slot_of(j), T);
                 encode_row(T, L.rows, L);
                 wave_lds_sync();
-                store_obs_block<TPW, true>(L.rows, 64, S.obs + ((size_t)k * (size_t)A.n + pt0) * kObsDim);
+                store_obs_block<TPW, kRollNT>(L.rows, 64, S.obs + ((size_t)k * (size_t)A.n + pt0) * kObsDim);
                 wave_lds_sync();  // the block's LDS reads are done before the next task's rows land
             }
         }
@@ -3406,7 +3411,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 unstage_state(slot_of(j), T);
                 encode_row(T, L.rows, L);
                 wave_lds_sync();
-                store_obs_block<TPW, true>(L.rows, 64, S.obs + ((size_t)k * (size_t)A.n + t0) * kObsDim);
+                store_obs_block<TPW, kRollNT>(L.rows, 64, S.obs + ((size_t)k * (size_t)A.n + t0) * kObsDim);
                 wave_lds_sync();
             }
         }
