@@ -69,7 +69,8 @@
 // timing ablations (wrong results by design): 1 tanh = identity, 2 one weight chunk (no ring
 // streaming: no LDS-DMA piece after the prologue, no per-tile barrier), 4 A fragments loaded once
 // per tile (no per-group LDS reads), 16 the ring without its barriers (waves race the slots), 32 no
-// per-table epilogue (no softmax / sample / argmax), 64 no observation loads (zero layer-1 operand);
+// per-table epilogue (no softmax / sample / argmax), 64 no observation loads (zero layer-1 operand),
+// 512 no MFMA at all (an empty asm keeps each product's operands live; 8 replaces it by a VALU op);
 // the tail kernel k_act32_narrow: 128 its launch and index lookups only, 256 no layers (zero logits)
 #ifndef SPL_POL_ABL
 #define SPL_POL_ABL 0
@@ -363,6 +364,10 @@ template <class F>
 __device__ __forceinline__ f32x4 mma(const typename F::pelx8 &a, const typename F::pelx8 &b, const f32x4 &c) {
 #if SPL_POL_ABL & 8
     return c + (float)a[0] * (float)b[1];
+#elif SPL_POL_ABL & 512  // no MFMA and no stand-in instruction: the operands stay live, the sum is the bias
+    f32x4 d = c;
+    asm volatile("" : "+v"(d) : "v"(a), "v"(b));
+    return d;
 #else
     if constexpr (F::kExact) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
     else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
