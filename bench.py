@@ -600,7 +600,7 @@ def self_launch(n, argv, device_count=None):
         device_count = torch.cuda.device_count()
     from splendor_gym.parallel import REHEARSAL_ENV
     if device_count < n and os.environ.get(REHEARSAL_ENV) != "1":
-        print(f"bench.py --gpus {n}: this node shows {device_count} GPU(s); an {n}-GPU run needs {n} "
+        print(f"bench.py --gpus {n}: this node shows {device_count} GPU(s); a run on {n} GPUs needs {n} "
               f"(no figure reported)", file=sys.stderr, flush=True)
         return 2
     if device_count < 1:

@@ -287,19 +287,21 @@ with open(os.path.join(sys.argv[2], f"rank{rank}.json"), "w") as f:
 '''
 
 
-def test_self_launched_ranks_over_gloo(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_self_launched_ranks_over_gloo(tmp_path, world):
     """bench.py --gpus N without a launcher starts N ranks itself
-    (parallel.launch_local_ranks).  Two ranks over gloo on CPU: each gets its rank / local rank /
-    world and the rendezvous, the census sees two devices, gather_returns and max_over_ranks agree."""
+    (parallel.launch_local_ranks).  Two and four ranks over gloo on CPU (1 001 tables: shards of
+    unequal size at four): each gets its rank / local rank / world and the rendezvous, the census sees
+    one device per rank, gather_returns and max_over_ranks agree."""
     from splendor_gym.parallel import launch_local_ranks
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    rc = launch_local_ranks(2, [sys.executable, "-c", _LAUNCHED_RANK, REPO, str(tmp_path), "distinct"], env=env)
+    rc = launch_local_ranks(world, [sys.executable, "-c", _LAUNCHED_RANK, REPO, str(tmp_path), "distinct"], env=env)
     assert rc == 0
-    recs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(2)]
+    recs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
     for r, rec in enumerate(recs):
-        assert rec["rank"] == r and rec["local"] == r and rec["world"] == 2 and rec["env"] == "1"
-        assert rec["census"]["devices"] == 2 and not rec["census"]["shared_device"]
-        assert rec["ret_ok"] and rec["cnt_ok"] and rec["max"] == 1.25
+        assert rec["rank"] == r and rec["local"] == r and rec["world"] == world and rec["env"] == "1"
+        assert rec["census"]["devices"] == world and not rec["census"]["shared_device"]
+        assert rec["ret_ok"] and rec["cnt_ok"] and rec["max"] == world - 1 + 0.25
 
 
 def test_self_launched_ranks_on_one_device_fail(tmp_path):
@@ -343,7 +345,7 @@ def test_bench_gpus_n_refuses_fewer_devices(capsys):
     sys.path.insert(0, REPO)
     import bench
     assert bench.self_launch(2, ["--gpus", "2"], device_count=1) == 2
-    assert "shows 1 GPU(s); an 2-GPU run needs 2" in capsys.readouterr().err
+    assert "shows 1 GPU(s); a run on 2 GPUs needs 2" in capsys.readouterr().err
     assert bench.self_launch(8, ["--gpus", "8"], device_count=0) == 2
 
 
