@@ -28,12 +28,12 @@ import torch
 from splendor_gym import _native
 from splendor_gym.device import Engine
 T = int(os.environ.get("STAMP_T", "65536"))
-e = Engine(T, 2, device="cuda:0", refill_period=0)
+e = Engine(T, 2, device="cuda:0", refill_period=0, step_tail=0)  # the two-wave shape this parser reads
 e.lib.spl_debug_set_stamps.argtypes = [ctypes.c_void_p]
 e.reset(seeds=range(T))
 buf = [torch.zeros(T, dtype=torch.int32, device=e.device) for _ in range(2)]
 e.sample_uniform(out=buf[0], seed=1, ply=0)
-st = torch.zeros((T // 64) * 2 * 16, dtype=torch.int64, device=e.device)
+st = torch.zeros((T // 64) * 3 * 16, dtype=torch.int64, device=e.device)  # room for three waves per workgroup
 _native.check(e.lib, e.lib.spl_debug_set_stamps(st.data_ptr()))
 out = []
 for k in range(96):
@@ -41,7 +41,7 @@ for k in range(96):
     if (k + 1) % 16 == 0: e.refill()
     if k >= 80:
         torch.cuda.synchronize()
-        out.append(st.view(-1, 16).cpu().tolist())
+        out.append(st.view(-1, 16)[: (T // 64) * 2].cpu().tolist())
         st.zero_()
 print(json.dumps(out))
 '''
