@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1443,7 +1444,9 @@ __device__ __forceinline__ void store_tab(const Tab<P> &T, const KArena &A, int 
 // the cached legal mask of table t's stored state, if it was computed under context tag `tag`
 struct LegalCache {
     uint32_t lo, hi;
-    __device__ __forceinline__ bool known(uint32_t tag) const { return (hi >> kLegalTagShift) == tag; }
+    // tag 0 is "unknown" on both sides: an entry a crafted upload left, and a context without a tag of its
+    // own (card_table_tag ran out) never trusts an entry
+    __device__ __forceinline__ bool known(uint32_t tag) const { return tag != 0u && (hi >> kLegalTagShift) == tag; }
     __device__ __forceinline__ uint64_t mask() const { return (uint64_t)lo | ((uint64_t)(hi & kLegalHiBits) << 32); }
 };
 __device__ __forceinline__ LegalCache load_legal(const KArena &A, int t) {
@@ -3969,7 +3972,7 @@ struct spl_ctx_s {
     int quad_resident[5];    // k_rollout_store_quad_<P>p: the same for the quad variant
     int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
     int partner_lead;    // six-wave dealer per-step store: partner hand-off lead in steps (0 off, < 0 forced)
-    uint32_t mtag;         // legal-mask cache tag of this context (its card table), 1..65535
+    uint32_t mtag;         // legal-mask cache tag of this context's card table (card_table_tag), 1..65535, or 0
     int step_tail;         // spl_step shape: -1 auto (the tail wave up to step_tail_blocks workgroups), 0 two waves, 1 three
     int64_t step_tail_blocks;
     uint64_t *fault_host;  // host-mapped, fine-grained: the serial of a launch that faulted (0 = none), spl_ctx_faults
@@ -4098,6 +4101,25 @@ int64_t spl_arena_bytes(int32_t n, int32_t players) {
     return arena_layout(n, players).total;
 }
 
+// The legal-mask cache tag of a card table (the 90 card and 10 noble records the kernels read; legal_moves
+// depends on the state and the card costs only): one tag per DISTINCT table in this process, never
+// recycled, so an arena stepped under two contexts reuses masks exactly when their tables are equal (an
+// edited table gets a tag of its own; contexts of the canonical table share one).  Past 65 535 distinct
+// tables a context gets tag 0: it neither trusts a cached mask nor publishes one (LegalCache::known).
+static uint32_t card_table_tag(const std::vector<uint4> &crec, const std::vector<uint2> &nrec) {
+    static std::mutex mu;
+    static std::map<std::string, uint32_t> tags;
+    std::string key(reinterpret_cast<const char *>(crec.data()), crec.size() * sizeof(uint4));
+    key.append(reinterpret_cast<const char *>(nrec.data()), nrec.size() * sizeof(uint2));
+    std::lock_guard<std::mutex> g(mu);
+    const auto it = tags.find(key);
+    if (it != tags.end()) return it->second;
+    if (tags.size() >= kLegalTagMax) return 0u;
+    const uint32_t tag = (uint32_t)tags.size() + 1u;
+    tags.emplace(std::move(key), tag);
+    return tag;
+}
+
 int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_ctx_t **out) {
     if (!cards || !nobles || !out) return fail(SPL_E_ARG, "null argument");
     *out = nullptr;
@@ -4159,10 +4181,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     }
     spl_ctx_t *c = new spl_ctx_t();
     c->device = device;
-    {  // a tag per context: an arena stepped under another card table never reuses this one's masks
-        static std::atomic<uint32_t> serial{0u};
-        c->mtag = serial.fetch_add(1u) % 0xFFFFu + 1u;
-    }
+    c->mtag = card_table_tag(crec, nrec);
     c->refill_period = 64;
     c->refill_fused = 1;
     c->deleg_every = SPL_DELEG_EVERY;

@@ -93,12 +93,14 @@ __host__ __device__ constexpr int pt_done_line(int side) { return DF_TASKS + 2 *
 __host__ __device__ constexpr int pt_epoch_line(int side) { return DF_PROD_EPOCH + side; }
 
 // Legal-mask cache (ABI 9): [2][n] u32, legal_moves of the table's STORED state as written by the
-// kernel that stored it — word 0 mask bits 0..31, word 1 bits 32..44 | context tag << 16.  A reader
-// trusts it only when the tag equals its context's (a context is one card table: an edited table's
-// context gets a tag of its own), and every kernel that stores table state writes the mask it computed
-// or tag 0 (unknown).  spl_step reads it so its pre-step check needs no legal_moves evaluation.
+// kernel that stored it — word 0 mask bits 0..31, word 1 bits 32..44 | card-table tag << 16.  A reader
+// trusts it only when the tag equals its context's nonzero tag (one tag per distinct card table in the
+// process: contexts of equal tables share it, an edited table gets its own), and every kernel that
+// stores table state writes the mask it computed or tag 0 (unknown).  spl_step reads it so its pre-step
+// check needs no legal_moves evaluation.
 constexpr uint32_t kLegalHiBits = 0x1FFFu;
 constexpr int kLegalTagShift = 16;
+constexpr uint32_t kLegalTagMax = 0xFFFFu;  // tags 1..65535 (16 bits above the mask's 13)
 
 struct ArenaLayout {
     int64_t planes, pool, slots, pcg, deleg, dflags, legal, total;

@@ -168,7 +168,7 @@ def test_crafted_upload_then_step_is_judged_on_the_new_state():
 
 
 def test_a_new_card_table_does_not_reuse_the_old_contexts_masks():
-    """The cache is tagged per context: after set_card_table the old entries are not this context's,
+    """The cache is tagged per card table: after set_card_table the old entries are not this context's,
     so the next step evaluates legal_moves under the edited table (a card made free is buyable)."""
     import torch
     from splendor_gym import _native
@@ -193,6 +193,30 @@ def test_a_new_card_table_does_not_reuse_the_old_contexts_masks():
     assert not int(e.flags[0]) & _native.F_ILLEGAL
     _, tag2 = cache_of(e)
     assert (tag2 != tag0).all() and len(set(tag2.tolist())) == 1
+
+
+def test_equal_card_tables_share_the_tag_and_an_edit_back_trusts_it_again():
+    """The tag belongs to the card table's contents (card_table_tag in spl_engine.hip): a second engine on the
+    canonical table carries the same tag, an edited table another, and switching back to the canonical
+    table (a new context) trusts the entries the first context wrote — and they are still exact."""
+    from splendor_gym.engine.state import load_tables
+    n = 256
+    e = engine(n, 2, refill_period=0)
+    e.reset(seeds=range(n))
+    tag0 = check_cache(e, "reset")
+    f = engine(64, 2, refill_period=0)
+    f.reset(seeds=range(64))
+    assert check_cache(f, "second engine, canonical table") == tag0
+    cards, _ = load_tables()
+    cards = np.array(cards, np.int32).copy()
+    cards[0, 3] += 1  # one cost edited: a different table
+    e.set_card_table(cards)
+    e.step(e.sample_uniform(seed=3, ply=1), autoreset=False)
+    tag_edit = check_cache(e, "step under the edited table")
+    assert tag_edit not in (0, tag0)
+    e.set_card_table(None)  # back to the canonical table: a new context with the canonical tag
+    e.step(e.sample_uniform(seed=3, ply=2), autoreset=False)
+    assert check_cache(e, "step back under the canonical table") == tag0
 
 
 @pytest.mark.parametrize("P,n,other", [(2, 4096, 1), (2, 65536, 1), (4, 2048, 1), (3, 1000, 1),
