@@ -173,10 +173,13 @@ def launch_local_ranks(n, cmd, env=None, port=None, poll_s=0.2, stream=None):
     SPLENDOR_SELF_LAUNCHED=1, inherits stdout / stderr, and picks its own device
     (`local_device(LOCAL_RANK)`): this process never touches a GPU, so the children are started from
     a process without a HIP context.  Waits for all of them; when one exits non-zero the others are
-    terminated (their exact PIDs) so none is left waiting in a collective.  Returns 0 when every rank
-    exited 0, else the first non-zero exit status seen (a signal -s maps to 128 + s)."""
+    terminated (their exact PIDs) so none is left waiting in a collective, and so are all of them when
+    this process is interrupted or sent SIGTERM.  Returns 0 when every rank exited 0, else the first
+    non-zero exit status seen (a signal -s maps to 128 + s)."""
+    import signal
     import subprocess
     import sys
+    import threading
     import time
     if n < 1:
         raise ValueError("n must be >= 1")
@@ -184,27 +187,44 @@ def launch_local_ranks(n, cmd, env=None, port=None, poll_s=0.2, stream=None):
     base = dict(os.environ if env is None else env)
     base.update(WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     base[SELF_LAUNCHED_ENV] = "1"
+    # a SIGTERM to this process (a driver's time limit) ends the children too instead of orphaning them
+    main = threading.current_thread() is threading.main_thread()
+
+    def _term(signum, frame):
+        raise SystemExit(128 + signum)
+    prev = signal.signal(signal.SIGTERM, _term) if main else None
     procs = []
-    for r in range(n):
-        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen(list(cmd), env=e))
     status = 0
-    live = list(procs)
-    while live:
-        time.sleep(poll_s)
-        for p in list(live):
-            rc = p.poll()
-            if rc is None:
-                continue
-            live.remove(p)
-            if rc != 0 and status == 0:
-                status = rc if rc > 0 else 128 - rc
-                print(f"rank {procs.index(p)} exited with status {rc}; stopping the other ranks",
-                      file=stream or sys.stderr, flush=True)
-                for q in live:
-                    q.terminate()
-    for p in procs:
-        p.wait()
+    try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen(list(cmd), env=e))
+        live = list(procs)
+        while live:
+            time.sleep(poll_s)
+            for p in list(live):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                live.remove(p)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 128 - rc
+                    print(f"rank {procs.index(p)} exited with status {rc}; stopping the other ranks",
+                          file=stream or sys.stderr, flush=True)
+                    for q in live:
+                        q.terminate()
+    finally:
+        for p in procs:  # normally all have exited; after an exception or a signal, stop the rest (exact PIDs)
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        if main:
+            signal.signal(signal.SIGTERM, prev)
     return status
 
 

@@ -426,3 +426,31 @@ def test_edited_cards_make_a_card_table():
     assert dict(cards_by_id()[card.id].cost) != card.cost
     fresh = SplendorState.from_record(rec)
     assert fresh.board[1][0] is not card and fresh.card_table() is None
+
+
+def test_launcher_stops_its_ranks_on_sigterm(tmp_path):
+    """SIGTERM to the launching process (a driver's time limit) ends its ranks too: none is orphaned."""
+    import signal
+    import subprocess
+    import time
+    pids = tmp_path / "pids"
+    pids.mkdir()
+    rank = ("import os, sys, time\nopen(os.path.join(sys.argv[1], os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+            "time.sleep(120)\n")
+    parent = ("import sys\nsys.path[:0] = [sys.argv[1]]\nfrom splendor_gym.parallel import launch_local_ranks\n"
+              "sys.exit(launch_local_ranks(2, [sys.executable, '-c', sys.argv[2], sys.argv[3]]))\n")
+    p = subprocess.Popen([sys.executable, "-c", parent, os.path.join(REPO, "splendor-gym_amd"), rank, str(pids)])
+    t = time.perf_counter()
+    while len(list(pids.iterdir())) < 2 and time.perf_counter() - t < 60:
+        time.sleep(0.1)
+    children = [int(f.read_text()) for f in pids.iterdir()]
+    assert len(children) == 2
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=60) == 128 + signal.SIGTERM
+    for pid in children:
+        try:
+            os.kill(pid, 0)
+            alive = True
+        except ProcessLookupError:
+            alive = False
+        assert not alive, pid
