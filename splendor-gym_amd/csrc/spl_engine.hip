@@ -1039,6 +1039,38 @@ __device__ __forceinline__ void st_v4(v4i *p, v4i v) {
     else *p = v;
 }
 
+// Cache policy of the NT output stream (the rollout store's per-step rows and masks): >= 0 a buffer store
+// with that cache-policy immediate (gfx950: sc0 = 1, nt = 2, sc1 = 16) on a resource over the block; -1 the
+// compiler's non-temporal store (`global_store_dwordx4 … nt`).  Default 19 = `sc0 nt sc1` (system scope,
+// non-temporal): headline 1 941-1 952 against 1 975-2 002 us per launch with `nt` alone, four alternations
+// on one box, 1.4 % on another; without nt 12 % slower (profiles/r06/store_policy_ab_r06u_v.txt)
+#ifndef SPL_ROLL_CPOL
+#define SPL_ROLL_CPOL 19
+#endif
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+// 16-byte output stores into one wave-uniform block (st_v4, or the buffer-store form of SPL_ROLL_CPOL)
+template <bool NT>
+struct V4Sink {
+    v4i *out;
+#if SPL_ROLL_CPOL >= 0
+    __amdgpu_buffer_rsrc_t rs;
+#endif
+    __device__ __forceinline__ explicit V4Sink(void *p) : out(reinterpret_cast<v4i *>(p)) {
+#if SPL_ROLL_CPOL >= 0
+        if (NT) rs = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, 0x7FFFFFF0, 0x00020000);
+#endif
+    }
+    __device__ __forceinline__ void put(int i, v4i v) const {
+#if SPL_ROLL_CPOL >= 0
+        if (NT) {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs, i * 16, 0, SPL_ROLL_CPOL);
+            return;
+        }
+#endif
+        st_v4<NT>(out + i, v);
+    }
+};
+
 __device__ __forceinline__ v4i expand4(uint32_t w) {
     v4i v = {(int)(w & 0xFFu), (int)((w >> 8) & 0xFFu), (int)((w >> 16) & 0xFFu), (int)(w >> 24)};
     return v;
@@ -1048,7 +1080,7 @@ __device__ __forceinline__ v4i expand4(uint32_t w) {
 template <bool NT = false>
 __device__ __forceinline__ void store_obs_range(const uint8_t *rows_lds, int32_t *dst, int d0, int d1) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
-    v4i *out = reinterpret_cast<v4i *>(dst);
+    const V4Sink<NT> out(dst);
     constexpr int U = 5;
     int d = d0 + lane_id();
 #pragma unroll 1
@@ -1057,14 +1089,14 @@ __device__ __forceinline__ void store_obs_range(const uint8_t *rows_lds, int32_t
 #pragma unroll
         for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
 #pragma unroll
-        for (int u = 0; u < U; ++u) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
+        for (int u = 0; u < U; ++u) out.put(d + 64 * u, expand4(w[u]));
     }
     uint32_t w[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) w[u] = (d + 64 * u < d1) ? src[d + 64 * u] : 0u;
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        if (d + 64 * u < d1) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
+        if (d + 64 * u < d1) out.put(d + 64 * u, expand4(w[u]));
 }
 constexpr int kObsBlockWords = 64 * kObsDim / 4;  // 4752 LDS words = 4752 16-byte stores per wave
 constexpr int kObsSplit = 64 * 5 * 7;             // 2240: 35 stores per lane in the first part
@@ -1077,7 +1109,7 @@ __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int row
     const int nbytes = rows * kObsDim;
     const int full = nbytes >> 2;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
-    v4i *out = reinterpret_cast<v4i *>(dst);
+    const V4Sink<NT> out(dst);
     constexpr int U = 5;
     int d = lane_id();
     if (rows == R) {  // every wave but a ragged last one: compile-time trip count
@@ -1088,17 +1120,17 @@ __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int row
 #pragma unroll
             for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
 #pragma unroll
-            for (int u = 0; u < U; ++u) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
+            for (int u = 0; u < U; ++u) out.put(d + 64 * u, expand4(w[u]));
         }
         uint32_t w[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) w[u] = (d + 64 * u < kFull) ? src[d + 64 * u] : 0u;
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (d + 64 * u < kFull) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
+            if (d + 64 * u < kFull) out.put(d + 64 * u, expand4(w[u]));
         return;
     }
-    for (; d < full; d += 64) st_v4<NT>(out + d, expand4(src[d]));
+    for (; d < full; d += 64) out.put(d, expand4(src[d]));
     for (int b = (full << 2) + lane_id(); b < nbytes; b += 64) dst[b] = (int32_t)rows_lds[b];
 }
 
@@ -1112,7 +1144,7 @@ __device__ __forceinline__ void store_obs_block_mid(const uint8_t *rows_lds, int
         return;
     }
     const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
-    v4i *out = reinterpret_cast<v4i *>(dst);
+    const V4Sink<NT> out(dst);
     constexpr int U = 5, kFull = 64 * kObsDim / 4, kIters = kFull / (64 * U);  // 4752 = 14 x 320 + 272
     int d = lane_id();
 #pragma unroll 1
@@ -1121,7 +1153,7 @@ __device__ __forceinline__ void store_obs_block_mid(const uint8_t *rows_lds, int
 #pragma unroll
         for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
 #pragma unroll
-        for (int u = 0; u < U; ++u) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
+        for (int u = 0; u < U; ++u) out.put(d + 64 * u, expand4(w[u]));
     }
     __asm__ volatile("" ::: "memory");
     mid();
@@ -1132,14 +1164,14 @@ __device__ __forceinline__ void store_obs_block_mid(const uint8_t *rows_lds, int
 #pragma unroll
         for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
 #pragma unroll
-        for (int u = 0; u < U; ++u) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
+        for (int u = 0; u < U; ++u) out.put(d + 64 * u, expand4(w[u]));
     }
     uint32_t w[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) w[u] = (d + 64 * u < kFull) ? src[d + 64 * u] : 0u;
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        if (d + 64 * u < kFull) st_v4<NT>(out + d + 64 * u, expand4(w[u]));
+        if (d + 64 * u < kFull) out.put(d + 64 * u, expand4(w[u]));
 }
 
 // Block store of `rows` compact rows (300 bytes each) staged in LDS to dst (16-byte aligned).
@@ -1219,14 +1251,14 @@ __device__ __forceinline__ void store_mask_block(const uint64_t *mask, uint32_t 
     }
     wave_lds_sync();
     if ((rows == 64 || rows == 32) && ((uintptr_t)dst & 15u) == 0) {  // 180 (90) x 16 B
-        v4i *out4 = reinterpret_cast<v4i *>(dst);
+        const V4Sink<NT> out4(dst);
         const int nc = rows * 45 / 16;
         for (int c = lane_id(); c < nc; c += 64) {
             const uint32_t half = (mbits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;  // stream bits 16c..16c+15
             v4i v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = (int)((((half >> (4 * q)) & 0xFu) * 0x00204081u) & 0x01010101u);
-            st_v4<NT>(out4 + c, v);
+            out4.put(c, v);
         }
         return;
     }
