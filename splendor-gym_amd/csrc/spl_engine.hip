@@ -217,6 +217,13 @@ __device__ __forceinline__ int wg_block() { return wg_block_of(blockIdx.x); }
 #ifndef SPL_STEP_OBS_NT
 #define SPL_STEP_OBS_NT false  // k_step_ws observation stores non-temporal (A/B switch)
 #endif
+// k_step_wst (at most two workgroups per CU) stores its int32 rows through the NT output stream
+// (SPL_ROLL_CPOL's sc0 nt sc1): per step 17.1 -> 16.0 us at 32 768 tables, 14.8 -> 12.8 at 16 384,
+// 12.7 -> 12.2 at 4 096 (profiles/r06/step_tail_store_ab_r06y.txt), where at 65 536 tables (k_step_ws)
+// non-temporal rows cost 22.4 -> 23.8 us (profiles/r06/step_store_policy_ab_r06x.txt)
+#ifndef SPL_STEP_TAIL_NT
+#define SPL_STEP_TAIL_NT true
+#endif
 #ifndef SPL_WS_PRIO
 #define SPL_WS_PRIO 1
 #endif
@@ -2502,7 +2509,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
             } else if (kOMask) {
                 store_obs_block_mid<SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim, mask_now);
             } else {
-                store_obs_block<64, SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
+                store_obs_block<64, kStepTail ? SPL_STEP_TAIL_NT : SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
             }
             if (S.obs_u8)  // both outputs: the compact copy of the same rows (a fused actor's input)
                 store_u8_from_rows(L.rows, rows, S.obs_u8 + (size_t)t0 * kObsU8, valid ? (uint32_t)get_moves(T.sw) >> 8 : 0u);
