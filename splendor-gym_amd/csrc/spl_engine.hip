@@ -224,6 +224,17 @@ __device__ __forceinline__ int wg_block() { return wg_block_of(blockIdx.x); }
 #ifndef SPL_STEP_TAIL_NT
 #define SPL_STEP_TAIL_NT true
 #endif
+// A/B switch: k_step_ws stores the first (1) or second (2) half of its row block through the NT output
+// stream and the other half plain (0: all plain)
+#ifndef SPL_STEP_WS_SPLIT
+#define SPL_STEP_WS_SPLIT 0
+#endif
+#ifndef SPL_STEP_BOTH_NT
+#define SPL_STEP_BOTH_NT 0
+#endif
+struct NoOp {
+    __device__ __forceinline__ void operator()() const {}
+};
 #ifndef SPL_WS_PRIO
 #define SPL_WS_PRIO 1
 #endif
@@ -1143,7 +1154,7 @@ __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int row
 
 // store_obs_block (64 rows) with `mid()` issued between its first and second half: work that fills the
 // wave's store-issue stalls instead of following the whole block (k_step_wso's legal mask)
-template <bool NT, class Mid>
+template <bool NT, class Mid, bool NT2 = NT>
 __device__ __forceinline__ void store_obs_block_mid(const uint8_t *rows_lds, int rows, int32_t *dst, Mid mid) {
     if (rows != 64) {
         mid();
@@ -1152,6 +1163,7 @@ __device__ __forceinline__ void store_obs_block_mid(const uint8_t *rows_lds, int
     }
     const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
     const V4Sink<NT> out(dst);
+    const V4Sink<NT2> out2(dst);  // the second half (and the tail) may take another store policy
     constexpr int U = 5, kFull = 64 * kObsDim / 4, kIters = kFull / (64 * U);  // 4752 = 14 x 320 + 272
     int d = lane_id();
 #pragma unroll 1
@@ -1171,14 +1183,14 @@ __device__ __forceinline__ void store_obs_block_mid(const uint8_t *rows_lds, int
 #pragma unroll
         for (int u = 0; u < U; ++u) w[u] = src[d + 64 * u];
 #pragma unroll
-        for (int u = 0; u < U; ++u) out.put(d + 64 * u, expand4(w[u]));
+        for (int u = 0; u < U; ++u) out2.put(d + 64 * u, expand4(w[u]));
     }
     uint32_t w[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) w[u] = (d + 64 * u < kFull) ? src[d + 64 * u] : 0u;
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        if (d + 64 * u < kFull) out.put(d + 64 * u, expand4(w[u]));
+        if (d + 64 * u < kFull) out2.put(d + 64 * u, expand4(w[u]));
 }
 
 // Block store of `rows` compact rows (300 bytes each) staged in LDS to dst (16-byte aligned).
@@ -2508,6 +2520,11 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
                 if (kOMask) mask_now();
             } else if (kOMask) {
                 store_obs_block_mid<SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim, mask_now);
+            } else if (!kStepTail && SPL_STEP_BOTH_NT && S.obs_u8) {  // A/B: with the compact copy (the dual step's
+                // opponent step, whose int32 rows go back to the caller and are not read on the device) as NT rows
+                store_obs_block<64, true>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
+            } else if (!kStepTail && SPL_STEP_WS_SPLIT != 0) {  // A/B: half the block NT (SPL_ROLL_CPOL), half plain
+                store_obs_block_mid<SPL_STEP_WS_SPLIT == 1, NoOp, SPL_STEP_WS_SPLIT == 2>(L.rows, rows, S.obs + (size_t)t0 * kObsDim, NoOp());
             } else {
                 store_obs_block<64, kStepTail ? SPL_STEP_TAIL_NT : SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
             }
