@@ -91,10 +91,11 @@ PRECISION_DTYPE = {
 NET_FP32_FLOP = 2 * (297 * 256 + 256 * 256 + 256 * 45 + 297 * 256 + 256 * 256 + 256)
 ROLLOUT_K = 128    # env steps per spl_rollout launch = ppo_splendor.py's --num-steps default (:71)
 MIN_TIMED_LAUNCHES = 8  # rollout mode times at least this many launches (>= 16 ms), whatever --steps says
+MIN_TIMED_REPLAYS = 4   # step mode (hipGraphs) times at least this many replays of a full graph (~12 ms)
 
 
 def step_plan(mode, steps, warmup, refill_period, rollout_k=ROLLOUT_K, graph_steps=128,
-              min_launches=MIN_TIMED_LAUNCHES):
+              min_launches=MIN_TIMED_LAUNCHES, min_replays=MIN_TIMED_REPLAYS):
     """Turn the requested --steps/--warmup into what is actually run.
 
     unit   = lcm(2 launches, refill period): the two action buffers alternate per launch, and a
@@ -102,7 +103,9 @@ def step_plan(mode, steps, warmup, refill_period, rollout_k=ROLLOUT_K, graph_ste
              the arena's step counter, which the graph bakes in).
     K      = steps timed    = --steps rounded up to whole units (>= 1 unit), and to at least
              `min_launches` launches in rollout mode (the driver's --steps 20 would otherwise time
-             two ~2 ms launches, where one box's jitter moves the figure by several percent)
+             two ~2 ms launches, where one box's jitter moves the figure by several percent) and to
+             at least `min_replays` full graphs in step mode (one ~1.5 ms replay let a single stall
+             move the figure by half)
     W      = warm-up steps  = --warmup rounded up to whole units (>= 1 unit: one full launch + a
              refill cycle, whatever --warmup says)
     G      = steps per captured graph (step mode only; 0 = eager launches): the largest multiple
@@ -124,6 +127,7 @@ def step_plan(mode, steps, warmup, refill_period, rollout_k=ROLLOUT_K, graph_ste
     g = 0
     if mode == "step" and graph_steps and graph_steps > 0:
         cap = max(int(graph_steps), unit)
+        k = max(k, int(min_replays) * (cap // unit) * unit)
         g = unit
         m = unit
         while m <= min(cap, k):
@@ -795,6 +799,10 @@ def main():
             except Exception as exc:  # capture unsupported: time eager launches instead
                 print(f"graph capture failed ({exc}); timing eager launches", file=sys.stderr)
                 graph, G = None, 0
+        warm_replays = 0
+        if graph is not None:  # one untimed replay: the graph's first launch is not part of the measurement
+            graph.replay()
+            warm_replays = 1
         torch.cuda.synchronize(dev)
         eps0 = int(ep_cnt.sum().item())
         barrier(dev)
@@ -826,7 +834,7 @@ def main():
               f"{(t_enq - t0) * 1e3:.3f} ms), GPU span first->last event {span * 1e3:.3f} ms", file=sys.stderr)
         terminations = int(ep_cnt.sum().item()) - eps0
         kt = "HIP events around each launch in the timed region"
-        k_next = k_base + W + K + 1
+        k_next = k_base + W + warm_replays * G + K + 1
         eager_s = None
         if graph is not None:
             # ROCm rejects timing events as graph nodes ("External events are disallowed"), so the

@@ -41,8 +41,8 @@ def test_driver_command_values():
     assert (p["K"], p["W"], p["launches"]) == (1024, 256, 8)
     p64 = bench.step_plan("rollout", 20, 5, 64, rollout_k=64)
     assert (p64["K"], p64["W"], p64["launches"]) == (512, 128, 8)
-    s = bench.step_plan("step", 20, 5, 64)
-    assert (s["K"], s["W"], s["G"]) == (64, 64, 64)
+    s = bench.step_plan("step", 20, 5, 64)  # at least four replays of a full 128-step graph
+    assert (s["K"], s["W"], s["G"]) == (512, 64, 128) and s["K"] // s["G"] == bench.MIN_TIMED_REPLAYS
 
 
 def test_eager_step_plan_and_disabled_refill():
