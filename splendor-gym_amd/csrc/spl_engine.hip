@@ -2324,10 +2324,11 @@ __device__ __forceinline__ void ws_sync() {
 // and the legal-mask cache entry off the rules wave's tail; hand-off 2 (rules -> output: row halves
 // staged) becomes an LDS counter, so the tail wave never waits on the other two after hand-off 1.
 // Without it (k_step_ws_<P>p, round 5's two waves) the rules wave evaluates the mask after hand-off 2.
-// Same outputs either way.  Measured alternating on one box (profiles/r06/stepab_r06g.txt, graph
+// Same outputs either way.  Measured alternating on one box (profiles/r06/stepab_r06g_h.txt, graph
 // events per step): 16 384 tables 17.4 -> 14.7 us with the tail wave; 65 536 tables 22.4 -> 22.9 us
 // (four workgroups per CU: 12 waves share the SIMDs and the LDS) — so spl_step picks it by grid size
-// (spl_ctx_set_step_tail: auto = at most ctx->step_tail_blocks workgroups).
+// (spl_ctx_set_step_tail: auto = at most ctx->step_tail_blocks workgroups).  Its rows leave as sc0 nt sc1
+// stores (SPL_STEP_TAIL_NT): 14.8 -> 12.8 us at 16 384 tables.
 
 template <int P>
 struct __align__(16) StepWsLDS : Consts {
