@@ -662,8 +662,8 @@ def main():
                          "taking it between its row stores; same results")
     ap.add_argument("--partner-lead", type=int, default=None,
                     help="rollout store (six-wave dealer and quad kernels): a team this many steps behind its "
-                         "neighbouring-XCC partner hands it whole steps of rows (library default: 4 in the six-wave "
-                         "dealer, 0 = off in the quad kernel; 0 = off, -1 = whenever a slot is free)")
+                         "neighbouring-XCC partner hands it whole steps of rows (library default 0 = off; "
+                         "-1 = whenever a slot is free)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args.gpus, sys.argv[1:]))

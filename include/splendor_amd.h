@@ -175,9 +175,9 @@ int spl_ctx_set_rollout_delegation(spl_ctx_t *ctx, int every);
  * workgroup on the neighbouring XCC hands whole steps of observation rows (its state words, ~6 KB) to
  * that team's output wave, which encodes and stores them between its own steps (the XCCs drain the
  * rollout store at different rates under load).  0 = off, -1 = hand off whenever a slot
- * is free (tests).  Other kernels ignore it.  Defaults (until this is called): 4 in the six-wave dealer,
- * 0 (off) in the quad variant (round 6: with its sc0 nt sc1 row stores the teams lag little and the
- * hand-off no longer pays; DESIGN.md §4.1 gives the measured A/B).  Results are identical either way. */
+ * is free (tests).  Other kernels ignore it.  Default 0 = off (round 6: with the sc0 nt sc1 row stores
+ * the teams lag little and the hand-off no longer pays; DESIGN.md §4.1 gives the measured A/B).
+ * Results are identical either way. */
 int spl_ctx_set_partner_lead(spl_ctx_t *ctx, int lead);
 /* spl_step's kernel shape (round 6): 0 = two waves (k_step_ws_<P>p: the rules wave evaluates the new
  * state's legal mask after the row halves), 1 = three waves per 64 tables (k_step_wst_<P>p: a TAIL wave

@@ -188,25 +188,15 @@ constexpr int kScratchStride = SPL_SCRATCH_STRIDE;
 #define SPL_DELEG_EVERY 0
 #endif
 #ifndef SPL_PARTNER_LEAD
-// partner hand-off of the six-wave dealer's rollout store (spl_ctx_set_partner_lead): a team hands a
-// step's rows to its neighbouring-XCC partner when that one is this many steps ahead.  With the flag
-// words polled by the dealer wave (it issues no row stores) and arms alternating on one box: C4 median
-// launch 1 081-1 084 (lead 4) / 1 076-1 080 (lead 2) vs 1 098-1 104 us off
-// (profiles/r04/partner_ab_r04u.txt).  Polled by the output wave itself the hand-off was slower than
-// off (partner_ab_r04n.txt).  Round 5: the two-wave kernels (the headline) have no partner hand-off —
-// at four workgroups per CU their sc1-load consumer was outside the guide's measured cross-XCD
-// envelope, and it bought 1.2-1.6 %; the six-wave dealer runs ONE workgroup per CU,
-// the guide's first measured row.
-#define SPL_PARTNER_LEAD 4
-#endif
-#ifndef SPL_QUAD_PARTNER_LEAD
-// the quad kernel's default lead: 0 (off) since its rows leave as sc0 nt sc1 stores (SPL_ROLL_CPOL) — the
-// teams then lag far less (~7 500 instead of ~43 000 of 131 072 team-steps handed off per launch at lead
-// 4) and the hand-off's polls cost more than it recovers: lead 0 / 4 / 8 1 873-1 898 / 1 909-1 925 /
-// 1 912-1 913 us per launch, arms alternating on one box (profiles/r06/quad_lead_ab_r06ad.txt).  Before
-// the store policy lead 4 paid 2.4 % (profiles/r06/headab_r06d.txt).  spl_ctx_set_partner_lead overrides
-// both defaults.
-#define SPL_QUAD_PARTNER_LEAD 0
+// partner hand-off of the one-workgroup-per-CU rollout stores (six-wave dealer, quad; spl_ctx_set_partner_lead):
+// a team hands a step's rows to its neighbouring-XCC partner when that one is this many steps ahead.
+// Default 0 (off) since round 6's sc0 nt sc1 row stores (SPL_ROLL_CPOL): the teams then lag far less and
+// the polls cost more than the hand-off recovers — quad lead 0 / 4 / 8: 1 873-1 898 / 1 909-1 925 /
+// 1 912-1 913 us per launch (another box: lead 0 / 4 1 863-1 873 / 1 892-1 900,
+// profiles/r06/quad_lead_ab_r06ad.txt); six-wave dealer (C4) 1 075-1 078 / 1 081-1 100 / 1 083-1 102
+// (profiles/r06/c4_lead_ab_r06ag.txt).  With nt-only stores lead 4 had paid 2.4 % (headline,
+// profiles/r06/headab_r06d.txt) and ~2 % (C4, profiles/r04/partner_ab_r04u.txt).
+#define SPL_PARTNER_LEAD 0
 #endif
 #ifndef SPL_XCD_MAP
 #define SPL_XCD_MAP 1
@@ -4024,7 +4014,6 @@ __global__ __launch_bounds__(64) void k_upload(KArena A, int first, int count, c
 // ==========================================================================================
 using namespace spl;
 
-constexpr int kLeadDefault = -1000;  // spl_ctx_t::partner_lead before spl_ctx_set_partner_lead: each kernel's own default
 struct spl_ctx_s {
     int device;
     uint4 *cards;
@@ -4038,7 +4027,7 @@ struct spl_ctx_s {
     int dealer2_resident[5]; // k_rollout_store_dealer2_<P>p: the same for the six-wave dealer variant
     int quad_resident[5];    // k_rollout_store_quad_<P>p: the same for the quad variant
     int deleg_every;     // spl_rollout per-step store: rollout-store delegation every n-th step (0 = off)
-    int partner_lead;    // per-step store partner hand-off lead in steps (0 off, -1 forced; kLeadDefault: per kernel)
+    int partner_lead;    // per-step store partner hand-off lead in steps (0 off, < 0 forced)
     uint32_t mtag;         // legal-mask cache tag of this context's card table (card_table_tag), 1..65535, or 0
     int step_tail;         // spl_step shape: -1 auto (the tail wave up to step_tail_blocks workgroups), 0 two waves, 1 three
     int64_t step_tail_blocks;
@@ -4252,7 +4241,7 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     c->refill_period = 64;
     c->refill_fused = 1;
     c->deleg_every = SPL_DELEG_EVERY;
-    c->partner_lead = kLeadDefault;  // SPL_PARTNER_LEAD in the six-wave dealer, SPL_QUAD_PARTNER_LEAD in the quad kernel
+    c->partner_lead = SPL_PARTNER_LEAD;
     c->step_tail = -1;
     {
         int cus = 0;
@@ -4608,11 +4597,8 @@ int spl_rollout(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, in
     const int deleg = ((int64_t)blocks_for(arena->n) <= resident && ctx->deleg_every > 0) ? ctx->deleg_every : 0;
     // the six-wave dealer's partner lead, likewise 0 unless every workgroup is resident (ADVICE r04:
     // pipeline "dealer2" forced on a larger grid)
-    const bool dflt = ctx->partner_lead == kLeadDefault;
-    const int lead2 = (int64_t)((arena->n + 127) / 128) <= ctx->dealer2_resident[arena->players]
-                          ? (dflt ? SPL_PARTNER_LEAD : ctx->partner_lead) : 0;
-    const int lead4 = (int64_t)((arena->n + 255) / 256) <= ctx->quad_resident[arena->players]
-                          ? (dflt ? SPL_QUAD_PARTNER_LEAD : ctx->partner_lead) : 0;
+    const int lead2 = (int64_t)((arena->n + 127) / 128) <= ctx->dealer2_resident[arena->players] ? ctx->partner_lead : 0;
+    const int lead4 = (int64_t)((arena->n + 255) / 256) <= ctx->quad_resident[arena->players] ? ctx->partner_lead : 0;
 #define SPL_LAUNCH_WS(TPW, BLOCKS)                                                                           \
     DISPATCH_P(arena->players, if (p_out) {                                                                  \
         hipLaunchKernelGGL((RolloutKernel<PP, TPW, true>::fn), dim3(BLOCKS), dim3(128), 0, s, A, ktables(ctx), S, \
