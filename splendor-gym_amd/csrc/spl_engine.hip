@@ -1064,6 +1064,11 @@ __device__ __forceinline__ void st_v4(v4i *p, v4i v) {
 #ifndef SPL_ROLL_CPOL
 #define SPL_ROLL_CPOL 19
 #endif
+// A/B switch: the rollout store's terminal rows and small outputs (reward, terminated, flags, winner)
+// through the same policy (0: plain stores)
+#ifndef SPL_ROLL_SMALL_NT
+#define SPL_ROLL_SMALL_NT 0
+#endif
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 // 16-byte output stores into one wave-uniform block (st_v4, or the buffer-store form of SPL_ROLL_CPOL)
 template <bool NT>
@@ -1917,6 +1922,23 @@ __device__ __forceinline__ void store_row_columns(const uint32_t *st, int stride
         const int e = lane_id() + 64 * i;
         if (e < kObsDim) dst[e] = (int32_t)v[i];
     }
+}
+// the same through the NT output stream's cache policy (SPL_ROLL_CPOL; dst wave-uniform)
+template <int P>
+__device__ __forceinline__ void store_row_columns_nt(const uint32_t *st, int stride, const Consts &L, const ColRecipes &C,
+                                                     int32_t *dst) {
+#if SPL_ROLL_CPOL >= 0
+    uint32_t v[5];
+    row_columns<P>(st, stride, L, C, v);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, kObsDim * 4, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const int e = lane_id() + 64 * i;
+        if (e < kObsDim) __builtin_amdgcn_raw_buffer_store_b32(v[i], rs, e * 4, 0, SPL_ROLL_CPOL);
+    }
+#else
+    store_row_columns<P>(st, stride, L, C, dst);
+#endif
 }
 // spl_step_args_t.gate_*: the dual step's opponent moves only where the agent's move was applied
 // and left the game running (wrappers/dual_step_native.py:120-140, spl_dual_gate); elsewhere its
@@ -3339,7 +3361,10 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 int32_t *fobs = S.final_obs + blk * kObsDim;
                 for (int idx = 0; fin; fin &= fin - 1, ++idx) {
                     const int r = __ffsll((unsigned long long)fin) - 1;
-                    store_row_columns<P>(&L.tst[b][idx][0], 1, L, crc, fobs + (size_t)(t0 + r) * kObsDim);
+                    if constexpr (per_step && SPL_ROLL_SMALL_NT)
+                        store_row_columns_nt<P>(&L.tst[b][idx][0], 1, L, crc, fobs + (size_t)(t0 + r) * kObsDim);
+                    else
+                        store_row_columns<P>(&L.tst[b][idx][0], 1, L, crc, fobs + (size_t)(t0 + r) * kObsDim);
                 }
             }
             const bool big_moves = __any(valid && get_moves(T.sw) > 255);
@@ -3394,11 +3419,30 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 store_mask_block<false>(L.mask[b], L.mbits, rows, S.mask + blk * 45 + (size_t)t0 * 45);
             }
             const uint32_t sm = L.small[b][lane];
+            if constexpr (per_step && SPL_ROLL_SMALL_NT && SPL_ROLL_CPOL >= 0) {  // A/B: the NT stream's policy
+                const size_t o = blk + (size_t)t0;  // this wave's 64 tables of step k (wave-uniform)
+                const auto rsr = __builtin_amdgcn_make_buffer_rsrc(S.reward + o, (short)0, 256, 0x00020000);
+                const auto rst = __builtin_amdgcn_make_buffer_rsrc(S.terminated + o, (short)0, 64, 0x00020000);
+                const auto rsf = __builtin_amdgcn_make_buffer_rsrc(S.flags + o, (short)0, 64, 0x00020000);
+                if (sm & (1u << 9)) {
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, reward_of_code((sm >> 13) & 7u)), rsr,
+                                                          (t - t0) * 4, 0, SPL_ROLL_CPOL);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((sm >> 8) & 1u), rst, t - t0, 0, SPL_ROLL_CPOL);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(sm & 0xFFu), rsf, t - t0, 0, SPL_ROLL_CPOL);
+                }
+                if (S.winner) {
+                    const auto rsw = __builtin_amdgcn_make_buffer_rsrc(S.winner + o, (short)0, 64, 0x00020000);
+                    if (sm & (1u << 9))
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)((int)((sm >> 10) & 7u) - 1), rsw, t - t0, 0, SPL_ROLL_CPOL);
+                }
+            }
             if (sm & (1u << 9)) {  // valid lane: the rules wave's small outputs and episode statistics
-                S.reward[blk + t] = reward_of_code((sm >> 13) & 7u);
-                S.terminated[blk + t] = (uint8_t)((sm >> 8) & 1u);
-                S.flags[blk + t] = (uint8_t)(sm & 0xFFu);
-                if (S.winner) S.winner[blk + t] = (int8_t)((int)((sm >> 10) & 7u) - 1);
+                if constexpr (!(per_step && SPL_ROLL_SMALL_NT && SPL_ROLL_CPOL >= 0)) {
+                    S.reward[blk + t] = reward_of_code((sm >> 13) & 7u);
+                    S.terminated[blk + t] = (uint8_t)((sm >> 8) & 1u);
+                    S.flags[blk + t] = (uint8_t)(sm & 0xFFu);
+                    if (S.winner) S.winner[blk + t] = (int8_t)((int)((sm >> 10) & 7u) - 1);
+                }
                 if (sm & (1u << 18)) {  // same per-table order and float rounding as k_step
                     if (S.ep_return) unsafeAtomicAdd(&S.ep_return[t], ep_of_code((sm >> 16) & 3u));
                     if (S.ep_count) atomicAdd(&S.ep_count[t], 1u);
