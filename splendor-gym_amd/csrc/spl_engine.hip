@@ -3437,7 +3437,7 @@ __device__ __forceinline__ void rollout_ws(LdsT &L, KArena A, KTables Tb, KStep 
                 }
             }
             if (sm & (1u << 9)) {  // valid lane: the rules wave's small outputs and episode statistics
-                if constexpr (!(per_step && SPL_ROLL_SMALL_NT && SPL_ROLL_CPOL >= 0)) {
+                if constexpr (!(per_step && SPL_ROLL_SMALL_NT && SPL_ROLL_CPOL >= 0) && !(SPL_ABL & ABL_SMALL_OUT)) {
                     S.reward[blk + t] = reward_of_code((sm >> 13) & 7u);
                     S.terminated[blk + t] = (uint8_t)((sm >> 8) & 1u);
                     S.flags[blk + t] = (uint8_t)(sm & 0xFFu);
