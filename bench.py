@@ -583,13 +583,13 @@ STEP_SHAPE_SUFFIX = {0: "ws", 1: "wst", 2: "wso"}
 
 def step_shape(mode, tables, cus=None):
     """spl_step's kernel shape for `tables` tables of full int32 outputs: the forced mode, or the library's
-    auto rule (spl_engine.hip spl_step: three waves up to two 64-table workgroups per CU, else two)."""
+    auto rule (spl_engine.hip spl_step: three waves up to three 64-table workgroups per CU, else two)."""
     if mode != "auto":
         return int(mode)
     if cus is None:
         import torch
         cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    return 1 if -(-int(tables) // 64) <= 2 * int(cus) else 0
+    return 1 if -(-int(tables) // 64) <= 3 * int(cus) else 0
 
 
 def self_launch(n, argv, device_count=None):

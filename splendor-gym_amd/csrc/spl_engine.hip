@@ -216,7 +216,7 @@ __device__ __forceinline__ int wg_block() { return wg_block_of(blockIdx.x); }
 #ifndef SPL_STEP_OBS_NT
 #define SPL_STEP_OBS_NT false  // k_step_ws observation stores non-temporal (A/B switch)
 #endif
-// k_step_wst (at most two workgroups per CU) stores its int32 rows through the NT output stream
+// k_step_wst (at most three workgroups per CU) stores its int32 rows through the NT output stream
 // (SPL_ROLL_CPOL's sc0 nt sc1): per step 17.1 -> 16.0 us at 32 768 tables, 14.8 -> 12.8 at 16 384,
 // 12.7 -> 12.2 at 4 096 (profiles/r06/step_tail_store_ab_r06y.txt), where at 65 536 tables (k_step_ws)
 // non-temporal rows cost 22.4 -> 23.8 us (profiles/r06/step_store_policy_ab_r06x.txt)
@@ -4290,7 +4290,9 @@ int spl_ctx_create(int device, const int32_t *cards, const int32_t *nobles, spl_
     {
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        c->step_tail_blocks = 2 * (int64_t)cus;  // up to two workgroups per CU (32 768 tables on 256 CUs)
+        // up to three workgroups per CU (49 152 tables on 256 CUs): per step 20.0 against 20.45 us there,
+        // 24.2 against 22.35 us at four (profiles/r06/step_shape_48k_64k_r06al.txt)
+        c->step_tail_blocks = 3 * (int64_t)cus;
     }
     c->pipeline = 1;
     memcpy(c->ws_resident, ws_resident, sizeof(ws_resident));
@@ -4532,7 +4534,7 @@ int spl_step(spl_ctx_t *ctx, spl_arena_t *arena, const spl_step_args_t *a, void 
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (kStepWs) {
         const unsigned blocks = blocks_for(arena->n);
-        // auto: the tail wave up to two workgroups per CU, and for compact-only outputs (obs_u8 without the
+        // auto: the tail wave up to three workgroups per CU, and for compact-only outputs (obs_u8 without the
         // int32 rows: a quarter of the row stores, so the rules wave's tail is the longer one)
         const int shape = ctx->step_tail >= 0 ? ctx->step_tail
                                               : (((int64_t)blocks <= ctx->step_tail_blocks || a->obs == nullptr) ? 1 : 0);

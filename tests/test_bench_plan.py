@@ -65,4 +65,5 @@ def test_step_shape_names_follow_the_library_rule():
     two 64-table workgroups per CU, two above; a forced --step-tail wins)."""
     assert bench.step_shape("auto", 65536, cus=256) == 0 and bench.step_shape("auto", 32768, cus=256) == 1
     assert bench.step_shape("auto", 16384, cus=256) == 1 and bench.step_shape("2", 65536, cus=256) == 2
+    assert bench.step_shape("auto", 49152, cus=256) == 1 and bench.step_shape("auto", 49153, cus=256) == 0
     assert [bench.STEP_SHAPE_SUFFIX[i] for i in range(3)] == ["ws", "wst", "wso"]
