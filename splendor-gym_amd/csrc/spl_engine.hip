@@ -223,6 +223,12 @@ __device__ __forceinline__ int wg_block() { return wg_block_of(blockIdx.x); }
 #ifndef SPL_STEP_TAIL_NT
 #define SPL_STEP_TAIL_NT true
 #endif
+// k_step_ws (four workgroups per CU) stores its int32 rows as `sc1` buffer stores (system scope, temporal;
+// -2 = plain): 22.35 -> 20.5 us per step at 65 536 tables; `sc0 sc1` the same, `sc0` alone as plain
+// (profiles/r06/step_ws_temporal_policy_r06an.txt); non-temporal rows were slower there (23.8 us)
+#ifndef SPL_STEP_WS_CPOL
+#define SPL_STEP_WS_CPOL 16
+#endif
 // A/B switch: k_step_ws stores the first (1) or second (2) half of its row block through the NT output
 // stream and the other half plain (0: all plain)
 #ifndef SPL_STEP_WS_SPLIT
@@ -1070,28 +1076,22 @@ __device__ __forceinline__ void st_v4(v4i *p, v4i v) {
 #define SPL_ROLL_SMALL_NT 0
 #endif
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-// 16-byte output stores into one wave-uniform block (st_v4, or the buffer-store form of SPL_ROLL_CPOL)
-template <bool NT>
+// 16-byte output stores into one wave-uniform block under cache policy CP: -2 plain, -1 the compiler's
+// non-temporal store, >= 0 a buffer store with that cache-policy immediate
+template <int CP>
 struct V4Sink {
     v4i *out;
-#if SPL_ROLL_CPOL >= 0
     __amdgpu_buffer_rsrc_t rs;
-#endif
     __device__ __forceinline__ explicit V4Sink(void *p) : out(reinterpret_cast<v4i *>(p)) {
-#if SPL_ROLL_CPOL >= 0
-        if (NT) rs = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, 0x7FFFFFF0, 0x00020000);
-#endif
+        if constexpr (CP >= 0) rs = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, 0x7FFFFFF0, 0x00020000);
     }
     __device__ __forceinline__ void put(int i, v4i v) const {
-#if SPL_ROLL_CPOL >= 0
-        if (NT) {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs, i * 16, 0, SPL_ROLL_CPOL);
-            return;
-        }
-#endif
-        st_v4<NT>(out + i, v);
+        if constexpr (CP >= 0) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), rs, i * 16, 0, CP);
+        else st_v4<CP == -1>(out + i, v);
     }
 };
+// the policy of an output stream: the NT stream (SPL_ROLL_CPOL) or plain stores
+constexpr int stream_cpol(bool nt) { return nt ? SPL_ROLL_CPOL : -2; }
 
 __device__ __forceinline__ v4i expand4(uint32_t w) {
     v4i v = {(int)(w & 0xFFu), (int)((w >> 8) & 0xFFu), (int)((w >> 16) & 0xFFu), (int)(w >> 24)};
@@ -1102,7 +1102,7 @@ __device__ __forceinline__ v4i expand4(uint32_t w) {
 template <bool NT = false>
 __device__ __forceinline__ void store_obs_range(const uint8_t *rows_lds, int32_t *dst, int d0, int d1) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
-    const V4Sink<NT> out(dst);
+    const V4Sink<stream_cpol(NT)> out(dst);
     constexpr int U = 5;
     int d = d0 + lane_id();
 #pragma unroll 1
@@ -1126,12 +1126,12 @@ constexpr int kObsSplit = 64 * 5 * 7;             // 2240: 35 stores per lane in
 // Block store of this wave's observation rows: LDS bytes [rows][297] -> int32 [rows][297] at
 // dst (16-byte aligned: 64-row blocks are 76032 B).  Dword d of the block is LDS word d.
 // R = the workgroup's table count (64, or 32 in the half-populated two-wave rollout).
-template <int R = 64, bool NT = false>
+template <int R = 64, bool NT = false, int CP = stream_cpol(NT)>
 __device__ __forceinline__ void store_obs_block(const uint8_t *rows_lds, int rows, int32_t *dst) {
     const int nbytes = rows * kObsDim;
     const int full = nbytes >> 2;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
-    const V4Sink<NT> out(dst);
+    const V4Sink<CP> out(dst);
     constexpr int U = 5;
     int d = lane_id();
     if (rows == R) {  // every wave but a ragged last one: compile-time trip count
@@ -1166,8 +1166,8 @@ __device__ __forceinline__ void store_obs_block_mid(const uint8_t *rows_lds, int
         return;
     }
     const uint32_t *src = reinterpret_cast<const uint32_t *>(rows_lds);
-    const V4Sink<NT> out(dst);
-    const V4Sink<NT2> out2(dst);  // the second half (and the tail) may take another store policy
+    const V4Sink<stream_cpol(NT)> out(dst);
+    const V4Sink<stream_cpol(NT2)> out2(dst);  // the second half (and the tail) may take another store policy
     constexpr int U = 5, kFull = 64 * kObsDim / 4, kIters = kFull / (64 * U);  // 4752 = 14 x 320 + 272
     int d = lane_id();
 #pragma unroll 1
@@ -1274,7 +1274,7 @@ __device__ __forceinline__ void store_mask_block(const uint64_t *mask, uint32_t 
     }
     wave_lds_sync();
     if ((rows == 64 || rows == 32) && ((uintptr_t)dst & 15u) == 0) {  // 180 (90) x 16 B
-        const V4Sink<NT> out4(dst);
+        const V4Sink<stream_cpol(NT)> out4(dst);
         const int nc = rows * 45 / 16;
         for (int c = lane_id(); c < nc; c += 64) {
             const uint32_t half = (mbits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;  // stream bits 16c..16c+15
@@ -2548,7 +2548,9 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
             } else if (!kStepTail && SPL_STEP_WS_SPLIT != 0) {  // A/B: half the block NT (SPL_ROLL_CPOL), half plain
                 store_obs_block_mid<SPL_STEP_WS_SPLIT == 1, NoOp, SPL_STEP_WS_SPLIT == 2>(L.rows, rows, S.obs + (size_t)t0 * kObsDim, NoOp());
             } else {
-                store_obs_block<64, kStepTail ? SPL_STEP_TAIL_NT : SPL_STEP_OBS_NT>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
+                constexpr int kCp = kStepTail ? stream_cpol(SPL_STEP_TAIL_NT)
+                                              : (SPL_STEP_OBS_NT ? SPL_ROLL_CPOL : SPL_STEP_WS_CPOL);
+                store_obs_block<64, false, kCp>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
             }
             if (S.obs_u8)  // both outputs: the compact copy of the same rows (a fused actor's input)
                 store_u8_from_rows(L.rows, rows, S.obs_u8 + (size_t)t0 * kObsU8, valid ? (uint32_t)get_moves(T.sw) >> 8 : 0u);
