@@ -226,6 +226,12 @@ __device__ __forceinline__ int wg_block() { return wg_block_of(blockIdx.x); }
 // k_step_ws (four workgroups per CU) stores its int32 rows as `sc1` buffer stores (system scope, temporal;
 // -2 = plain): 22.35 -> 20.5 us per step at 65 536 tables; `sc0 sc1` the same, `sc0` alone as plain
 // (profiles/r06/step_ws_temporal_policy_r06an.txt); non-temporal rows were slower there (23.8 us)
+// the three-wave step's row policy (-3: SPL_STEP_TAIL_NT's stream): `sc1` (16), per step 15.98 -> 15.07 us at
+// 32 768 tables, 20.0 -> 18.2 at 49 152, 12.85 -> 12.82 at 16 384 against sc0 nt sc1
+// (profiles/r06/step_tail_sc1_ab_r06ap.txt)
+#ifndef SPL_STEP_TAIL_CPOL
+#define SPL_STEP_TAIL_CPOL 16
+#endif
 #ifndef SPL_STEP_WS_CPOL
 #define SPL_STEP_WS_CPOL 16
 #endif
@@ -2548,7 +2554,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
             } else if (!kStepTail && SPL_STEP_WS_SPLIT != 0) {  // A/B: half the block NT (SPL_ROLL_CPOL), half plain
                 store_obs_block_mid<SPL_STEP_WS_SPLIT == 1, NoOp, SPL_STEP_WS_SPLIT == 2>(L.rows, rows, S.obs + (size_t)t0 * kObsDim, NoOp());
             } else {
-                constexpr int kCp = kStepTail ? stream_cpol(SPL_STEP_TAIL_NT)
+                constexpr int kCp = kStepTail ? (SPL_STEP_TAIL_CPOL != -3 ? SPL_STEP_TAIL_CPOL : stream_cpol(SPL_STEP_TAIL_NT))
                                               : (SPL_STEP_OBS_NT ? SPL_ROLL_CPOL : SPL_STEP_WS_CPOL);
                 store_obs_block<64, false, kCp>(L.rows, rows, S.obs + (size_t)t0 * kObsDim);
             }
