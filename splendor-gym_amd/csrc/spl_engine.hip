@@ -232,6 +232,10 @@ __device__ __forceinline__ int wg_block() { return wg_block_of(blockIdx.x); }
 #ifndef SPL_STEP_TAIL_CPOL
 #define SPL_STEP_TAIL_CPOL 16
 #endif
+// A/B switch: spl_step's mask block store policy (-2 plain)
+#ifndef SPL_STEP_MASK_CPOL
+#define SPL_STEP_MASK_CPOL -2
+#endif
 #ifndef SPL_STEP_WS_CPOL
 #define SPL_STEP_WS_CPOL 16
 #endif
@@ -1265,7 +1269,7 @@ __device__ __forceinline__ void store_u8_from_rows(const uint8_t *rows_lds, int 
 // bits are first laid out as ONE bit stream in LDS (row r at bits 45r..45r+44; each stream
 // dword is cut from at most two rows), so every output dword is one nibble of the stream,
 // spread to 4 bytes by a multiply: bit i of n moves to bit 8i in n * 0x204081.
-template <bool NT = false>
+template <bool NT = false, int CP = stream_cpol(NT)>
 __device__ __forceinline__ void store_mask_block(const uint64_t *mask, uint32_t *mbits, int rows, int8_t *dst) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -1280,7 +1284,7 @@ __device__ __forceinline__ void store_mask_block(const uint64_t *mask, uint32_t 
     }
     wave_lds_sync();
     if ((rows == 64 || rows == 32) && ((uintptr_t)dst & 15u) == 0) {  // 180 (90) x 16 B
-        const V4Sink<stream_cpol(NT)> out4(dst);
+        const V4Sink<CP> out4(dst);
         const int nc = rows * 45 / 16;
         for (int c = lane_id(); c < nc; c += 64) {
             const uint32_t half = (mbits[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;  // stream bits 16c..16c+15
@@ -2492,7 +2496,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
             // masks and small outputs leave from this wave while the output wave streams the rows
             L.mask[lane] = o.mask;
             wave_lds_sync();
-            if (!abl(ABL_MASK_STORE)) store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+            if (!abl(ABL_MASK_STORE)) store_mask_block<false, SPL_STEP_MASK_CPOL>(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
         }
         STAMP(8);
         store_step_info(S, A.n, t, valid, o.flags);
@@ -2565,7 +2569,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         if (kOMask) {  // the mask block, the fused policy's action and the legal-mask cache entry
             L.mask[lane] = m;
             wave_lds_sync();
-            if (!abl(ABL_MASK_STORE)) store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+            if (!abl(ABL_MASK_STORE)) store_mask_block<false, SPL_STEP_MASK_CPOL>(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
             if (valid) {
                 if (S.next_actions) {
                     const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
@@ -2591,7 +2595,7 @@ __device__ __forceinline__ void step_ws(StepWsLDS<P> &L, KArena A, KTables Tb, K
         if (m & kMaskDeferred) m = abl(ABL_LEGAL_POST) ? 0ull : legal_of(T, L);
         L.mask[lane] = m;
         wave_lds_sync();
-        if (!abl(ABL_MASK_STORE)) store_mask_block(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
+        if (!abl(ABL_MASK_STORE)) store_mask_block<false, SPL_STEP_MASK_CPOL>(L.mask, L.mbits, rows, S.mask + (size_t)t0 * 45);
         if (valid) {
             if (S.next_actions) {
                 const uint64_t ply = S.ply + (S.ply_base ? *S.ply_base : 0ull);
